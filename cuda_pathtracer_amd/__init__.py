@@ -1,0 +1,16 @@
+"""MI355X-native Monte-Carlo path tracer (drop-in for the render loop of sgong-0224/CUDA_Pathtracer).
+
+The hot path (ray generation, intersection, shading, stream compaction) is hand-written HIP for
+gfx950 in csrc/, exported through the C ABI in include/pt_amd.h and include/sc_amd.h and bound
+here with ctypes.  There is no CPU fallback: importing works without the shared object, but every
+entry point raises NativeLibraryError if libpt_amd.so is missing.
+"""
+from ._native import LIB_PATH, NativeLibraryError, PtError, lib  # noqa: F401
+from .pathtrace import (  # noqa: F401
+    CUBE, MESH, SPHERE, GuiDataContainer, InitDataContainer, PathTracer, Scene, pathtrace, pathtraceFree,
+    pathtraceInit, render, save_image, tonemap)
+from .stream_compaction import Efficient, compact_device, partition_device, scan_device  # noqa: F401
+
+__all__ = ["Scene", "PathTracer", "GuiDataContainer", "Efficient", "scan_device", "compact_device",
+           "partition_device", "render", "save_image", "tonemap", "pathtraceInit", "pathtraceFree", "pathtrace",
+           "InitDataContainer", "lib", "LIB_PATH", "NativeLibraryError", "PtError"]

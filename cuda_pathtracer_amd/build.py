@@ -1,0 +1,88 @@
+"""In-tree build of the native library (libpt_amd.so, gfx950) and the CPU test oracle.
+
+Everything is compiled with plain hipcc / g++ command lines (no cmake, no JIT cache) so the
+shared objects sit next to the sources and travel to the GPU box with the repository snapshot.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+ROOT = PKG.parent
+CSRC = PKG / "csrc"
+LIB = PKG / "libpt_amd.so"
+CLI = PKG / "pathtracer_amd"
+ORACLE_DIR = ROOT / "oracle"
+ORACLE_LIB = ORACLE_DIR / "build" / "liboracle.so"
+
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+# -ffp-contract=off: the evaluation contract — every multiply-add is two
+# correctly-rounded operations unless the source writes fmaf(); keeps GPU == oracle bitwise.
+COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall", "-Wno-unused-function"]
+DEVICE_SRCS = ["sc_kernels.hip", "pt_kernels.hip"]
+HOST_SRCS = ["pt_scene.cpp", "pt_mesh.cpp", "pt_image.cpp"]
+
+
+def _run(cmd: list[str], verbose: bool) -> None:
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        sys.stderr.write(res.stdout + res.stderr)
+        raise RuntimeError(f"build step failed: {' '.join(cmd[:4])} ... ({res.returncode})")
+
+
+def _stale(target: Path, deps: list[Path]) -> bool:
+    if not target.exists():
+        return True
+    t = target.stat().st_mtime
+    return any(d.stat().st_mtime > t for d in deps)
+
+
+def build_native(verbose: bool = False, force: bool = False) -> Path:
+    objdir = PKG / "build"
+    objdir.mkdir(exist_ok=True)
+    headers = list(CSRC.glob("*.h")) + list((ROOT / "include").glob("*.h"))
+    jobs = []
+    objs = []
+    for src in DEVICE_SRCS + HOST_SRCS:
+        s = CSRC / src
+        o = objdir / (src + ".o")
+        objs.append(o)
+        if force or _stale(o, [s] + headers):
+            lang = ["-x", "hip", f"--offload-arch={ARCH}"] if src.endswith(".hip") else []
+            jobs.append([HIPCC, *lang, *COMMON, "-I", str(ROOT / "include"), "-c", str(s), "-o", str(o)])
+    with cf.ThreadPoolExecutor(max_workers=min(8, max(1, len(jobs)))) as ex:
+        list(ex.map(lambda c: _run(c, verbose), jobs))
+    if force or jobs or _stale(LIB, objs):
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(LIB), *map(str, objs), "-lz"], verbose)
+    cli_src = CSRC / "pt_cli.cpp"
+    if cli_src.exists() and (force or _stale(CLI, [cli_src, LIB] + headers)):
+        _run([HIPCC, *COMMON, "-I", str(ROOT / "include"), str(cli_src), "-o", str(CLI), "-L", str(PKG),
+              "-lpt_amd", f"-Wl,-rpath,$ORIGIN"], verbose)
+    return LIB
+
+
+def build_oracle(verbose: bool = False, force: bool = False) -> Path:
+    """The CPU checker (test infrastructure only): serial g++ build, no FMA contraction."""
+    srcs = [ORACLE_DIR / "sc_oracle.cpp", ORACLE_DIR / "pt_oracle.cpp"]
+    ORACLE_LIB.parent.mkdir(exist_ok=True)
+    if force or _stale(ORACLE_LIB, srcs):
+        _run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-fno-fast-math",
+              "-o", str(ORACLE_LIB), *map(str, srcs)], verbose)
+    return ORACLE_LIB
+
+
+def build_all(verbose: bool = False, force: bool = False) -> None:
+    build_native(verbose, force)
+    build_oracle(verbose, force)
+
+
+if __name__ == "__main__":
+    build_all(verbose="-v" in sys.argv, force="-f" in sys.argv)
+    print(LIB)

@@ -1,0 +1,144 @@
+// Device-side math for the MI355X path tracer (gfx950, wave64).
+//
+// Evaluation contract: this file is compiled with -ffp-contract=off, so every
+// a*b+c below is a separate correctly-rounded multiply and add unless fmaf() is written; the
+// association follows glm 0.9.6.3 as used by the reference (dot = (xx'+yy')+zz',
+// mat*vec = (m0 v0 + m1 v1) + (m2 v2 + m3 v3), normalize = v * (1/sqrt(dot))).  hipcc lowers
+// sqrtf and '/' to correctly-rounded sequences on gfx950, so the kernels reproduce the CPU
+// oracle bit for bit.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ptd {
+
+constexpr float kPI = 3.1415926535897932384626422832795028841971f;       // utilities.h:12
+constexpr float kTWO_PI = 6.2831853071795864769252867665590057683943f;   // utilities.h:13
+constexpr float kSQRT_1_3 = 0.5773502691896257645091487805019574556476f; // utilities.h:14
+constexpr float kFLT_MAX = 3.402823466e+38f;
+constexpr float kFLT_EPS = 1.192092896e-07f;
+
+struct f3 { float x, y, z; };
+__device__ __forceinline__ f3 F3(float x, float y, float z) { return f3{x, y, z}; }
+__device__ __forceinline__ f3 operator+(f3 a, f3 b) { return F3(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ f3 operator-(f3 a, f3 b) { return F3(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ f3 operator-(f3 a) { return F3(-a.x, -a.y, -a.z); }
+__device__ __forceinline__ f3 hadamard(f3 a, f3 b) { return F3(a.x * b.x, a.y * b.y, a.z * b.z); }
+__device__ __forceinline__ f3 operator*(f3 a, float s) { return F3(a.x * s, a.y * s, a.z * s); }
+__device__ __forceinline__ f3 operator*(float s, f3 a) { return F3(s * a.x, s * a.y, s * a.z); }
+__device__ __forceinline__ f3 operator/(f3 a, float s) { return F3(a.x / s, a.y / s, a.z / s); }
+__device__ __forceinline__ float dot(f3 a, f3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+__device__ __forceinline__ f3 cross(f3 a, f3 b) {
+    return F3(a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y);
+}
+__device__ __forceinline__ f3 normalize(f3 v) { return v * (1.0f / sqrtf(dot(v, v))); }
+__device__ __forceinline__ float length(f3 v) { return sqrtf(dot(v, v)); }
+__device__ __forceinline__ float gmin(float a, float b) { return a < b ? a : b; }
+__device__ __forceinline__ float gmax(float a, float b) { return a > b ? a : b; }
+__device__ __forceinline__ float at(f3 v, int i) { return i == 0 ? v.x : (i == 1 ? v.y : v.z); }
+
+// Affine 3x4 in glm column order + the exact glm w-term constants.
+//   point  (w=1): (c0 x + c1 y) + (c2 z + c3)
+//   vector (w=0): (c0 x + c1 y) + (c2 z + z3),  z3 = c3 * 0.0f (a signed zero)
+struct Affine {
+    float c[4][3];
+    float z3[3];
+};
+__device__ __forceinline__ f3 xform_point(const Affine& m, f3 v) {
+    return F3((m.c[0][0] * v.x + m.c[1][0] * v.y) + (m.c[2][0] * v.z + m.c[3][0]),
+              (m.c[0][1] * v.x + m.c[1][1] * v.y) + (m.c[2][1] * v.z + m.c[3][1]),
+              (m.c[0][2] * v.x + m.c[1][2] * v.y) + (m.c[2][2] * v.z + m.c[3][2]));
+}
+__device__ __forceinline__ f3 xform_vector(const Affine& m, f3 v) {
+    return F3((m.c[0][0] * v.x + m.c[1][0] * v.y) + (m.c[2][0] * v.z + m.z3[0]),
+              (m.c[0][1] * v.x + m.c[1][1] * v.y) + (m.c[2][1] * v.z + m.z3[1]),
+              (m.c[0][2] * v.x + m.c[1][2] * v.y) + (m.c[2][2] * v.z + m.z3[2]));
+}
+
+// Device copy of a Geom: what intersection needs, nothing else (176 bytes, scalar-loaded).
+struct DGeom {
+    int32_t type, material, tri_start, tri_end;
+    Affine inv;      // inverseTransform
+    Affine xf;       // transform
+    Affine itr;      // invTranspose
+    float bmin[3], bmax[3];
+};
+
+struct DMaterial {   // == pt_material
+    float color[3];
+    float spec_exponent;
+    float spec_color[3];
+    float has_reflective, has_refractive, ior, emittance;
+    int32_t texture_id;
+};
+
+struct DTexture {
+    int32_t width, height, components, pad;
+    const uint8_t* data;
+};
+
+// Triangle hot data: v0 and the two edges (e1 = v1 - v0, e2 = v2 - v0 computed on the host with
+// the same single subtraction glm performs), so the per-test arithmetic is unchanged.
+struct DTri {
+    float v0[3], e1[3], e2[3];
+    int32_t id;
+};
+struct DTriAttr {    // read once for the closest hit
+    float n[3][3];
+    float uv[3][2];
+};
+struct DNode {       // == pt_bvh_node
+    float bmin[3], bmax[3];
+    int32_t sub_areas, axis, first, rchild;
+};
+
+// ---- RNG: thrust::default_random_engine (minstd_rand) seeded like makeSeededRandomEngine ----
+__device__ __forceinline__ uint32_t utilhash(uint32_t a) {   // intersections.h:13-22
+    a = (a + 0x7ed55d16u) + (a << 12);
+    a = (a ^ 0xc761c23cu) ^ (a >> 19);
+    a = (a + 0x165667b1u) + (a << 5);
+    a = (a + 0xd3a2646cu) ^ (a << 9);
+    a = (a + 0xfd7046c5u) + (a << 3);
+    a = (a ^ 0xb55a4f09u) ^ (a >> 16);
+    return a;
+}
+struct Rng {
+    uint32_t x;
+    __device__ __forceinline__ Rng(int iter, int index, int depth) {
+        const uint32_t key = 0x80000000u | ((uint32_t)depth << 22) | (uint32_t)iter;
+        const uint32_t h = utilhash(key) ^ utilhash((uint32_t)index);
+        const uint32_t s = h % 2147483647u;
+        x = s == 0u ? 1u : s;
+    }
+    // x <- 48271 x mod (2^31 - 1) via the Mersenne fold (exact), u = float(x-1) / 2^31.
+    __device__ __forceinline__ float u01() {
+        const uint64_t p = (uint64_t)48271u * x;
+        uint32_t r = (uint32_t)(p & 0x7fffffffu) + (uint32_t)(p >> 31);
+        if (r >= 2147483647u) r -= 2147483647u;
+        x = r;
+        return (float)(x - 1u) * 4.656612873077392578125e-10f;   // / 2147483648.0f (exact)
+    }
+};
+
+// ---- deterministic sin/cos (evaluation contract; mirrored by the oracle) --------------------
+__device__ __forceinline__ void sincos_c(float x, float* s_out, float* c_out) {
+    const float j = rintf(x * 0.636619772367581343f);
+    float r = fmaf(-j, 1.5707962513e+00f, x);
+    r = fmaf(-j, 7.5497894159e-08f, r);
+    r = fmaf(-j, 5.3903029534e-15f, r);
+    const float z = r * r;
+    const float ps = fmaf(fmaf(z, -1.9515295891e-4f, 8.3321608736e-3f), z, -1.6666654611e-1f);
+    const float s = fmaf(r * z, ps, r);
+    const float pc = fmaf(fmaf(z, 2.443315711809948e-5f, -1.388731625493765e-3f), z, 4.166664568298827e-2f);
+    const float c = fmaf(z * z, pc, fmaf(-0.5f, z, 1.0f));
+    const int q = ((int)j) & 3;
+    const float sa = (q & 1) ? c : s;
+    const float ca = (q & 1) ? s : c;
+    *s_out = (q & 2) ? -sa : sa;
+    *c_out = ((q + 1) & 2) ? -ca : ca;
+}
+
+// getPointOnRay (intersections.h:29-32)
+__device__ __forceinline__ f3 point_on_ray(f3 o, f3 d, float t) { return o + (t - .0001f) * normalize(d); }
+
+}  // namespace ptd

@@ -1,0 +1,45 @@
+// Internal host-side types shared by the scene loader, mesh/BVH builder and render context.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/pt_amd.h"
+
+namespace pt {
+
+extern thread_local std::string g_err;
+int fail(int code, const std::string& msg);
+
+struct TextureHost {
+    std::string path;            // set by the JSON loader; pixels filled by pt_scene_set_texture_pixels
+    int32_t width = 0, height = 0, components = 0;
+    std::vector<uint8_t> pixels;
+};
+
+struct Scene {
+    std::vector<pt_geom> geoms;
+    std::vector<pt_material> materials;
+    std::vector<pt_triangle> triangles;     // BVH (DFS) order after finalize
+    std::vector<pt_bvh_node> bvh;
+    std::vector<TextureHost> textures;
+    pt_camera camera{};
+    float fovy = 45.0f;
+    float eye[3] = {0, 0, 0}, look_at[3] = {0, 0, 0}, up[3] = {0, 1, 0};
+    int32_t iterations = 1, depth = 8;
+    std::string file = "render";
+    bool camera_set = false;
+    bool finalized = false;
+    bool bvh_built = false;
+};
+
+int scene_add_geom(Scene& S, int32_t type, int32_t mat, const float* t, const float* r, const float* s);
+int scene_finalize(Scene& S);
+// Mesh / BVH (pt_mesh.cpp)
+int load_obj_mesh(Scene& S, const std::string& path, int32_t mat, const float* t, const float* r, const float* s);
+int add_mesh(Scene& S, int32_t mat, const float* t, const float* r, const float* s, const float* pos, int32_t npos,
+             const float* nrm, int32_t nnrm, const float* uv, int32_t nuv, const int32_t* face_sizes, int32_t nfaces,
+             const int32_t* ip, const int32_t* in, const int32_t* it);
+int build_bvh(Scene& S);
+
+}  // namespace pt

@@ -1,0 +1,1116 @@
+// MI355X path-tracer hot path: ray generation -> ray/scene intersection -> BSDF shading ->
+// stable compaction of terminated paths, one fused kernel per bounce.
+//
+// Reference: path_tracer/src/pathtrace.cu:183-528 (generateRayFromCamera, computeIntersections,
+// shadeMaterials, relocate_terminated_paths, finalGather), intersections.cu, interactions.cu,
+// sceneStructs.h.  MI355X design:
+//   * path state and hit records are structure-of-arrays (4-byte lanes, wave-coalesced);
+//   * one persistent 256-thread workgroup loop per bounce: each tile of 256 paths is loaded,
+//     intersected (geoms are wave-uniform -> scalar loads), shaded, and the survivors are
+//     written to the next buffer at their stable rank (wave ballot + mbcnt, 4 wave counts in
+//     LDS, decoupled look-back across tiles).  No hit-record round trip, no memset of all W*H
+//     hit records per bounce, no host round trip for the live count (it stays on the device);
+//   * a path's radiance is added to the framebuffer the moment it terminates (each pixel owns
+//     one path per iteration, so this equals finalGather); spp > 1 passes write per-slot colours
+//     and a finalize kernel adds them in sample order;
+//   * material-sorted shading (flag) = stable counting sort: per-wave key histograms, one device
+//     scan, a rank scatter, then a shade+compact kernel reading paths through the permutation.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "lookback.h"
+#include "pt_device.h"
+#include "pt_internal.h"
+#include "../../include/sc_amd.h"
+
+using namespace ptd;
+
+namespace {
+
+constexpr int kBlock = 256;
+
+struct PathSoA {
+    float *ox, *oy, *oz, *dx, *dy, *dz, *cr, *cg, *cb;
+    int32_t *slot, *bounces;
+};
+struct HitSoA {
+    float *t, *nx, *ny, *nz, *u, *v;
+    int32_t* mat;
+};
+struct Ctl {            // per-parity control block (16 B)
+    uint32_t ticket;
+    uint32_t live;
+    uint32_t pad[2];
+};
+struct DevStats {
+    unsigned long long segments, passes, bounce_live[64], emissive_hits;
+    uint32_t err, pad;
+};
+
+struct SceneDev {
+    const DGeom* __restrict__ geoms;
+    const DMaterial* __restrict__ mats;
+    const DTri* __restrict__ tris;
+    const DTriAttr* __restrict__ attrs;
+    const DNode* __restrict__ nodes;
+    const DTexture* __restrict__ texs;
+    int32_t ngeoms, nmats, ntris, nnodes;
+};
+struct CamDev {
+    float pos[3], view[3], up[3], right[3], pl[2];
+    int32_t res[2];
+};
+struct FlagsDev {
+    int32_t rr, bvh, bbox, ssaa, dof;
+    float aperture, focal;
+};
+struct TileDev {
+    int32_t W, rank, world, npix, spp, P, depth, iter_first;
+};
+struct KArgs {
+    SceneDev S;
+    CamDev cam;
+    FlagsDev fl;
+    TileDev tile;
+    PathSoA in, out;
+    HitSoA hit;
+    const int32_t* perm;
+    float* image;          // npix * 3 (AoS float3, tile-local)
+    float* colbuf;         // P * 3 (spp > 1)
+    Ctl* ctl;              // [2]
+    uint64_t* status;      // [2][max_tiles]
+    int32_t max_tiles;
+    int32_t parity;
+    int32_t bounce;
+    int32_t n_fixed;       // >= 0: path count is known on the host (first bounce)
+    DevStats* stats;
+};
+
+// ------------------------------------------------------------------------------------------
+// Intersection (computeIntersections, pathtrace.cu:229-298)
+// ------------------------------------------------------------------------------------------
+struct Hit {
+    float t;
+    f3 n;
+    int32_t mat;
+    float u, v;
+};
+
+// boxIntersectionTest (intersections.cu:3-58).  The world normal is deferred to the closest
+// hit: we keep the slab code (axis*2 + sign, -1 = zero vector) and rebuild n from it.
+__device__ __forceinline__ float box_test(const DGeom& g, f3 ro, f3 rd, int& ncode) {
+    const f3 qo = xform_point(g.inv, ro);
+    const f3 qd = normalize(xform_vector(g.inv, rd));
+    float tmin = -1e38f, tmax = 1e38f;
+    int nmin = -1, nmax = -1;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const float qa = at(qd, a), oa = at(qo, a);
+        const float t1 = (-0.5f - oa) / qa;
+        const float t2 = (+0.5f - oa) / qa;
+        const float ta = gmin(t1, t2), tb = gmax(t1, t2);
+        const int code = 2 * a + (t2 < t1 ? 0 : 1);
+        if (ta > 0 && ta > tmin) { tmin = ta; nmin = code; }
+        if (tb < tmax) { tmax = tb; nmax = code; }
+    }
+    if (tmax >= tmin && tmax > 0) {
+        if (tmin <= 0) { tmin = tmax; nmin = nmax; }
+        const f3 ip = xform_point(g.xf, point_on_ray(qo, qd, tmin));
+        ncode = nmin;
+        return length(ro - ip);
+    }
+    return -1.0f;
+}
+__device__ __forceinline__ f3 box_normal(const DGeom& g, int code) {
+    f3 n = F3(0.0f, 0.0f, 0.0f);
+    if (code >= 0) {
+        const float s = (code & 1) ? -1.0f : 1.0f;
+        const int a = code >> 1;
+        n = F3(a == 0 ? s : 0.0f, a == 1 ? s : 0.0f, a == 2 ? s : 0.0f);
+    }
+    return normalize(xform_vector(g.itr, n));
+}
+
+// sphereIntersectionTest (intersections.cu:60-115); normal deferred (object-space hit point kept).
+__device__ __forceinline__ float sphere_test(const DGeom& g, f3 r_o, f3 r_d, f3& obj, bool& outside) {
+    const f3 ro = xform_point(g.inv, r_o);
+    const f3 rd = normalize(xform_vector(g.inv, r_d));
+    const float vdd = dot(ro, rd);
+    const float radicand = vdd * vdd - (dot(ro, ro) - 0.25f);   // powf(0.5f, 2) == 0.25f
+    if (radicand < 0) return -1.0f;
+    const float sq = sqrtf(radicand);
+    const float first = -vdd;
+    const float t1 = first + sq, t2 = first - sq;
+    float t;
+    if (t1 < 0 && t2 < 0) return -1.0f;
+    if (t1 > 0 && t2 > 0) { t = gmin(t1, t2); outside = true; }
+    else { t = gmax(t1, t2); outside = false; }
+    obj = point_on_ray(ro, rd, t);
+    const f3 ip = xform_point(g.xf, obj);
+    return length(r_o - ip);
+}
+__device__ __forceinline__ f3 sphere_normal(const DGeom& g, f3 obj, bool outside) {
+    const f3 n = normalize(xform_vector(g.itr, obj));
+    return outside ? n : -n;
+}
+
+// glm::intersectRayTriangle (gtx/intersect.inl:37-74) with e1/e2 precomputed on the host.
+__device__ __forceinline__ bool ray_tri(const DTri& tr, f3 o, f3 d, float& bx, float& by, float& bz) {
+    const f3 v0 = F3(tr.v0[0], tr.v0[1], tr.v0[2]);
+    const f3 e1 = F3(tr.e1[0], tr.e1[1], tr.e1[2]);
+    const f3 e2 = F3(tr.e2[0], tr.e2[1], tr.e2[2]);
+    const f3 p = cross(d, e2);
+    const float a = dot(e1, p);
+    if (a < kFLT_EPS) return false;
+    const float f = 1.0f / a;
+    const f3 s = o - v0;
+    bx = f * dot(s, p);
+    if (bx < 0.0f || bx > 1.0f) return false;
+    const f3 q = cross(s, e1);
+    by = f * dot(d, q);
+    if (by < 0.0f || by + bx > 1.0f) return false;
+    bz = f * dot(e2, q);
+    return bz >= 0.0f;
+}
+
+// BoundingBox::intersect (boundingbox.h:73-92)
+__device__ __forceinline__ bool aabb_hit(const float* bmin, const float* bmax, f3 o, f3 inv) {
+    const float mx = (bmin[0] - o.x) * inv.x, Mx = (bmax[0] - o.x) * inv.x;
+    const float my = (bmin[1] - o.y) * inv.y, My = (bmax[1] - o.y) * inv.y;
+    const float mz = (bmin[2] - o.z) * inv.z, Mz = (bmax[2] - o.z) * inv.z;
+    const float lo = gmax(gmax(gmin(mx, Mx), gmin(my, My)), gmin(mz, Mz));
+    const float hi = gmin(gmin(gmax(mx, Mx), gmax(my, My)), gmax(mz, Mz));
+    return !(hi < 0) && !(lo > hi);
+}
+
+struct MeshHit {
+    bool any;          // BVHIntersectionTest's return value
+    int32_t id;        // original triangle id of the closest hit
+    int32_t idx;       // index in the BVH-ordered triangle array
+    float t, bx, by;
+};
+
+// BVHIntersectionTest (intersections.cu:169-224): explicit stack of 64, near child first,
+// pops silently on overflow, no t culling; ties keep the first triangle found.
+__device__ MeshHit bvh_traverse(const SceneDev& S, f3 o, f3 d) {
+    MeshHit r{false, -1, -1, kFLT_MAX, 0.f, 0.f};
+    if (S.nnodes == 0) return r;
+    int stack[64];
+    int top = 0, cur = 0;
+    const bool neg[3] = {d.x < 0.0f, d.y < 0.0f, d.z < 0.0f};
+    const f3 inv = F3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    for (;;) {
+        const DNode nd = S.nodes[cur];
+        if (aabb_hit(nd.bmin, nd.bmax, o, inv)) {
+            if (nd.sub_areas > 0) {
+                for (int k = 0; k < nd.sub_areas; ++k) {
+                    const DTri tr = S.tris[nd.first + k];
+                    float bx, by, bz;
+                    if (ray_tri(tr, o, d, bx, by, bz)) {
+                        r.any = true;
+                        if (r.t == -1.0f || bz < r.t) { r.t = bz; r.bx = bx; r.by = by; r.id = tr.id; r.idx = nd.first + k; }
+                    }
+                }
+                if (top == 0) break;
+                cur = stack[--top];
+            } else {
+                if (top == 64) { cur = stack[--top]; continue; }
+                if (neg[nd.axis]) { stack[top++] = cur + 1; cur = nd.rchild; }
+                else { stack[top++] = nd.rchild; cur = cur + 1; }
+            }
+        } else {
+            if (top == 0) break;
+            cur = stack[--top];
+        }
+    }
+    return r;
+}
+
+// Triangle::intersect's attributes for the closest triangle (sceneStructs.h:151-154).
+__device__ __forceinline__ void tri_attrs(const DTriAttr& a, float bx, float by, f3& n, float& u, float& v) {
+    const float w = (1.0f - bx) - by;
+    u = (a.uv[0][0] * w + a.uv[1][0] * bx) + a.uv[2][0] * by;
+    v = (a.uv[0][1] * w + a.uv[1][1] * bx) + a.uv[2][1] * by;
+    const f3 n0 = F3(a.n[0][0], a.n[0][1], a.n[0][2]) * bx;
+    const f3 n1 = F3(a.n[1][0], a.n[1][1], a.n[1][2]) * by;
+    const f3 n2 = F3(a.n[2][0], a.n[2][1], a.n[2][2]) * ((1.0f - bx) - by);
+    n = normalize((n0 + n1) + n2);
+}
+
+// meshIntersectionTest (intersections.cu:119-167): linear loop, optional world-AABB cull.
+__device__ float mesh_linear(const SceneDev& S, const DGeom& g, f3 o, f3 d, bool use_bbox, f3& n, float& u, float& v) {
+    if (use_bbox) {
+        const f3 inv = F3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+        if (!aabb_hit(g.bmin, g.bmax, o, inv)) return -1.0f;
+    }
+    int best = -1;
+    float tmin = kFLT_MAX, b0 = 0.f, b1 = 0.f;
+    for (int i = g.tri_start; i < g.tri_end; ++i) {
+        float bx, by, bz;
+        if (ray_tri(S.tris[i], o, d, bx, by, bz) && bz > 0.0f && bz < tmin) { best = i; tmin = bz; b0 = bx; b1 = by; }
+    }
+    if (best == -1) return -1.0f;
+    const float az = (1.0f - b0) - b1;
+    const DTriAttr& a = S.attrs[best];
+    const f3 s = (az * F3(a.n[0][0], a.n[0][1], a.n[0][2]) + F3(a.n[1][0], a.n[1][1], a.n[1][2])) +
+                 F3(a.n[2][0], a.n[2][1], a.n[2][2]);
+    n = normalize(s);
+    u = (az * a.uv[0][0] + a.uv[1][0]) + a.uv[2][0];
+    v = (az * a.uv[0][1] + a.uv[1][1]) + a.uv[2][1];
+    return tmin;
+}
+
+__device__ __forceinline__ Hit intersect_scene(const SceneDev& S, const FlagsDev& fl, f3 ro, f3 rd) {
+    float t_min = kFLT_MAX;
+    int hit_geom = -1, best_code = -1;
+    f3 best_obj = F3(0, 0, 0), best_n = F3(0, 0, 0);
+    bool best_outside = true;
+    float tmp_u = 0.f, tmp_v = 0.f, cu = 0.f, cv = 0.f;
+    f3 tmp_n = F3(0, 0, 0);
+    MeshHit mh{false, -1, -1, kFLT_MAX, 0.f, 0.f};
+    bool traversed = false;
+    for (int i = 0; i < S.ngeoms; ++i) {
+        const DGeom& g = S.geoms[i];
+        float t = -1.0f;
+        int code = -1;
+        f3 obj = F3(0, 0, 0);
+        bool outside = true;
+        if (g.type == PT_GEOM_CUBE) {
+            t = box_test(g, ro, rd, code);
+        } else if (g.type == PT_GEOM_SPHERE) {
+            t = sphere_test(g, ro, rd, obj, outside);
+        } else if (g.type == PT_GEOM_MESH) {
+            if (fl.bvh) {
+                if (!traversed) { mh = bvh_traverse(S, ro, rd); traversed = true; }
+                if (mh.any && mh.id >= g.tri_start && mh.id < g.tri_end) {
+                    t = mh.t;
+                    tri_attrs(S.attrs[mh.idx], mh.bx, mh.by, tmp_n, tmp_u, tmp_v);
+                }
+            } else {
+                float u2, v2;
+                f3 n2;
+                t = mesh_linear(S, g, ro, rd, fl.bbox != 0, n2, u2, v2);
+                if (t != -1.0f) { tmp_n = n2; tmp_u = u2; tmp_v = v2; }
+            }
+        }
+        if (t > 0.0f && t_min > t) {
+            t_min = t;
+            hit_geom = i;
+            cu = tmp_u;
+            cv = tmp_v;
+            best_code = code;
+            best_obj = obj;
+            best_outside = outside;
+            best_n = tmp_n;
+        }
+    }
+    Hit h;
+    if (hit_geom < 0) {
+        h.t = -1.0f;
+        h.mat = 0;
+        h.n = F3(0, 0, 0);
+        h.u = h.v = 0.f;
+        return h;
+    }
+    const DGeom& g = S.geoms[hit_geom];
+    h.t = t_min;
+    h.mat = g.material;
+    h.u = cu;
+    h.v = cv;
+    if (g.type == PT_GEOM_CUBE) h.n = box_normal(g, best_code);
+    else if (g.type == PT_GEOM_SPHERE) h.n = sphere_normal(g, best_obj, best_outside);
+    else h.n = best_n;
+    return h;
+}
+
+// ------------------------------------------------------------------------------------------
+// Shading (shadeMaterials pathtrace.cu:300-344, scatterRay interactions.cu:43-85)
+// ------------------------------------------------------------------------------------------
+struct PathReg {
+    f3 o, d, c;
+    int32_t slot, bounces;
+};
+
+__device__ __forceinline__ f3 tex_color(const DTexture& tx, float u, float v) {   // sceneStructs.h:176-189
+    int X = (int)gmin(1.f * tx.width * u, 1.f * tx.width - 1.0f);
+    int Y = (int)gmin(1.f * tx.height * (1.0f - v), 1.f * tx.height - 1.0f);
+    X = X < 0 ? 0 : X;
+    Y = Y < 0 ? 0 : Y;
+    const int id = Y * tx.width + X;
+    if (tx.components == 3) {
+        const uint8_t* p = tx.data + 3 * (size_t)id;
+        return 0.003921568627f * F3((float)p[0], (float)p[1], (float)p[2]);
+    }
+    return F3(0, 0, 0);
+}
+
+__device__ __forceinline__ f3 hemisphere(f3 n, Rng& rng) {   // interactions.cu:3-41
+    const float up = sqrtf(rng.u01());
+    const float over = sqrtf(1 - up * up);
+    const float around = rng.u01() * kTWO_PI;
+    f3 dnn;
+    if (fabsf(n.x) < kSQRT_1_3) dnn = F3(1, 0, 0);
+    else if (fabsf(n.y) < kSQRT_1_3) dnn = F3(0, 1, 0);
+    else dnn = F3(0, 0, 1);
+    const f3 p1 = normalize(cross(n, dnn));
+    const f3 p2 = normalize(cross(n, p1));
+    float sa, ca;
+    sincos_c(around, &sa, &ca);
+    return (up * n + (ca * over) * p1) + (sa * over) * p2;
+}
+
+__device__ __forceinline__ f3 reflect(f3 I, f3 N) { return I - hadamard(N * dot(N, I), F3(2, 2, 2)); }
+__device__ __forceinline__ f3 refract(f3 I, f3 N, float eta) {   // glm 0.9.6.3: NaN when k < 0
+    const float dv = dot(N, I);
+    const float k = 1.0f - eta * eta * (1.0f - dv * dv);
+    return (eta * I - (eta * dv + sqrtf(k)) * N) * (float)(k >= 0.0f);
+}
+
+// Returns true if the path survives.  `idx` is the path's position in the (compacted, possibly
+// material-sorted) array — the RNG key of the reference (pathtrace.cu:315).
+__device__ __forceinline__ bool shade(const SceneDev& S, const FlagsDev& fl, int depth, int iter, int idx,
+                                      PathReg& p, const Hit& h) {
+    if (h.t <= 0.0f) { p.c = F3(0, 0, 0); return false; }
+    int remaining = depth - p.bounces;
+    Rng rng(iter, idx, remaining);
+    const DMaterial& m = S.mats[h.mat];
+    const f3 mcol = F3(m.color[0], m.color[1], m.color[2]);
+    if (m.emittance > 0.0f) {
+        p.c = hadamard(p.c, mcol * m.emittance);
+        return false;
+    }
+    const f3 hitp = point_on_ray(p.o, p.d, h.t);
+    const f3 n = h.n;
+    p.o = hitp + 0.0001f * n;
+    const f3 alb = m.texture_id != -1 ? tex_color(S.texs[m.texture_id], h.u, h.v) : mcol;
+    p.c = hadamard(p.c, alb);
+    const f3 scol = F3(m.spec_color[0], m.spec_color[1], m.spec_color[2]);
+    if (m.has_refractive != 0.0f) {
+        const float eta = m.ior;
+        const float R0 = ((eta - 1) * (eta - 1)) / ((eta + 1) * (eta + 1));
+        const float X = 1 - fabsf(dot(p.d, n));
+        const float X2 = X * X;
+        const float R = R0 + (1 - R0) * ((X * X2) * X2);
+        if (R < rng.u01()) { p.d = refract(p.d, n, eta); p.c = hadamard(p.c, mcol); }
+        else { p.d = reflect(p.d, n); p.c = hadamard(p.c, scol); }
+    } else if (rng.u01() < m.has_reflective) {
+        p.d = reflect(p.d, n);
+        p.c = hadamard(p.c, scol);
+    } else {
+        p.d = hemisphere(n, rng);
+    }
+    p.c = hadamard(p.c, mcol);
+    p.bounces += 1;
+    remaining -= 1;
+    if (remaining == 0) { p.c = F3(0, 0, 0); return false; }
+    if (fl.rr && p.bounces > 3) {
+        const f3 luma = F3((float)0.2126, (float)0.7152, (float)0.0722);
+        const float l = dot(p.c, luma);
+        const float q = gmax(0.05f, 1 - l);
+        if (rng.u01() < q) { p.c = F3(0, 0, 0); return false; }
+        p.c = p.c / (1.0f - q);
+    }
+    return true;
+}
+
+// generateRayFromCamera (pathtrace.cu:183-227) for tile slot `slot`.
+__device__ __forceinline__ void raygen(const CamDev& cam, const FlagsDev& fl, const TileDev& T, int slot, PathReg& p) {
+    const int s = slot / T.npix;
+    const int lp = slot - s * T.npix;
+    const int row = lp / T.W;
+    const int x = lp - row * T.W;
+    const int y = row * T.world + T.rank;
+    const int index = x + y * cam.res[0];
+    p.o = F3(cam.pos[0], cam.pos[1], cam.pos[2]);
+    p.c = F3(1.0f, 1.0f, 1.0f);
+    Rng rng(T.iter_first + s, index, T.depth);
+    float ax = (float)x - (float)cam.res[0] * 0.5f;
+    float ay = (float)y - (float)cam.res[1] * 0.5f;
+    if (fl.ssaa) {
+        ax = ax + rng.u01();
+        ay = ay + rng.u01();
+    }
+    const f3 view = F3(cam.view[0], cam.view[1], cam.view[2]);
+    const f3 right = F3(cam.right[0], cam.right[1], cam.right[2]);
+    const f3 up = F3(cam.up[0], cam.up[1], cam.up[2]);
+    p.d = normalize((view - (right * cam.pl[0]) * ax) - (up * cam.pl[1]) * ay);
+    if (fl.dof) {
+        const float r = rng.u01() * fl.aperture;
+        const float th = (rng.u01() * 2) * kPI;
+        float sth, cth;
+        sincos_c(th, &sth, &cth);
+        const f3 lens = F3(r * cth, r * sth, 0.0f);
+        const float ft = fl.focal / fabsf(p.d.z);
+        const f3 focus = p.o + ft * p.d;
+        p.o = p.o + lens;
+        p.d = normalize(focus - p.o);
+    }
+    p.slot = slot;
+    p.bounces = 0;
+}
+
+__device__ __forceinline__ void load_path(const PathSoA& B, int i, PathReg& p) {
+    p.o = F3(B.ox[i], B.oy[i], B.oz[i]);
+    p.d = F3(B.dx[i], B.dy[i], B.dz[i]);
+    p.c = F3(B.cr[i], B.cg[i], B.cb[i]);
+    p.slot = B.slot[i];
+    p.bounces = B.bounces[i];
+}
+__device__ __forceinline__ void store_path(const PathSoA& B, int i, const PathReg& p) {
+    B.ox[i] = p.o.x; B.oy[i] = p.o.y; B.oz[i] = p.o.z;
+    B.dx[i] = p.d.x; B.dy[i] = p.d.y; B.dz[i] = p.d.z;
+    B.cr[i] = p.c.x; B.cg[i] = p.c.y; B.cb[i] = p.c.z;
+    B.slot[i] = p.slot;
+    B.bounces[i] = p.bounces;
+}
+
+// A path that terminated this bounce: its colour is final (finalGather, pathtrace.cu:347-356).
+template <bool SPP1>
+__device__ __forceinline__ void retire(const KArgs& A, const PathReg& p) {
+    if (SPP1) {
+        if (p.c.x != 0.0f || p.c.y != 0.0f || p.c.z != 0.0f) {
+            float* px = A.image + 3 * (size_t)p.slot;
+            px[0] += p.c.x;
+            px[1] += p.c.y;
+            px[2] += p.c.z;
+        }
+    } else {
+        float* q = A.colbuf + 3 * (size_t)p.slot;
+        q[0] = p.c.x;
+        q[1] = p.c.y;
+        q[2] = p.c.z;
+    }
+}
+
+// Zero the control block + tile status words the NEXT launch (other parity) will use, and
+// return this launch's path count.
+__device__ __forceinline__ int begin_launch(const KArgs& A) {
+    const int q = A.parity, nq = q ^ 1;
+    uint64_t* nst = A.status + (size_t)nq * A.max_tiles;
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < A.max_tiles; j += gridDim.x * blockDim.x) nst[j] = 0ull;
+    if (blockIdx.x == 0 && threadIdx.x == 0) A.ctl[nq].ticket = 0u;
+    return A.n_fixed >= 0 ? A.n_fixed : (int)A.ctl[q].live;
+}
+
+// Per-tile stable compaction: returns this thread's output position (valid when alive) and
+// publishes the tile's survivor count; the last tile writes the next launch's path count.
+__device__ __forceinline__ int compact_tile(const KArgs& A, int tile, int num_tiles, bool alive,
+                                            uint32_t* s_wc, uint32_t* s_excl) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint64_t m = __ballot(alive);
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    if (lane == 0) s_wc[wave] = (uint32_t)__popcll(m);
+    __syncthreads();
+    const uint32_t w0 = s_wc[0], w1 = s_wc[1], w2 = s_wc[2], w3 = s_wc[3];
+    const uint32_t total = (w0 + w1) + (w2 + w3);
+    const uint32_t before = (wave > 0 ? w0 : 0u) + (wave > 1 ? w1 : 0u) + (wave > 2 ? w2 : 0u);
+    uint64_t* st = A.status + (size_t)A.parity * A.max_tiles;
+    if (wave == 0) {
+        uint32_t excl = 0;
+        if (tile == 0) {
+            if (lane == 0) lb::publish(st, 0, lb::kFlagPre, total);
+        } else {
+            if (lane == 0) lb::publish(st, tile, lb::kFlagAgg, total);
+            excl = lb::lookback(st, tile, lane, &A.stats->err);
+            if (lane == 0) lb::publish(st, tile, lb::kFlagPre, excl + total);
+        }
+        if (lane == 0) {
+            *s_excl = excl;
+            if (tile == num_tiles - 1) A.ctl[A.parity ^ 1].live = excl + total;
+        }
+    }
+    __syncthreads();
+    return (int)(*s_excl + before + rank);
+}
+
+__device__ __forceinline__ void count_emissive(const KArgs& A, bool emitted) {
+    const uint64_t m = __ballot(emitted);
+    if (m && (threadIdx.x & 63) == 0) atomicAdd(&A.stats->emissive_hits, (unsigned long long)__popcll(m));
+}
+
+// The fused bounce: [raygen] -> intersect -> shade -> compact.  Persistent tile loop.
+template <bool FIRST, bool SPP1>
+__global__ __launch_bounds__(kBlock) void k_bounce(const KArgs A) {
+    __shared__ uint32_t s_tile, s_excl;
+    __shared__ uint32_t s_wc[4];
+    const int N = begin_launch(A);
+    const int num_tiles = (N + kBlock - 1) / kBlock;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (num_tiles == 0) A.ctl[A.parity ^ 1].live = 0u;
+        atomicAdd(&A.stats->bounce_live[A.bounce], (unsigned long long)N);
+        atomicAdd(&A.stats->segments, (unsigned long long)N);
+    }
+    if ((int)blockIdx.x >= num_tiles) return;
+    for (;;) {
+        if (threadIdx.x == 0) s_tile = atomicAdd(&A.ctl[A.parity].ticket, 1u);
+        __syncthreads();
+        const int tile = (int)s_tile;
+        if (tile >= num_tiles) break;
+        const int i = tile * kBlock + (int)threadIdx.x;
+        bool alive = false, emitted = false;
+        PathReg p;
+        if (i < N) {
+            if (FIRST) raygen(A.cam, A.fl, A.tile, i, p);
+            else load_path(A.in, i, p);
+            const Hit h = intersect_scene(A.S, A.fl, p.o, p.d);
+            const int iter = A.tile.iter_first + (SPP1 ? 0 : p.slot / A.tile.npix);
+            alive = shade(A.S, A.fl, A.tile.depth, iter, i, p, h);
+            if (!alive) {
+                emitted = p.c.x != 0.0f || p.c.y != 0.0f || p.c.z != 0.0f;
+                retire<SPP1>(A, p);
+            }
+        }
+        count_emissive(A, emitted);
+        const int pos = compact_tile(A, tile, num_tiles, alive, s_wc, &s_excl);
+        if (alive) store_path(A.out, pos, p);
+    }
+}
+
+// ---- material-sorted mode (pathtrace.cu:479-491: stable sort_by_key on materialId) ---------
+__global__ __launch_bounds__(kBlock) void k_raygen(const KArgs A) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < A.tile.P; i += gridDim.x * blockDim.x) {
+        PathReg p;
+        raygen(A.cam, A.fl, A.tile, i, p);
+        store_path(A.in, i, p);
+    }
+}
+
+// Intersect + per-wave (64-path "sort tile") histogram of material keys.  hist is key-major:
+// hist[key * max_t64 + t64], written for every t64 < max_t64 so a flat exclusive scan of it
+// yields every path's stable sorted position base.
+__global__ __launch_bounds__(kBlock) void k_isect_hist(const KArgs A, int32_t* __restrict__ keys,
+                                                        int32_t* __restrict__ hist, int max_t64) {
+    const int N = A.n_fixed >= 0 ? A.n_fixed : (int)A.ctl[A.parity].live;
+    const int lane = threadIdx.x & 63;
+    const int waves = gridDim.x * (blockDim.x >> 6);
+    for (int t64 = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); t64 < max_t64; t64 += waves) {
+        const int i = t64 * 64 + lane;
+        int key = -1;
+        if (i < N) {
+            const f3 o = F3(A.in.ox[i], A.in.oy[i], A.in.oz[i]);
+            const f3 d = F3(A.in.dx[i], A.in.dy[i], A.in.dz[i]);
+            const Hit h = intersect_scene(A.S, A.fl, o, d);
+            A.hit.t[i] = h.t;
+            A.hit.nx[i] = h.n.x; A.hit.ny[i] = h.n.y; A.hit.nz[i] = h.n.z;
+            A.hit.u[i] = h.u; A.hit.v[i] = h.v;
+            key = h.t == -1.0f ? 0 : h.mat;     // misses keep the memset materialId 0 (pathtrace.cu:466)
+            A.hit.mat[i] = key;
+            keys[i] = key;
+        }
+        for (int k0 = 0; k0 < A.S.nmats; k0 += 64) {
+            const int k = k0 + lane;
+            const uint64_t dummy = 0;
+            (void)dummy;
+            uint32_t cnt = 0;
+            // count of lanes whose key == k (k differs per lane): loop over the wave's keys
+            for (int src = 0; src < 64; ++src) cnt += (__shfl(key, src, 64) == k) ? 1u : 0u;
+            if (k < A.S.nmats) hist[(size_t)k * max_t64 + t64] = (int32_t)cnt;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_sort_scatter(const KArgs A, const int32_t* __restrict__ keys,
+                                                          const int32_t* __restrict__ offs, int32_t* __restrict__ perm,
+                                                          int max_t64) {
+    const int N = A.n_fixed >= 0 ? A.n_fixed : (int)A.ctl[A.parity].live;
+    const int lane = threadIdx.x & 63;
+    const int waves = gridDim.x * (blockDim.x >> 6);
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    for (int t64 = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); t64 * 64 < N; t64 += waves) {
+        const int i = t64 * 64 + lane;
+        const int key = i < N ? keys[i] : -1;
+        uint64_t same = 0;
+        for (int src = 0; src < 64; ++src) {
+            const int ks = __shfl(key, src, 64);
+            same |= (ks == key) ? (1ull << src) : 0ull;
+        }
+        if (i < N) perm[offs[(size_t)key * max_t64 + t64] + __popcll(same & lt)] = i;
+    }
+}
+
+template <bool SPP1>
+__global__ __launch_bounds__(kBlock) void k_shade_sorted(const KArgs A) {
+    __shared__ uint32_t s_tile, s_excl;
+    __shared__ uint32_t s_wc[4];
+    const int N = begin_launch(A);
+    const int num_tiles = (N + kBlock - 1) / kBlock;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (num_tiles == 0) A.ctl[A.parity ^ 1].live = 0u;
+        atomicAdd(&A.stats->bounce_live[A.bounce], (unsigned long long)N);
+        atomicAdd(&A.stats->segments, (unsigned long long)N);
+    }
+    if ((int)blockIdx.x >= num_tiles) return;
+    for (;;) {
+        if (threadIdx.x == 0) s_tile = atomicAdd(&A.ctl[A.parity].ticket, 1u);
+        __syncthreads();
+        const int tile = (int)s_tile;
+        if (tile >= num_tiles) break;
+        const int idx = tile * kBlock + (int)threadIdx.x;
+        bool alive = false, emitted = false;
+        PathReg p;
+        if (idx < N) {
+            const int i = A.perm[idx];
+            load_path(A.in, i, p);
+            Hit h;
+            h.t = A.hit.t[i];
+            h.n = F3(A.hit.nx[i], A.hit.ny[i], A.hit.nz[i]);
+            h.mat = A.hit.mat[i];
+            h.u = A.hit.u[i];
+            h.v = A.hit.v[i];
+            const int iter = A.tile.iter_first + (SPP1 ? 0 : p.slot / A.tile.npix);
+            alive = shade(A.S, A.fl, A.tile.depth, iter, idx, p, h);
+            if (!alive) {
+                emitted = p.c.x != 0.0f || p.c.y != 0.0f || p.c.z != 0.0f;
+                retire<SPP1>(A, p);
+            }
+        }
+        count_emissive(A, emitted);
+        const int pos = compact_tile(A, tile, num_tiles, alive, s_wc, &s_excl);
+        if (alive) store_path(A.out, pos, p);
+    }
+}
+
+// spp > 1: add the per-slot colours in sample order (finalGather as `spp` sequential iterations).
+__global__ void k_finalize_spp(float* __restrict__ image, const float* __restrict__ col, int npix, int spp) {
+    for (int lp = blockIdx.x * blockDim.x + threadIdx.x; lp < npix; lp += gridDim.x * blockDim.x) {
+        float r = image[3 * (size_t)lp], g = image[3 * (size_t)lp + 1], b = image[3 * (size_t)lp + 2];
+        for (int s = 0; s < spp; ++s) {
+            const float* c = col + 3 * ((size_t)s * npix + lp);
+            r += c[0]; g += c[1]; b += c[2];
+        }
+        image[3 * (size_t)lp] = r; image[3 * (size_t)lp + 1] = g; image[3 * (size_t)lp + 2] = b;
+    }
+}
+
+__global__ void k_stats_pass(DevStats* st) { atomicAdd(&st->passes, 1ull); }
+
+// sendImageToPBO (pathtrace.cu:64-86)
+__global__ void k_preview(const float* __restrict__ image, uint8_t* __restrict__ rgba, int npix, int iter) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < npix; i += gridDim.x * blockDim.x) {
+        for (int k = 0; k < 3; ++k) {
+            int v = (int)((double)(image[3 * (size_t)i + k] / iter) * 255.0);
+            v = v < 0 ? 0 : (v > 255 ? 255 : v);
+            rgba[4 * (size_t)i + k] = (uint8_t)v;
+        }
+        rgba[4 * (size_t)i + 3] = 0;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Host context
+// ------------------------------------------------------------------------------------------
+#define HIP_TRY(expr)                                                                       \
+    do {                                                                                    \
+        hipError_t _e = (expr);                                                             \
+        if (_e != hipSuccess)                                                               \
+            return pt::fail(PT_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+    } while (0)
+
+struct ProfEv {
+    hipEvent_t a, b;
+    bool bounce;
+};
+
+}  // namespace
+
+struct pt_ctx {
+    int device = 0;
+    int depth = 8;
+    int nmats = 0;
+    pt_flags flags{};
+    KArgs args{};
+    int max_tiles = 0, max_t64 = 0;
+    int grid_persistent = 0;
+    // owned device allocations
+    std::vector<void*> allocs;
+    PathSoA buf[2]{};
+    int cur = 0;
+    int32_t *keys = nullptr, *hist = nullptr, *offs = nullptr, *perm = nullptr;
+    void* scan_ws = nullptr;
+    DevStats* stats = nullptr;
+    bool profiling = false;
+    std::vector<ProfEv> events;
+    std::vector<uint64_t> prof_bytes;
+    double bounce_ms = 0.0, total_ms = 0.0;
+    uint64_t bounce_launches = 0, bytes = 0;
+
+    ~pt_ctx() {
+        for (auto& e : events) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
+        for (void* p : allocs) (void)hipFree(p);
+    }
+    template <typename T>
+    int alloc(T** p, size_t count) {
+        void* q = nullptr;
+        const size_t bytes_ = std::max<size_t>(count * sizeof(T), 16);
+        hipError_t e = hipMalloc(&q, bytes_);
+        if (e != hipSuccess) return pt::fail(PT_ERR_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+        allocs.push_back(q);
+        *p = static_cast<T*>(q);
+        return PT_OK;
+    }
+};
+
+namespace {
+
+void set_flags_dev(pt_ctx* c, const pt_flags& f) {
+    c->flags = f;
+    c->args.fl.rr = f.russian_roulette;
+    c->args.fl.bvh = f.use_bvh;
+    c->args.fl.bbox = f.use_bbox;
+    c->args.fl.ssaa = f.ssaa;
+    c->args.fl.dof = f.dof;
+    c->args.fl.aperture = f.aperture;
+    c->args.fl.focal = f.focal_dist;
+}
+
+Affine to_affine(const float* m) {   // glm column-major 4x4 -> 3x4 + the exact w=0 terms
+    Affine a;
+    for (int col = 0; col < 4; ++col)
+        for (int r = 0; r < 3; ++r) a.c[col][r] = m[4 * col + r];
+    for (int r = 0; r < 3; ++r) a.z3[r] = m[12 + r] * 0.0f;
+    return a;
+}
+
+int alloc_paths(pt_ctx* c, PathSoA& B, size_t P) {
+    float** f[9] = {&B.ox, &B.oy, &B.oz, &B.dx, &B.dy, &B.dz, &B.cr, &B.cg, &B.cb};
+    for (auto* p : f)
+        if (int rc = c->alloc(p, P)) return rc;
+    if (int rc = c->alloc(&B.slot, P)) return rc;
+    return c->alloc(&B.bounces, P);
+}
+
+template <typename K>
+int launch_k(pt_ctx* c, K kernel, int grid, hipStream_t st, bool is_bounce, const KArgs& a) {
+    ProfEv ev{};
+    if (c->profiling) {
+        HIP_TRY(hipEventCreate(&ev.a));
+        HIP_TRY(hipEventCreate(&ev.b));
+        HIP_TRY(hipEventRecord(ev.a, st));
+    }
+    hipLaunchKernelGGL(kernel, dim3(grid), dim3(kBlock), 0, st, a);
+    HIP_TRY(hipGetLastError());
+    if (c->profiling) {
+        HIP_TRY(hipEventRecord(ev.b, st));
+        ev.bounce = is_bounce;
+        c->events.push_back(ev);
+    }
+    return PT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shard, pt_ctx** out) {
+    if (!scene || !out) return pt::fail(PT_ERR_ARG, "null argument");
+    const auto& S = *reinterpret_cast<const pt::Scene*>(scene);
+    if (!S.finalized) return pt::fail(PT_ERR_ARG, "scene not finalized (pt_scene_finalize)");
+    if (S.materials.empty() || S.geoms.empty()) return pt::fail(PT_ERR_ARG, "scene has no geometry/materials");
+    pt_shard sh{0, 1, 1, 0};
+    if (shard) sh = *shard;
+    if (sh.world < 1 || sh.rank < 0 || sh.rank >= sh.world || sh.spp < 1)
+        return pt::fail(PT_ERR_ARG, "bad shard (rank/world/spp)");
+    const int W = S.camera.res[0], H = S.camera.res[1];
+    const int rows = (H - sh.rank + sh.world - 1) / sh.world;
+    if (rows <= 0) return pt::fail(PT_ERR_ARG, "empty tile");
+    const long long npix = (long long)rows * W;
+    const long long P = npix * sh.spp;
+    if (P > 0x7fffffffLL - 4096) return pt::fail(PT_ERR_ARG, "too many paths per pass");
+    for (const auto& t : S.textures)
+        if (t.pixels.empty()) return pt::fail(PT_ERR_ARG, "texture without pixels: " + t.path);
+
+    auto* c = new pt_ctx();
+    auto bail = [&](int rc) { delete c; return rc; };
+    hipError_t e = hipGetDevice(&c->device);
+    if (e != hipSuccess) return bail(pt::fail(PT_ERR_HIP, std::string("hipGetDevice: ") + hipGetErrorString(e)));
+    c->depth = S.depth;
+    c->nmats = (int)S.materials.size();
+    KArgs& A = c->args;
+    std::memset(&A, 0, sizeof A);
+    set_flags_dev(c, flags ? *flags : [] { pt_flags f; pt_flags_default(&f); return f; }());
+
+    // ---- scene upload ----
+    std::vector<DGeom> dg(S.geoms.size());
+    for (size_t i = 0; i < S.geoms.size(); ++i) {
+        const pt_geom& g = S.geoms[i];
+        DGeom& d = dg[i];
+        std::memset(&d, 0, sizeof d);
+        d.type = g.type;
+        d.material = g.material_id;
+        d.tri_start = g.tri_start;
+        d.tri_end = g.tri_end;
+        d.inv = to_affine(g.inverse_transform);
+        d.xf = to_affine(g.transform);
+        d.itr = to_affine(g.inv_transpose);
+        for (int k = 0; k < 3; ++k) { d.bmin[k] = g.min_bound[k]; d.bmax[k] = g.max_bound[k]; }
+    }
+    DGeom* d_geoms;
+    DMaterial* d_mats;
+    if (int rc = c->alloc(&d_geoms, dg.size())) return bail(rc);
+    if (int rc = c->alloc(&d_mats, S.materials.size())) return bail(rc);
+    if ((e = hipMemcpy(d_geoms, dg.data(), dg.size() * sizeof(DGeom), hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMemcpy(d_mats, S.materials.data(), S.materials.size() * sizeof(DMaterial), hipMemcpyHostToDevice)) != hipSuccess)
+        return bail(pt::fail(PT_ERR_HIP, std::string("scene upload: ") + hipGetErrorString(e)));
+    static_assert(sizeof(DMaterial) == sizeof(pt_material), "material layout");
+    static_assert(sizeof(DNode) == sizeof(pt_bvh_node), "bvh node layout");
+    A.S.geoms = d_geoms;
+    A.S.mats = d_mats;
+    A.S.ngeoms = (int)dg.size();
+    A.S.nmats = (int)S.materials.size();
+    if (!S.triangles.empty()) {
+        std::vector<DTri> tr(S.triangles.size());
+        std::vector<DTriAttr> at(S.triangles.size());
+        for (size_t i = 0; i < S.triangles.size(); ++i) {
+            const pt_triangle& t = S.triangles[i];
+            for (int k = 0; k < 3; ++k) {
+                tr[i].v0[k] = t.v[0][k];
+                tr[i].e1[k] = t.v[1][k] - t.v[0][k];
+                tr[i].e2[k] = t.v[2][k] - t.v[0][k];
+            }
+            tr[i].id = t.id;
+            std::memcpy(at[i].n, t.n, sizeof at[i].n);
+            std::memcpy(at[i].uv, t.uv, sizeof at[i].uv);
+        }
+        DTri* d_tr;
+        DTriAttr* d_at;
+        if (int rc = c->alloc(&d_tr, tr.size())) return bail(rc);
+        if (int rc = c->alloc(&d_at, at.size())) return bail(rc);
+        if ((e = hipMemcpy(d_tr, tr.data(), tr.size() * sizeof(DTri), hipMemcpyHostToDevice)) != hipSuccess ||
+            (e = hipMemcpy(d_at, at.data(), at.size() * sizeof(DTriAttr), hipMemcpyHostToDevice)) != hipSuccess)
+            return bail(pt::fail(PT_ERR_HIP, std::string("triangle upload: ") + hipGetErrorString(e)));
+        A.S.tris = d_tr;
+        A.S.attrs = d_at;
+        A.S.ntris = (int)tr.size();
+    }
+    if (!S.bvh.empty()) {
+        DNode* d_nodes;
+        if (int rc = c->alloc(&d_nodes, S.bvh.size())) return bail(rc);
+        if ((e = hipMemcpy(d_nodes, S.bvh.data(), S.bvh.size() * sizeof(DNode), hipMemcpyHostToDevice)) != hipSuccess)
+            return bail(pt::fail(PT_ERR_HIP, std::string("bvh upload: ") + hipGetErrorString(e)));
+        A.S.nodes = d_nodes;
+        A.S.nnodes = (int)S.bvh.size();
+    }
+    if (!S.textures.empty()) {
+        std::vector<DTexture> tx(S.textures.size());
+        for (size_t i = 0; i < S.textures.size(); ++i) {
+            const auto& t = S.textures[i];
+            uint8_t* d_px;
+            if (int rc = c->alloc(&d_px, t.pixels.size())) return bail(rc);
+            if ((e = hipMemcpy(d_px, t.pixels.data(), t.pixels.size(), hipMemcpyHostToDevice)) != hipSuccess)
+                return bail(pt::fail(PT_ERR_HIP, std::string("texture upload: ") + hipGetErrorString(e)));
+            tx[i] = DTexture{t.width, t.height, t.components, 0, d_px};
+        }
+        DTexture* d_tx;
+        if (int rc = c->alloc(&d_tx, tx.size())) return bail(rc);
+        if ((e = hipMemcpy(d_tx, tx.data(), tx.size() * sizeof(DTexture), hipMemcpyHostToDevice)) != hipSuccess)
+            return bail(pt::fail(PT_ERR_HIP, std::string("texture table upload: ") + hipGetErrorString(e)));
+        A.S.texs = d_tx;
+    }
+
+    // ---- camera / tile ----
+    const pt_camera& cam = S.camera;
+    for (int k = 0; k < 3; ++k) {
+        A.cam.pos[k] = cam.position[k];
+        A.cam.view[k] = cam.view[k];
+        A.cam.up[k] = cam.up[k];
+        A.cam.right[k] = cam.right[k];
+    }
+    A.cam.pl[0] = cam.pixel_length[0];
+    A.cam.pl[1] = cam.pixel_length[1];
+    A.cam.res[0] = W;
+    A.cam.res[1] = H;
+    A.tile = TileDev{W, sh.rank, sh.world, (int)npix, sh.spp, (int)P, S.depth, 1};
+
+    // ---- path state, image, control ----
+    for (int b = 0; b < 2; ++b)
+        if (int rc = alloc_paths(c, c->buf[b], (size_t)P)) return bail(rc);
+    if (int rc = c->alloc(&A.image, (size_t)npix * 3)) return bail(rc);
+    if (sh.spp > 1)
+        if (int rc = c->alloc(&A.colbuf, (size_t)P * 3)) return bail(rc);
+    c->max_tiles = (int)((P + kBlock - 1) / kBlock);
+    if (int rc = c->alloc(&A.ctl, 2)) return bail(rc);
+    if (int rc = c->alloc(&A.status, (size_t)2 * c->max_tiles)) return bail(rc);
+    if (int rc = c->alloc(&c->stats, 1)) return bail(rc);
+    A.stats = c->stats;
+    A.max_tiles = c->max_tiles;
+    if ((e = hipMemset(A.image, 0, (size_t)npix * 3 * sizeof(float))) != hipSuccess ||
+        (e = hipMemset(A.ctl, 0, 2 * sizeof(Ctl))) != hipSuccess ||
+        (e = hipMemset(A.status, 0, (size_t)2 * c->max_tiles * sizeof(uint64_t))) != hipSuccess ||
+        (e = hipMemset(c->stats, 0, sizeof(DevStats))) != hipSuccess)
+        return bail(pt::fail(PT_ERR_HIP, std::string("hipMemset: ") + hipGetErrorString(e)));
+    // hit SoA + sort buffers (material-sorted mode)
+    {
+        float** f[6] = {&A.hit.t, &A.hit.nx, &A.hit.ny, &A.hit.nz, &A.hit.u, &A.hit.v};
+        for (auto* p : f)
+            if (int rc = c->alloc(p, (size_t)P)) return bail(rc);
+        if (int rc = c->alloc(&A.hit.mat, (size_t)P)) return bail(rc);
+        c->max_t64 = (int)((P + 63) / 64);
+        const size_t hn = (size_t)c->max_t64 * c->nmats;
+        if (int rc = c->alloc(&c->keys, (size_t)P)) return bail(rc);
+        if (int rc = c->alloc(&c->hist, hn)) return bail(rc);
+        if (int rc = c->alloc(&c->offs, hn)) return bail(rc);
+        if (int rc = c->alloc(&c->perm, (size_t)P)) return bail(rc);
+        uint8_t* ws;
+        if (int rc = c->alloc(&ws, sc_workspace_bytes((int64_t)hn))) return bail(rc);
+        c->scan_ws = ws;
+    }
+    // persistent grid: enough workgroups to fill every CU at the kernel's occupancy
+    int cus = 256, per_cu = 0;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_bounce<false, true>, kBlock, 0) != hipSuccess || per_cu <= 0)
+        per_cu = 4;
+    per_cu = std::min(per_cu, 8);
+    c->grid_persistent = std::max(1, std::min(c->max_tiles, cus * per_cu));
+    *out = c;
+    return PT_OK;
+}
+
+int pt_destroy(pt_ctx* c) {
+    if (c) {
+        (void)hipDeviceSynchronize();
+        delete c;
+    }
+    return PT_OK;
+}
+
+int pt_set_flags(pt_ctx* c, const pt_flags* f) {
+    if (!c || !f) return pt::fail(PT_ERR_ARG, "null argument");
+    set_flags_dev(c, *f);
+    return PT_OK;
+}
+
+int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
+    if (!c) return pt::fail(PT_ERR_ARG, "null context");
+    if (iter_first < 0) return pt::fail(PT_ERR_ARG, "iteration index must be >= 0");
+    hipStream_t st = (hipStream_t)stream;
+    KArgs A = c->args;
+    A.tile.iter_first = iter_first;
+    const bool spp1 = A.tile.spp == 1;
+    const bool sorted = c->flags.sort_by_material != 0;
+    int cur = 0;   // paths start in buf[0]
+    for (int b = 0; b < c->depth; ++b) {
+        A.in = c->buf[cur];
+        A.out = c->buf[cur ^ 1];
+        A.bounce = b;
+        A.n_fixed = b == 0 ? A.tile.P : -1;
+        if (!sorted) {
+            int rc;
+            if (b == 0) rc = spp1 ? launch_k(c, k_bounce<true, true>, c->grid_persistent, st, true, A)
+                                  : launch_k(c, k_bounce<true, false>, c->grid_persistent, st, true, A);
+            else rc = spp1 ? launch_k(c, k_bounce<false, true>, c->grid_persistent, st, true, A)
+                           : launch_k(c, k_bounce<false, false>, c->grid_persistent, st, true, A);
+            if (rc) return rc;
+        } else {
+            if (b == 0) {
+                if (int rc = launch_k(c, k_raygen, std::min(c->max_tiles, 4096), st, false, A)) return rc;
+            }
+            const int g64 = std::min((c->max_t64 + 3) / 4, 8192);
+            hipLaunchKernelGGL(k_isect_hist, dim3(g64), dim3(kBlock), 0, st, A, c->keys, c->hist, c->max_t64);
+            HIP_TRY(hipGetLastError());
+            const int64_t hn = (int64_t)c->max_t64 * c->nmats;
+            if (sc_scan_exclusive_i32(c->hist, c->offs, hn, c->scan_ws, st) != SC_OK)
+                return pt::fail(PT_ERR_HIP, std::string("material scan: ") + sc_last_error());
+            hipLaunchKernelGGL(k_sort_scatter, dim3(g64), dim3(kBlock), 0, st, A, c->keys, c->offs, c->perm, c->max_t64);
+            HIP_TRY(hipGetLastError());
+            A.perm = c->perm;
+            int rc = spp1 ? launch_k(c, k_shade_sorted<true>, c->grid_persistent, st, true, A)
+                          : launch_k(c, k_shade_sorted<false>, c->grid_persistent, st, true, A);
+            if (rc) return rc;
+        }
+        A.parity ^= 1;
+        cur ^= 1;
+    }
+    c->args.parity = A.parity;
+    if (!spp1) {
+        const int npix = A.tile.npix;
+        hipLaunchKernelGGL(k_finalize_spp, dim3(std::min((npix + 255) / 256, 4096)), dim3(256), 0, st, A.image,
+                           (const float*)A.colbuf, npix, A.tile.spp);
+        HIP_TRY(hipGetLastError());
+    }
+    hipLaunchKernelGGL(k_stats_pass, dim3(1), dim3(1), 0, st, c->stats);
+    HIP_TRY(hipGetLastError());
+    return PT_OK;
+}
+
+int pt_preview_rgba(pt_ctx* c, int32_t iter, uint8_t* d_rgba, void* stream) {
+    if (!c || !d_rgba || iter <= 0) return pt::fail(PT_ERR_ARG, "bad argument");
+    const int npix = c->args.tile.npix;
+    hipLaunchKernelGGL(k_preview, dim3(std::min((npix + 255) / 256, 4096)), dim3(256), 0, (hipStream_t)stream,
+                       (const float*)c->args.image, d_rgba, npix, iter);
+    HIP_TRY(hipGetLastError());
+    return PT_OK;
+}
+
+int pt_tile_info(const pt_ctx* c, int32_t* width, int32_t* rows, int32_t* npix, int32_t* npaths) {
+    if (!c) return pt::fail(PT_ERR_ARG, "null context");
+    const TileDev& T = c->args.tile;
+    if (width) *width = T.W;
+    if (rows) *rows = T.npix / T.W;
+    if (npix) *npix = T.npix;
+    if (npaths) *npaths = T.P;
+    return PT_OK;
+}
+
+int pt_get_image(pt_ctx* c, float* host_rgb) {
+    if (!c || !host_rgb) return pt::fail(PT_ERR_ARG, "null argument");
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(host_rgb, c->args.image, (size_t)c->args.tile.npix * 3 * sizeof(float), hipMemcpyDeviceToHost));
+    return PT_OK;
+}
+
+int pt_copy_image(pt_ctx* c, float* d_rgb, void* stream) {
+    if (!c || !d_rgb) return pt::fail(PT_ERR_ARG, "null argument");
+    HIP_TRY(hipMemcpyAsync(d_rgb, c->args.image, (size_t)c->args.tile.npix * 3 * sizeof(float),
+                           hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    return PT_OK;
+}
+
+int pt_reset_image(pt_ctx* c, void* stream) {
+    if (!c) return pt::fail(PT_ERR_ARG, "null context");
+    HIP_TRY(hipMemsetAsync(c->args.image, 0, (size_t)c->args.tile.npix * 3 * sizeof(float), (hipStream_t)stream));
+    return PT_OK;
+}
+
+int pt_stats(pt_ctx* c, pt_stats_t* out) {
+    if (!c || !out) return pt::fail(PT_ERR_ARG, "null argument");
+    HIP_TRY(hipDeviceSynchronize());
+    DevStats s;
+    HIP_TRY(hipMemcpy(&s, c->stats, sizeof s, hipMemcpyDeviceToHost));
+    std::memset(out, 0, sizeof *out);
+    out->segments = s.segments;
+    out->passes = s.passes;
+    for (int k = 0; k < 64; ++k) out->bounce_live[k] = s.bounce_live[k];
+    out->emissive_hits = s.emissive_hits;
+    out->device_error = s.err;
+    return s.err ? pt::fail(PT_ERR_DEVICE, "device-side look-back spin bound was hit") : PT_OK;
+}
+
+int pt_profile_enable(pt_ctx* c, int32_t on) {
+    if (!c) return pt::fail(PT_ERR_ARG, "null context");
+    c->profiling = on != 0;
+    return PT_OK;
+}
+
+int pt_profile_read(pt_ctx* c, double* bounce_ms, uint64_t* bounce_launches, double* total_ms) {
+    if (!c) return pt::fail(PT_ERR_ARG, "null context");
+    HIP_TRY(hipDeviceSynchronize());
+    for (auto& ev : c->events) {
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, ev.a, ev.b));
+        c->total_ms += ms;
+        if (ev.bounce) { c->bounce_ms += ms; c->bounce_launches += 1; }
+        (void)hipEventDestroy(ev.a);
+        (void)hipEventDestroy(ev.b);
+    }
+    c->events.clear();
+    if (bounce_ms) *bounce_ms = c->bounce_ms;
+    if (bounce_launches) *bounce_launches = c->bounce_launches;
+    if (total_ms) *total_ms = c->total_ms;
+    return PT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,322 @@
+// MI355X stream compaction: single-pass exclusive scan / compaction / stable partition of int32.
+//
+// Replaces StreamCompaction::Efficient (path_tracer/stream_compaction/efficient.cu:46-219) and
+// Common::kernMapToBoolean / kernScatter (common.cu:25-46).  The reference runs a recursive
+// Blelloch scan with 64 elements per block (blockDim = warpSize = 32), pads n to a power of two
+// and allocates/frees device memory on every call.  Here one launch streams each element once:
+//   tile = 256 threads x 4 x int4 = 4096 elements, loaded as wave-contiguous 16-byte vectors
+//   (chunk k of a tile is 1 KiB per wave-instruction), per-thread 4-element scan, wave64 DPP scan
+//   of the per-thread sums, 16 wave totals through LDS, then a decoupled look-back across tiles
+//   (lookback.h).  Algorithmic traffic: 8 B/element for scan (4 read + 4 write), 4 B/element +
+//   4 B/kept for compaction.
+#include <hip/hip_runtime.h>
+#include <mutex>
+#include <string>
+#include <vector>
+#include <cstring>
+
+#include "lookback.h"
+#include "../../include/sc_amd.h"
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kChunks = 4;                       // int4 chunks per thread
+constexpr int kTile = kThreads * kChunks * 4;    // 4096 elements
+constexpr size_t kCtlBytes = 256;                // ticket, error word (padded)
+
+thread_local std::string g_err;
+thread_local float g_timer_ms = 0.f;
+
+int fail(int code, const std::string& msg) { g_err = msg; return code; }
+int hip_fail(hipError_t e, const char* where) {
+    return fail(SC_ERR_HIP, std::string(where) + ": " + hipGetErrorString(e));
+}
+
+enum Mode { kScan = 0, kCompact = 1, kPartition = 2 };
+
+template <int MODE, bool ALIGNED>
+__global__ __launch_bounds__(kThreads) void k_scan_tiles(const int32_t* __restrict__ in,
+                                                         int32_t* __restrict__ out, int64_t n,
+                                                         uint64_t* __restrict__ status,
+                                                         uint32_t* __restrict__ ctl,
+                                                         int64_t* __restrict__ d_count,
+                                                         int32_t* __restrict__ dead) {
+    __shared__ uint32_t s_tile;
+    __shared__ uint32_t s_wsum[kChunks][4];
+    __shared__ uint32_t s_excl;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid == 0) s_tile = atomicAdd(&ctl[0], 1u);
+    __syncthreads();
+    const int tile = (int)s_tile;
+    const int64_t base = (int64_t)tile * kTile;
+    const bool full = base + kTile <= n;
+
+    int32_t v[kChunks][4];
+#pragma unroll
+    for (int k = 0; k < kChunks; ++k) {
+        const int64_t e0 = base + (int64_t)k * (kThreads * 4) + 4 * tid;
+        if (ALIGNED && full) {
+            const int4 q = *reinterpret_cast<const int4*>(in + e0);
+            v[k][0] = q.x; v[k][1] = q.y; v[k][2] = q.z; v[k][3] = q.w;
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[k][e] = (e0 + e < n) ? in[e0 + e] : 0;
+        }
+    }
+    uint32_t s[kChunks], incl[kChunks];
+#pragma unroll
+    for (int k = 0; k < kChunks; ++k) {
+        if (MODE == kScan)
+            s[k] = ((uint32_t)v[k][0] + (uint32_t)v[k][1]) + ((uint32_t)v[k][2] + (uint32_t)v[k][3]);
+        else
+            s[k] = (uint32_t)(v[k][0] != 0) + (uint32_t)(v[k][1] != 0) + (uint32_t)(v[k][2] != 0) +
+                   (uint32_t)(v[k][3] != 0);
+        incl[k] = lb::wave_inclusive_scan(s[k]);
+        if (lane == 63) s_wsum[k][wave] = incl[k];
+    }
+    __syncthreads();
+    uint32_t off[kChunks];
+    uint32_t run = 0;
+#pragma unroll
+    for (int k = 0; k < kChunks; ++k) {
+        uint32_t before = 0;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            const uint32_t x = s_wsum[k][w];
+            before += (w < wave) ? x : 0u;
+        }
+        off[k] = run + before;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) run += s_wsum[k][w];
+    }
+    const uint32_t total = run;
+    if (wave == 0) {
+        uint32_t excl = 0;
+        if (tile == 0) {
+            if (lane == 0) lb::publish(status, 0, lb::kFlagPre, total);
+        } else {
+            if (lane == 0) lb::publish(status, tile, lb::kFlagAgg, total);
+            excl = lb::lookback(status, tile, lane, &ctl[1]);
+            if (lane == 0) lb::publish(status, tile, lb::kFlagPre, excl + total);
+        }
+        if (lane == 0) s_excl = excl;
+    }
+    __syncthreads();
+    const uint32_t excl = s_excl;
+#pragma unroll
+    for (int k = 0; k < kChunks; ++k) {
+        const int64_t e0 = base + (int64_t)k * (kThreads * 4) + 4 * tid;
+        uint32_t run_k = excl + off[k] + (incl[k] - s[k]);
+        if (MODE == kScan) {
+            int32_t o[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) { o[e] = (int32_t)run_k; run_k += (uint32_t)v[k][e]; }
+            if (ALIGNED && full) {
+                *reinterpret_cast<int4*>(out + e0) = make_int4(o[0], o[1], o[2], o[3]);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if (e0 + e < n) out[e0 + e] = o[e];
+            }
+        } else if (MODE == kCompact) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if (v[k][e] != 0) out[run_k++] = v[k][e];
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int64_t idx = e0 + e;
+                if (idx < n) {
+                    if (v[k][e] != 0) out[run_k++] = (int32_t)idx;
+                    else dead[idx - (int64_t)run_k] = (int32_t)idx;
+                }
+            }
+        }
+    }
+    if (MODE != kScan && tid == 0 && base + kTile >= n) *d_count = (int64_t)(excl + total);
+}
+
+__global__ void k_append_dead(const int32_t* __restrict__ dead, int32_t* __restrict__ perm,
+                              int64_t n, const int64_t* __restrict__ d_live) {
+    const int64_t live = *d_live;
+    const int64_t ndead = n - live;
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < ndead;
+         j += (int64_t)gridDim.x * blockDim.x)
+        perm[live + j] = dead[j];
+}
+
+size_t status_bytes(int64_t n) {
+    const int64_t tiles = (n + kTile - 1) / kTile;
+    return (size_t)(tiles > 0 ? tiles : 1) * sizeof(uint64_t);
+}
+
+struct Workspace {
+    void* ptr = nullptr;
+    size_t bytes = 0;
+};
+std::mutex g_ws_mu;
+std::vector<Workspace> g_ws;   // per device
+
+int get_cached_ws(size_t need, void** out) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
+    std::lock_guard<std::mutex> lk(g_ws_mu);
+    if ((int)g_ws.size() <= dev) g_ws.resize(dev + 1);
+    Workspace& w = g_ws[dev];
+    if (w.bytes < need) {
+        if (w.ptr) (void)hipFree(w.ptr);
+        w.ptr = nullptr;
+        w.bytes = 0;
+        e = hipMalloc(&w.ptr, need);
+        if (e != hipSuccess) return hip_fail(e, "hipMalloc(workspace)");
+        w.bytes = need;
+    }
+    *out = w.ptr;
+    return SC_OK;
+}
+
+template <int MODE>
+int launch(const int32_t* d_in, int32_t* d_out, int64_t n, int64_t* d_count, void* workspace,
+           hipStream_t stream) {
+    if (n < 0 || n > 0x7fffffffLL) return fail(SC_ERR_ARG, "n out of range [0, 2^31-1]");
+    if (n > 0 && (!d_in || !d_out)) return fail(SC_ERR_ARG, "null pointer");
+    if (MODE != kScan && !d_count) return fail(SC_ERR_ARG, "null count pointer");
+    const size_t need = sc_workspace_bytes(n);
+    if (!workspace) {
+        const int rc = get_cached_ws(need, &workspace);
+        if (rc) return rc;
+    }
+    uint8_t* ws = static_cast<uint8_t*>(workspace);
+    uint32_t* ctl = reinterpret_cast<uint32_t*>(ws);
+    uint64_t* status = reinterpret_cast<uint64_t*>(ws + kCtlBytes);
+    int32_t* dead = reinterpret_cast<int32_t*>(ws + kCtlBytes + status_bytes(n));
+    if (n == 0) {
+        if (MODE != kScan) {
+            hipError_t e = hipMemsetAsync(d_count, 0, sizeof(int64_t), stream);
+            if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync");
+        }
+        return SC_OK;
+    }
+    hipError_t e = hipMemsetAsync(ws, 0, kCtlBytes + status_bytes(n), stream);
+    if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(workspace)");
+    const int64_t tiles = (n + kTile - 1) / kTile;
+    const bool aligned = ((reinterpret_cast<uintptr_t>(d_in) | reinterpret_cast<uintptr_t>(d_out)) & 15) == 0;
+    if (aligned)
+        hipLaunchKernelGGL((k_scan_tiles<MODE, true>), dim3((unsigned)tiles), dim3(kThreads), 0, stream,
+                           d_in, d_out, n, status, ctl, d_count, dead);
+    else
+        hipLaunchKernelGGL((k_scan_tiles<MODE, false>), dim3((unsigned)tiles), dim3(kThreads), 0, stream,
+                           d_in, d_out, n, status, ctl, d_count, dead);
+    e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "k_scan_tiles launch");
+    if (MODE == kPartition) {
+        const int64_t blocks = std::min<int64_t>((n + 255) / 256, 4096);
+        hipLaunchKernelGGL(k_append_dead, dim3((unsigned)blocks), dim3(256), 0, stream, dead, d_out, n,
+                           (const int64_t*)d_count);
+        e = hipGetLastError();
+        if (e != hipSuccess) return hip_fail(e, "k_append_dead launch");
+    }
+    return SC_OK;
+}
+
+// Host-pointer helper buffers (per device).
+struct HostBufs {
+    int32_t* in = nullptr;
+    int32_t* out = nullptr;
+    int64_t* cnt = nullptr;
+    int64_t cap = 0;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+};
+std::mutex g_hb_mu;
+std::vector<HostBufs> g_hb;
+
+int get_host_bufs(int64_t n, HostBufs** out) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
+    if ((int)g_hb.size() <= dev) g_hb.resize(dev + 1);
+    HostBufs& b = g_hb[dev];
+    if (!b.ev0) {
+        if ((e = hipEventCreate(&b.ev0)) != hipSuccess) return hip_fail(e, "hipEventCreate");
+        if ((e = hipEventCreate(&b.ev1)) != hipSuccess) return hip_fail(e, "hipEventCreate");
+        if ((e = hipMalloc(&b.cnt, sizeof(int64_t))) != hipSuccess) return hip_fail(e, "hipMalloc");
+    }
+    if (b.cap < n) {
+        if (b.in) (void)hipFree(b.in);
+        if (b.out) (void)hipFree(b.out);
+        b.in = b.out = nullptr;
+        b.cap = 0;
+        const size_t bytes = (size_t)(n > 0 ? n : 1) * sizeof(int32_t);
+        if ((e = hipMalloc(&b.in, bytes)) != hipSuccess) return hip_fail(e, "hipMalloc(in)");
+        if ((e = hipMalloc(&b.out, bytes)) != hipSuccess) return hip_fail(e, "hipMalloc(out)");
+        b.cap = n;
+    }
+    *out = &b;
+    return SC_OK;
+}
+
+template <int MODE>
+int host_op(int n, int* odata, const int* idata, int* count_out) {
+    if (n < 0) return fail(SC_ERR_ARG, "n < 0");
+    if (n > 0 && (!odata || !idata)) return fail(SC_ERR_ARG, "null pointer");
+    std::lock_guard<std::mutex> lk(g_hb_mu);
+    HostBufs* b = nullptr;
+    int rc = get_host_bufs(n, &b);
+    if (rc) return rc;
+    hipError_t e;
+    if (n > 0 && (e = hipMemcpy(b->in, idata, (size_t)n * 4, hipMemcpyHostToDevice)) != hipSuccess)
+        return hip_fail(e, "hipMemcpy H2D");
+    void* ws = nullptr;
+    if ((rc = get_cached_ws(sc_workspace_bytes(n), &ws))) return rc;
+    (void)hipEventRecord(b->ev0, nullptr);
+    rc = launch<MODE>(b->in, b->out, n, b->cnt, ws, nullptr);
+    if (rc) return rc;
+    (void)hipEventRecord(b->ev1, nullptr);
+    if ((e = hipEventSynchronize(b->ev1)) != hipSuccess) return hip_fail(e, "hipEventSynchronize");
+    (void)hipEventElapsedTime(&g_timer_ms, b->ev0, b->ev1);
+    int64_t cnt = n;
+    if (MODE != kScan) {
+        if ((e = hipMemcpy(&cnt, b->cnt, sizeof cnt, hipMemcpyDeviceToHost)) != hipSuccess)
+            return hip_fail(e, "hipMemcpy count");
+        if (count_out) *count_out = (int)cnt;
+    }
+    if (cnt > 0 && (e = hipMemcpy(odata, b->out, (size_t)cnt * 4, hipMemcpyDeviceToHost)) != hipSuccess)
+        return hip_fail(e, "hipMemcpy D2H");
+    return SC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* sc_last_error(void) { return g_err.c_str(); }
+
+size_t sc_workspace_bytes(int64_t n) {
+    return kCtlBytes + status_bytes(n) + (size_t)(n > 0 ? n : 0) * sizeof(int32_t);
+}
+
+int sc_scan_exclusive_i32(const int32_t* d_in, int32_t* d_out, int64_t n, void* workspace, void* stream) {
+    return launch<kScan>(d_in, d_out, n, nullptr, workspace, (hipStream_t)stream);
+}
+
+int sc_compact_i32(const int32_t* d_in, int32_t* d_out, int64_t n, int64_t* d_count, void* workspace,
+                   void* stream) {
+    return launch<kCompact>(d_in, d_out, n, d_count, workspace, (hipStream_t)stream);
+}
+
+int sc_partition_i32(const int32_t* d_flags, int32_t* d_perm, int64_t n, int64_t* d_live, void* workspace,
+                     void* stream) {
+    return launch<kPartition>(d_flags, d_perm, n, d_live, workspace, (hipStream_t)stream);
+}
+
+int sc_efficient_scan(int n, int* odata, const int* idata) { return host_op<kScan>(n, odata, idata, nullptr); }
+
+int sc_efficient_compact(int n, int* odata, const int* idata, int* count_out) {
+    return host_op<kCompact>(n, odata, idata, count_out);
+}
+
+float sc_timer_gpu_ms(void) { return g_timer_ms; }
+
+}  // extern "C"

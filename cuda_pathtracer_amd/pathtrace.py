@@ -1,0 +1,307 @@
+"""Python mirror of the reference's render boundary, backed by libpt_amd.so.
+
+Reference interfaces (path_tracer/src):
+  Scene::Scene(filename) / loadFromJSON           scene.h:17-35, scene.cpp:16-219   -> Scene(path)
+  GuiDataContainer (runtime flags)                utilities.h:17-34                 -> GuiDataContainer
+  InitDataContainer / pathtraceInit / pathtraceFree / pathtrace   pathtrace.h:6-9   -> same names
+  runCuda's iteration loop + saveImage            main.cpp:88-168                   -> render(), save_image()
+The reference keeps one implicit global render (file-static device buffers); the module-level
+functions below reproduce that, while PathTracer objects allow any number of independent
+contexts (one per GPU / pixel tile).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import time
+from dataclasses import dataclass
+from pathlib import Path
+
+import numpy as np
+
+from . import _native as N
+from ._native import check_pt, lib
+
+SPHERE, CUBE, MESH = 0, 1, 2
+
+
+class GuiDataContainer:
+    """Runtime flags with the reference defaults (utilities.h:17-34)."""
+
+    def __init__(self):
+        self.TracedDepth = 0
+        self.russianRoulette = True
+        self.useBVHtree = True
+        self.useBBox = True
+        self.sortbyMaterial = False
+        self.useThrustPartition = False
+        self.SSAA = True
+        self.DoF = True
+        self.aperture = 0.1
+        self.focal_len = 10.0
+
+    def to_c(self) -> N.Flags:
+        f = N.Flags()
+        f.russian_roulette = int(bool(self.russianRoulette))
+        f.use_bvh = int(bool(self.useBVHtree))
+        f.use_bbox = int(bool(self.useBBox))
+        f.sort_by_material = int(bool(self.sortbyMaterial))
+        f.use_thrust_partition = int(bool(self.useThrustPartition))
+        f.ssaa = int(bool(self.SSAA))
+        f.dof = int(bool(self.DoF))
+        f.aperture = float(self.aperture)
+        f.focal_dist = float(self.focal_len)
+        return f
+
+
+@dataclass
+class RenderState:
+    iterations: int
+    traceDepth: int
+    imageName: str
+
+
+def _load_texture_pixels(path: str) -> tuple[int, int, int, bytes]:
+    # The reference decodes with stb_image (scene.cpp:61-71).  Decoding is host-side I/O, not
+    # the hot path; PIL is used when present.
+    from PIL import Image as _PILImage  # noqa: N814
+    im = _PILImage.open(path)
+    if im.mode not in ("RGB", "RGBA", "L"):
+        im = im.convert("RGB")
+    comps = {"RGB": 3, "RGBA": 4, "L": 1}[im.mode]
+    return im.width, im.height, comps, im.tobytes()
+
+
+class Scene:
+    """Scene description; `Scene(path)` loads a reference JSON scene file."""
+
+    def __init__(self, filename: str | os.PathLike | None = None):
+        self._h = C.c_void_p()
+        L = lib()
+        if filename is None:
+            check_pt(L.pt_scene_create(C.byref(self._h)))
+            return
+        check_pt(L.pt_scene_load_json(str(filename).encode(), C.byref(self._h)))
+        _, _, _, _, ntex = self.counts()
+        buf = C.create_string_buffer(4096)
+        for t in range(ntex):
+            check_pt(L.pt_scene_texture_path(self._h, t, buf, 4096))
+            w, h, comps, data = _load_texture_pixels(buf.value.decode())
+            check_pt(L.pt_scene_set_texture_pixels(self._h, t, w, h, comps, data))
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                lib().pt_scene_free(h)
+            except Exception:
+                pass
+            self._h = None
+
+    @property
+    def handle(self) -> C.c_void_p:
+        return self._h
+
+    # -- programmatic construction --
+    def add_material(self, rgb=(0, 0, 0), specrgb=None, specex=1.0, reflective=0.0, refractive=0.0, ior=0.0,
+                     emittance=0.0, texture_id=-1) -> int:
+        m = N.Material()
+        m.color[:] = [float(v) for v in rgb]
+        m.spec_color[:] = [float(v) for v in (specrgb if specrgb is not None else rgb)]
+        m.spec_exponent = specex
+        m.has_reflective = reflective
+        m.has_refractive = refractive
+        m.ior = ior
+        m.emittance = emittance
+        m.texture_id = texture_id
+        out = C.c_int32()
+        check_pt(lib().pt_scene_add_material(self._h, C.byref(m), C.byref(out)))
+        return out.value
+
+    def add_geom(self, type_: int, material: int, trans, rotat, scale) -> int:
+        out = C.c_int32()
+        check_pt(lib().pt_scene_add_geom(self._h, type_, material, N.f3(trans), N.f3(rotat), N.f3(scale),
+                                         C.byref(out)))
+        return out.value
+
+    def set_camera(self, res, fovy, eye, lookat, up=(0, 1, 0)) -> None:
+        check_pt(lib().pt_scene_set_camera(self._h, int(res[0]), int(res[1]), float(fovy), N.f3(eye), N.f3(lookat),
+                                           N.f3(up)))
+
+    def set_render(self, iterations: int, depth: int, file: str = "render") -> None:
+        check_pt(lib().pt_scene_set_render(self._h, iterations, depth, file.encode()))
+
+    def finalize(self) -> None:
+        check_pt(lib().pt_scene_finalize(self._h))
+
+    # -- inspection --
+    def counts(self):
+        v = [C.c_int32() for _ in range(5)]
+        check_pt(lib().pt_scene_counts(self._h, *[C.byref(x) for x in v]))
+        return tuple(x.value for x in v)
+
+    def camera(self) -> N.Camera:
+        cam = N.Camera()
+        check_pt(lib().pt_scene_get_camera(self._h, C.byref(cam)))
+        return cam
+
+    def state(self) -> RenderState:
+        it, d = C.c_int32(), C.c_int32()
+        buf = C.create_string_buffer(1024)
+        check_pt(lib().pt_scene_get_render(self._h, C.byref(it), C.byref(d), buf, 1024))
+        return RenderState(it.value, d.value, buf.value.decode())
+
+    def geoms(self):
+        ng = self.counts()[0]
+        arr = (N.Geom * max(ng, 1))()
+        lib().pt_scene_get_geoms(self._h, arr, ng)
+        return list(arr)[:ng]
+
+    def materials(self):
+        nm = self.counts()[1]
+        arr = (N.Material * max(nm, 1))()
+        lib().pt_scene_get_materials(self._h, arr, nm)
+        return list(arr)[:nm]
+
+
+def _stream_ptr(stream):
+    if stream is None:
+        return None
+    return int(getattr(stream, "cuda_stream", stream))
+
+
+class PathTracer:
+    """One render context (pathtraceInit ... pathtraceFree) for a pixel tile of the image.
+
+    rank/world select the rows y % world == rank; spp iterations are traced per pass.
+    """
+
+    def __init__(self, scene: Scene, gui: GuiDataContainer | None = None, rank: int = 0, world: int = 1,
+                 spp: int = 1):
+        self.scene = scene
+        self.gui = gui or GuiDataContainer()
+        self._h = C.c_void_p()
+        flags = self.gui.to_c()
+        shard = N.Shard(rank, world, spp, 0)
+        check_pt(lib().pt_create(scene.handle, C.byref(flags), C.byref(shard), C.byref(self._h)))
+        w, rows, npix, npaths = (C.c_int32() for _ in range(4))
+        check_pt(lib().pt_tile_info(self._h, C.byref(w), C.byref(rows), C.byref(npix), C.byref(npaths)))
+        self.width, self.rows, self.npix, self.npaths = w.value, rows.value, npix.value, npaths.value
+        self.rank, self.world, self.spp = rank, world, spp
+
+    def free(self) -> None:
+        if self._h is not None and self._h.value:
+            check_pt(lib().pt_destroy(self._h))
+        self._h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+    def set_flags(self, gui: GuiDataContainer) -> None:
+        self.gui = gui
+        check_pt(lib().pt_set_flags(self._h, C.byref(gui.to_c())))
+
+    def render_pass(self, iter_first: int, stream=None) -> None:
+        """pathtrace(): iterations [iter_first, iter_first + spp) for this tile, asynchronous."""
+        check_pt(lib().pt_render_pass(self._h, int(iter_first), _stream_ptr(stream)))
+
+    def image(self) -> np.ndarray:
+        """Tile accumulator (sum of radiance over iterations), shape (rows, width, 3) float32."""
+        out = np.empty((self.rows, self.width, 3), dtype=np.float32)
+        check_pt(lib().pt_get_image(self._h, out.ctypes.data))
+        return out
+
+    def copy_image_to(self, dst_ptr: int, stream=None) -> None:
+        check_pt(lib().pt_copy_image(self._h, C.c_void_p(dst_ptr), _stream_ptr(stream)))
+
+    def reset_image(self, stream=None) -> None:
+        check_pt(lib().pt_reset_image(self._h, _stream_ptr(stream)))
+
+    def preview_rgba(self, iteration: int, dst_ptr: int, stream=None) -> None:
+        check_pt(lib().pt_preview_rgba(self._h, int(iteration), C.c_void_p(dst_ptr), _stream_ptr(stream)))
+
+    def stats(self) -> dict:
+        s = N.Stats()
+        check_pt(lib().pt_stats(self._h, C.byref(s)))
+        depth = self.scene.state().traceDepth
+        return {"segments": int(s.segments), "passes": int(s.passes),
+                "bounce_live": [int(s.bounce_live[k]) for k in range(depth)],
+                "emissive_hits": int(s.emissive_hits)}
+
+    def profile(self, on: bool = True) -> None:
+        check_pt(lib().pt_profile_enable(self._h, int(on)))
+
+    def profile_read(self) -> dict:
+        bms, n, tms = C.c_double(), C.c_uint64(), C.c_double()
+        check_pt(lib().pt_profile_read(self._h, C.byref(bms), C.byref(n), C.byref(tms)))
+        return {"bounce_ms": bms.value, "bounce_launches": int(n.value), "total_ms": tms.value}
+
+
+def tonemap(image: np.ndarray, samples: float) -> np.ndarray:
+    """saveImage + Image::savePNG pixel math (x-mirrored, clamp, x255, truncation) -> (H, W, 3) uint8."""
+    img = np.ascontiguousarray(image, dtype=np.float32)
+    H, W = img.shape[0], img.shape[1]
+    out = np.empty((H, W, 3), dtype=np.uint8)
+    check_pt(lib().pt_tonemap(img.ctypes.data, W, H, float(samples), out.ctypes.data))
+    return out
+
+
+def save_image(path: str, image: np.ndarray, samples: float) -> str:
+    img = np.ascontiguousarray(image, dtype=np.float32)
+    check_pt(lib().pt_save_png(str(path).encode(), img.ctypes.data, img.shape[1], img.shape[0], float(samples)))
+    return str(path)
+
+
+def render(scene_path: str, iterations: int | None = None, out_dir: str | None = None,
+           gui: GuiDataContainer | None = None) -> tuple[np.ndarray, str | None]:
+    """Headless runCuda loop (main.cpp:114-168): ITERATIONS passes, then saveImage."""
+    scene = Scene(scene_path)
+    st = scene.state()
+    iters = iterations if iterations is not None else st.iterations
+    pt = PathTracer(scene, gui)
+    for it in range(1, iters + 1):
+        pt.render_pass(it)
+    img = pt.image()
+    path = None
+    if out_dir is not None:
+        stamp = time.strftime("%Y-%m-%d_%H-%M-%Sz", time.gmtime())
+        path = str(Path(out_dir) / f"{st.imageName}.{stamp}.{iters}samp.png")
+        save_image(path, img, iters)
+    pt.free()
+    return img, path
+
+
+# ---- the reference's global-state API (pathtrace.h:6-9) ------------------------------------
+_GLOBAL: dict = {"gui": None, "ctx": None}
+
+
+def InitDataContainer(gui: GuiDataContainer) -> None:  # noqa: N802
+    _GLOBAL["gui"] = gui
+    if _GLOBAL["ctx"] is not None:
+        _GLOBAL["ctx"].set_flags(gui)
+
+
+def pathtraceInit(scene: Scene) -> None:  # noqa: N802
+    pathtraceFree()
+    _GLOBAL["ctx"] = PathTracer(scene, _GLOBAL["gui"])
+
+
+def pathtraceFree() -> None:  # noqa: N802
+    if _GLOBAL["ctx"] is not None:
+        _GLOBAL["ctx"].free()
+    _GLOBAL["ctx"] = None
+
+
+def pathtrace(pbo_ptr: int | None, frame: int, iteration: int) -> None:
+    """One iteration; writes the RGBA preview into pbo_ptr (device) when given."""
+    ctx = _GLOBAL["ctx"]
+    if ctx is None:
+        raise RuntimeError("pathtraceInit() was not called")
+    if _GLOBAL["gui"] is not None:
+        ctx.set_flags(_GLOBAL["gui"])
+    ctx.render_pass(iteration)
+    if pbo_ptr:
+        ctx.preview_rgba(iteration, pbo_ptr)

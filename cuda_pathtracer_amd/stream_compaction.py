@@ -1,0 +1,108 @@
+"""Python mirror of the reference's StreamCompaction API, backed by the HIP kernels.
+
+Reference: path_tracer/stream_compaction/{efficient,common}.{h,cu}.
+  StreamCompaction::Efficient::scan(n, odata, idata)     -> Efficient.scan
+  StreamCompaction::Efficient::compact(n, odata, idata)  -> Efficient.compact
+  StreamCompaction::Efficient::timer()                   -> Efficient.timer()
+The host-array calls keep the reference semantics (host arrays in, host arrays out, GPU time of
+the device work only).  The device-tensor functions (scan_device, compact_device,
+partition_device) take torch tensors already resident on the GPU and never synchronise.
+StreamCompaction::CPU is deliberately absent: the CPU version is the test oracle (oracle/), and
+this package has no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from ._native import check_sc, lib
+
+
+class _Timer:
+    """PerformanceTimer (common.h:46-130), GPU side only."""
+
+    def getGpuElapsedTimeForPreviousOperation(self) -> float:  # noqa: N802 (reference name)
+        return float(lib().sc_timer_gpu_ms())
+
+
+_TIMER = _Timer()
+
+
+def _i32(a: np.ndarray, name: str) -> np.ndarray:
+    if not isinstance(a, np.ndarray) or a.dtype != np.int32 or not a.flags.c_contiguous:
+        raise TypeError(f"{name} must be a C-contiguous numpy int32 array")
+    return a
+
+
+class Efficient:
+    @staticmethod
+    def timer() -> _Timer:
+        return _TIMER
+
+    @staticmethod
+    def scan(n: int, odata: np.ndarray, idata: np.ndarray) -> None:
+        """Exclusive prefix sum of idata[:n] into odata[:n] (int32, wrapping)."""
+        _i32(odata, "odata"); _i32(idata, "idata")
+        if n < 0 or n > len(idata) or n > len(odata):
+            raise ValueError("n out of range")
+        check_sc(lib().sc_efficient_scan(n, odata.ctypes.data, idata.ctypes.data))
+
+    @staticmethod
+    def compact(n: int, odata: np.ndarray, idata: np.ndarray) -> int:
+        """Keep the non-zero elements of idata[:n] in order; returns how many were kept."""
+        _i32(odata, "odata"); _i32(idata, "idata")
+        if n < 0 or n > len(idata) or n > len(odata):
+            raise ValueError("n out of range")
+        cnt = C.c_int32(0)
+        check_sc(lib().sc_efficient_compact(n, odata.ctypes.data, idata.ctypes.data, C.byref(cnt)))
+        return int(cnt.value)
+
+
+def _stream_ptr(stream) -> int:
+    if stream is None:
+        import torch
+        return torch.cuda.current_stream().cuda_stream
+    return int(getattr(stream, "cuda_stream", stream))
+
+
+def _check_dev_i32(t, name: str):
+    import torch
+    if not (isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == torch.int32 and t.is_contiguous()):
+        raise TypeError(f"{name} must be a contiguous int32 CUDA tensor")
+
+
+def scan_device(d_in, d_out=None, stream=None):
+    """Exclusive scan of a device int32 tensor (single-pass decoupled look-back)."""
+    import torch
+    _check_dev_i32(d_in, "d_in")
+    if d_out is None:
+        d_out = torch.empty_like(d_in)
+    _check_dev_i32(d_out, "d_out")
+    check_sc(lib().sc_scan_exclusive_i32(d_in.data_ptr(), d_out.data_ptr(), d_in.numel(), None, _stream_ptr(stream)))
+    return d_out
+
+
+def compact_device(d_in, d_out=None, stream=None):
+    """Returns (d_out, d_count): non-zero elements first (in order), count as a 1-element int64 tensor."""
+    import torch
+    _check_dev_i32(d_in, "d_in")
+    if d_out is None:
+        d_out = torch.empty_like(d_in)
+    _check_dev_i32(d_out, "d_out")
+    cnt = torch.zeros(1, dtype=torch.int64, device=d_in.device)
+    check_sc(lib().sc_compact_i32(d_in.data_ptr(), d_out.data_ptr(), d_in.numel(), cnt.data_ptr(), None,
+                                  _stream_ptr(stream)))
+    return d_out, cnt
+
+
+def partition_device(d_flags, d_perm=None, stream=None):
+    """Stable partition of indices (live first, then dead), like pathtrace.cu:366-376 `keep`."""
+    import torch
+    _check_dev_i32(d_flags, "d_flags")
+    if d_perm is None:
+        d_perm = torch.empty_like(d_flags)
+    live = torch.zeros(1, dtype=torch.int64, device=d_flags.device)
+    check_sc(lib().sc_partition_i32(d_flags.data_ptr(), d_perm.data_ptr(), d_flags.numel(), live.data_ptr(), None,
+                                    _stream_ptr(stream)))
+    return d_perm, live

@@ -1,0 +1,200 @@
+/* pt_amd.h — C ABI of the MI355X path tracer (libpt_amd.so).
+ *
+ * Replaces the reference's render boundary path_tracer/src/pathtrace.h:6-9
+ *     void InitDataContainer(GuiDataContainer*);   -> pt_set_flags
+ *     void pathtraceInit(Scene*);                  -> pt_create
+ *     void pathtraceFree();                        -> pt_destroy
+ *     void pathtrace(uchar4* pbo, int frame, int iteration);
+ *                                                  -> pt_render_pass (+ pt_preview_rgba for the PBO)
+ * the scene loader path_tracer/src/scene.h:17-35 / scene.cpp:16-219 (Scene::Scene, loadFromJSON)
+ *                                                  -> pt_scene_load_json / pt_scene_* builders
+ * the first-frame camera recompute of main.cpp:59-73,117-136           -> pt_scene_finalize
+ * and the image output main.cpp:88-112 + image.cpp:22-42 (saveImage, Image::savePNG)
+ *                                                  -> pt_save_png / pt_tonemap
+ *
+ * Differences from the reference, by design:
+ *   - no file-static globals: every render owns a pt_ctx; any number can coexist;
+ *   - status codes (PT_OK / PT_ERR_*) instead of exit(); pt_last_error() gives the message;
+ *   - explicit stream (hipStream_t passed as void*; NULL = the legacy default stream);
+ *   - no per-iteration device->host copy of the image: pt_get_image / pt_copy_image on demand;
+ *   - the context renders a pixel TILE (rows y with y % world == rank) and may trace `spp`
+ *     consecutive iterations per pass; world == 1, spp == 1 is exactly the reference's
+ *     pathtrace() (same RNG keys, same stable compaction order, same accumulation).
+ * All structs are plain C with the reference's field order (sceneStructs.h).
+ */
+#ifndef PT_AMD_H
+#define PT_AMD_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PT_OK 0
+#define PT_ERR_ARG 1
+#define PT_ERR_HIP 2
+#define PT_ERR_NOMEM 3
+#define PT_ERR_IO 4
+#define PT_ERR_PARSE 5
+#define PT_ERR_DEVICE 6   /* a device-side check failed (e.g. look-back spin bound hit) */
+
+#define PT_GEOM_SPHERE 0  /* sceneStructs.h:12-17 */
+#define PT_GEOM_CUBE 1
+#define PT_GEOM_MESH 2
+
+/* Runtime flags: GuiDataContainer (utilities.h:17-34), mirrored into Settings (pathtrace.cu:31-55). */
+typedef struct pt_flags {
+    int32_t russian_roulette;     /* default 1 */
+    int32_t use_bvh;              /* default 1 */
+    int32_t use_bbox;             /* default 1 (linear mesh path only) */
+    int32_t sort_by_material;     /* default 0: stable material sort before shading */
+    int32_t use_thrust_partition; /* default 0: same stable partition either way */
+    int32_t ssaa;                 /* default 1 */
+    int32_t dof;                  /* default 1 */
+    float aperture;               /* default 0.1 */
+    float focal_dist;             /* default 10 */
+} pt_flags;
+
+/* Material (sceneStructs.h:43-57), 48 bytes. */
+typedef struct pt_material {
+    float color[3];
+    float spec_exponent;
+    float spec_color[3];
+    float has_reflective;
+    float has_refractive;
+    float ior;
+    float emittance;
+    int32_t texture_id;           /* -1: none */
+} pt_material;
+
+/* Geom (sceneStructs.h:25-41), 272 bytes.  Matrices are glm column-major: m[c][r] = a[4c+r]. */
+typedef struct pt_geom {
+    int32_t type;
+    int32_t material_id;
+    float translation[3];
+    float rotation[3];            /* degrees */
+    float scale[3];
+    float transform[16];
+    float inverse_transform[16];
+    float inv_transpose[16];
+    int32_t tri_start, tri_end, bbox_idx;
+    float min_bound[3], max_bound[3];
+} pt_geom;
+
+/* Camera (sceneStructs.h:59-69). */
+typedef struct pt_camera {
+    int32_t res[2];
+    float position[3], look_at[3], view[3], up[3], right[3];
+    float fov[2];
+    float pixel_length[2];
+} pt_camera;
+
+/* Triangle (sceneStructs.h:103-161), 124 bytes, world space. */
+typedef struct pt_triangle {
+    int32_t id;                   /* original (load-order) index */
+    float v[3][3];
+    float uv[3][2];
+    float n[3][3];
+    float bmin[3], bmax[3];
+} pt_triangle;
+
+/* Flattened BVH node (BVH_tree.h:54-61), 40 bytes. */
+typedef struct pt_bvh_node {
+    float bmin[3], bmax[3];
+    int32_t sub_areas, axis, first_area_idx, rchild_idx;
+} pt_bvh_node;
+
+typedef struct pt_scene pt_scene;
+typedef struct pt_ctx pt_ctx;
+
+/* Tile / batching of one context.  rank/world: this context owns image rows y % world == rank.
+ * spp: iterations traced together per pass (1 = the reference). */
+typedef struct pt_shard {
+    int32_t rank, world, spp, reserved;
+} pt_shard;
+
+/* Per-context counters (device-side, read back by pt_stats). */
+typedef struct pt_stats_t {
+    uint64_t segments;            /* sum over bounces of live paths entering intersection */
+    uint64_t passes;
+    uint64_t bounce_live[64];     /* live paths entering bounce k (k < depth) */
+    uint64_t emissive_hits;       /* paths that terminated with non-zero radiance (framebuffer adds) */
+    uint32_t device_error;        /* nonzero: a device-side bound was hit */
+    uint32_t reserved;
+} pt_stats_t;
+
+const char* pt_last_error(void);
+void pt_flags_default(pt_flags* f);
+
+/* ---- scene ---------------------------------------------------------------------------- */
+int pt_scene_load_json(const char* path, pt_scene** out);   /* Scene::Scene(filename) incl. pt_scene_finalize */
+int pt_scene_create(pt_scene** out);
+void pt_scene_free(pt_scene* s);
+int pt_scene_add_material(pt_scene* s, const pt_material* m, int32_t* id_out);
+/* Texture pixels (row-major, `components` bytes per texel; only 3 is shaded, like the reference). */
+int pt_scene_add_texture(pt_scene* s, int32_t width, int32_t height, int32_t components,
+                         const uint8_t* pixels, int32_t* id_out);
+/* JSON scenes reference textures by file (scene.cpp:61-71, stb_image).  The loader records the
+ * path; the host fills the decoded pixels before pt_create (pt_create fails while any is empty). */
+int pt_scene_texture_path(const pt_scene* s, int32_t id, char* buf, int32_t cap);
+int pt_scene_set_texture_pixels(pt_scene* s, int32_t id, int32_t width, int32_t height,
+                                int32_t components, const uint8_t* pixels);
+/* Cube / sphere: builds transform, inverse, inverse-transpose like scene.cpp:80-91. */
+int pt_scene_add_geom(pt_scene* s, int32_t type, int32_t material_id, const float t[3],
+                      const float r[3], const float sc[3], int32_t* id_out);
+/* Mesh: object-space polygon soup, fan-triangulated (tinyobj triangulate=true), pre-transformed
+ * to world space (scene.cpp:94-173).  face_sizes[f] vertices per face; idx_* per face-vertex
+ * (-1 = absent), positions/normals (xyz), uvs (uv). */
+int pt_scene_add_mesh(pt_scene* s, int32_t material_id, const float t[3], const float r[3],
+                      const float sc[3], const float* positions, int32_t npos,
+                      const float* normals, int32_t nnorm, const float* uvs, int32_t nuv,
+                      const int32_t* face_sizes, int32_t nfaces, const int32_t* idx_pos,
+                      const int32_t* idx_norm, const int32_t* idx_uv, int32_t* id_out);
+int pt_scene_set_camera(pt_scene* s, int32_t res_x, int32_t res_y, float fovy, const float eye[3],
+                        const float look_at[3], const float up[3]);
+int pt_scene_set_render(pt_scene* s, int32_t iterations, int32_t depth, const char* file);
+/* Camera orbit recompute of the first frame (main.cpp:59-73,117-136) + BVH build (scene.cpp:218). */
+int pt_scene_finalize(pt_scene* s);
+int pt_scene_counts(const pt_scene* s, int32_t* ngeoms, int32_t* nmats, int32_t* ntris,
+                    int32_t* nnodes, int32_t* ntex);
+int pt_scene_get_camera(const pt_scene* s, pt_camera* out);
+int pt_scene_get_render(const pt_scene* s, int32_t* iterations, int32_t* depth, char* file, int32_t cap);
+int pt_scene_get_geoms(const pt_scene* s, pt_geom* out, int32_t cap);
+int pt_scene_get_materials(const pt_scene* s, pt_material* out, int32_t cap);
+int pt_scene_get_triangles(const pt_scene* s, pt_triangle* out, int32_t cap);
+int pt_scene_get_bvh(const pt_scene* s, pt_bvh_node* out, int32_t cap);
+
+/* ---- render context -------------------------------------------------------------------- */
+/* pathtraceInit: uploads the scene to the current HIP device, allocates SoA path buffers for
+ * rows_in_tile * width * spp paths.  shard may be NULL (= {0, 1, 1}). */
+int pt_create(const pt_scene* s, const pt_flags* flags, const pt_shard* shard, pt_ctx** out);
+int pt_destroy(pt_ctx* c);                                  /* pathtraceFree */
+int pt_set_flags(pt_ctx* c, const pt_flags* flags);         /* InitDataContainer / Settings */
+/* One pass: iterations [iter_first, iter_first + spp) for this tile, accumulated into the tile
+ * image.  Asynchronous on `stream`; no host synchronisation inside. */
+int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream);
+/* sendImageToPBO (pathtrace.cu:64-86) for the tile: d_rgba = npix * 4 bytes on the device. */
+int pt_preview_rgba(pt_ctx* c, int32_t iter, uint8_t* d_rgba, void* stream);
+int pt_tile_info(const pt_ctx* c, int32_t* width, int32_t* rows, int32_t* npix, int32_t* npaths);
+int pt_get_image(pt_ctx* c, float* host_rgb);               /* tile accumulator, npix*3 floats (sync) */
+int pt_copy_image(pt_ctx* c, float* d_rgb, void* stream);   /* device-to-device copy */
+int pt_reset_image(pt_ctx* c, void* stream);
+int pt_stats(pt_ctx* c, pt_stats_t* out);                   /* synchronises the context stream */
+/* Per-kernel device timing with hipEvents on the launch stream (for the roofline).  When
+ * enabled, pt_render_pass records events around every bounce kernel; pt_profile_read returns
+ * the summed milliseconds and launch count of the fused bounce kernels and of everything. */
+int pt_profile_enable(pt_ctx* c, int32_t on);
+int pt_profile_read(pt_ctx* c, double* bounce_ms, uint64_t* bounce_launches, double* total_ms);
+
+/* ---- image output ---------------------------------------------------------------------- */
+/* saveImage + Image::savePNG pixel math: out[3*(y*W + (W-1-x)) + k] = uchar(clamp(rgb/spp,0,1)*255). */
+int pt_tonemap(const float* rgb, int32_t width, int32_t height, float samples, uint8_t* out);
+/* Writes `path` as an 8-bit RGB PNG of the tonemapped image. */
+int pt_save_png(const char* path, const float* rgb, int32_t width, int32_t height, float samples);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PT_AMD_H */

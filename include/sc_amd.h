@@ -1,0 +1,76 @@
+/* sc_amd.h — C ABI of the MI355X stream-compaction library (libpt_amd.so).
+ *
+ * Replaces the reference's StreamCompaction namespace (path_tracer/stream_compaction/ and the
+ * standalone stream_compaction/stream_compaction/ copy):
+ *   Efficient::scan      efficient.h:9   / efficient.cu:150-174   -> sc_efficient_scan, sc_scan_exclusive_i32
+ *   Efficient::compact   efficient.h:11  / efficient.cu:185-219   -> sc_efficient_compact, sc_compact_i32
+ *   Efficient::timer()   efficient.h:7   / common.h:46-130        -> sc_timer_gpu_ms
+ *   Common::kernMapToBoolean / kernScatter  common.cu:25-46       -> fused into sc_compact_i32
+ *   mark_valid + scan + keep  path_tracer/src/pathtrace.cu:359-407 -> sc_partition_i32 (stable partition)
+ * The reference's CPU:: functions (cpu.h:9-13) are the test ORACLE (oracle/sc_oracle.cpp), not part
+ * of this product library: there is no CPU fallback here.
+ *
+ * Differences from the reference, by design:
+ *   - every entry point returns a status code (SC_OK / SC_ERR_*) instead of exit()ing
+ *     (common.cu:3-15); sc_last_error() gives the message;
+ *   - device-pointer entry points take an explicit hipStream_t (passed as void*) and never
+ *     allocate or synchronise (graph-capturable when given a workspace);
+ *   - no power-of-two padding: n is any value in [0, 2^31 - 1]; the reference's n == 1 failure
+ *      does not exist here;
+ *   - sums wrap in int32 exactly like the reference (two's complement).
+ * All functions are thread-compatible (no hidden globals besides a per-device workspace cache
+ * used only by the *_auto / host-pointer helpers, guarded by a mutex).
+ */
+#ifndef SC_AMD_H
+#define SC_AMD_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SC_OK 0
+#define SC_ERR_ARG 1
+#define SC_ERR_HIP 2
+#define SC_ERR_NOMEM 3
+
+/* Last error message of the calling thread ("" if none). */
+const char* sc_last_error(void);
+
+/* Bytes of device workspace the device-pointer entry points need for n elements
+ * (decoupled look-back tile status words + control words). */
+size_t sc_workspace_bytes(int64_t n);
+
+/* Exclusive prefix sum of int32 (wrapping), device pointers, single pass (decoupled look-back).
+ * d_out may alias d_in.  workspace: >= sc_workspace_bytes(n) bytes of device memory, or NULL
+ * to use the library's cached per-device workspace.  Replaces Efficient::scan. */
+int sc_scan_exclusive_i32(const int32_t* d_in, int32_t* d_out, int64_t n,
+                          void* workspace, void* stream);
+
+/* Stream compaction of int32: keeps the non-zero elements in order.  Writes the kept count to
+ * *d_count (device int64).  Replaces Efficient::compact (map + scan + scatter fused). */
+int sc_compact_i32(const int32_t* d_in, int32_t* d_out, int64_t n, int64_t* d_count,
+                   void* workspace, void* stream);
+
+/* Stable partition of indices by flags: d_perm[j] = source index of output slot j, live
+ * (flag != 0) elements first in original order, then dead ones in original order — exactly the
+ * `keep` placement of pathtrace.cu:366-376.  *d_live (device int64) = number of live elements. */
+int sc_partition_i32(const int32_t* d_flags, int32_t* d_perm, int64_t n, int64_t* d_live,
+                     void* workspace, void* stream);
+
+/* Host-pointer helpers with the reference's exact call semantics (Efficient::scan / compact take
+ * host arrays and return after the result is on the host).  They allocate device buffers from a
+ * per-device cache and time the device work with hipEvents like PerformanceTimer::startGpuTimer. */
+int sc_efficient_scan(int n, int* odata, const int* idata);
+int sc_efficient_compact(int n, int* odata, const int* idata, int* count_out);
+
+/* Elapsed device time (ms) of the previous host-pointer operation
+ * (PerformanceTimer::getGpuElapsedTimeForPreviousOperation, common.h:98-101). */
+float sc_timer_gpu_ms(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SC_AMD_H */

@@ -1,0 +1,247 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY.
+
+ctypes binding of oracle/build/liboracle.so (the serial CPU restatement of the reference in
+oracle/sc_oracle.cpp and oracle/pt_oracle.cpp).  Only tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py may import this module, and only as the checker; the product
+package (cuda_pathtracer_amd) never imports, loads or calls it.
+
+Also restates scene.cpp:33-219's JSON handling in Python (key defaults, alphabetical material
+ids, object order) so scene parity is checked against an independent parse.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import json
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+ORACLE_DIR = Path(__file__).resolve().parent
+LIB = ORACLE_DIR / "build" / "liboracle.so"
+
+
+class OGeom(C.Structure):
+    _fields_ = [("type", C.c_int32), ("materialid", C.c_int32), ("translation", C.c_float * 3),
+                ("rotation", C.c_float * 3), ("scale", C.c_float * 3), ("transform", C.c_float * 16),
+                ("inverse_transform", C.c_float * 16), ("inv_transpose", C.c_float * 16),
+                ("tri_start", C.c_int32), ("tri_end", C.c_int32), ("bbox_idx", C.c_int32),
+                ("min_bound", C.c_float * 3), ("max_bound", C.c_float * 3)]
+
+
+class OMaterial(C.Structure):
+    _fields_ = [("color", C.c_float * 3), ("spec_exponent", C.c_float), ("spec_color", C.c_float * 3),
+                ("has_reflective", C.c_float), ("has_refractive", C.c_float), ("ior", C.c_float),
+                ("emittance", C.c_float), ("texture_id", C.c_int32)]
+
+
+class OCamera(C.Structure):
+    _fields_ = [("res", C.c_int32 * 2), ("position", C.c_float * 3), ("look_at", C.c_float * 3),
+                ("view", C.c_float * 3), ("up", C.c_float * 3), ("right", C.c_float * 3),
+                ("fov", C.c_float * 2), ("pixel_length", C.c_float * 2)]
+
+
+class OFlags(C.Structure):
+    _fields_ = [("russian_roulette", C.c_int32), ("use_bvh", C.c_int32), ("use_bbox", C.c_int32),
+                ("sort_by_material", C.c_int32), ("use_thrust_partition", C.c_int32), ("ssaa", C.c_int32),
+                ("dof", C.c_int32), ("aperture", C.c_float), ("focal_dist", C.c_float)]
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not LIB.exists():
+            subprocess.run(["make", "-s", "-C", str(ORACLE_DIR)], check=True)
+        L = C.CDLL(str(LIB))
+        P, I64 = C.c_void_p, C.c_int64
+        L.oracle_scan.argtypes = [I64, P, P]
+        L.oracle_compact_without_scan.argtypes = [I64, P, P]
+        L.oracle_compact_without_scan.restype = I64
+        L.oracle_compact_with_scan.argtypes = [I64, P, P]
+        L.oracle_compact_with_scan.restype = I64
+        L.oracle_partition_indices.argtypes = [I64, P, P]
+        L.oracle_partition_indices.restype = I64
+        L.oracle_time_scan_ms.argtypes = [I64, P, P, C.c_int]
+        L.oracle_time_scan_ms.restype = C.c_double
+        L.oracle_time_compact_ms.argtypes = [I64, P, P, C.c_int, C.POINTER(I64)]
+        L.oracle_time_compact_ms.restype = C.c_double
+        L.oracle_sincos.argtypes = [C.c_float, C.POINTER(C.c_float), C.POINTER(C.c_float)]
+        L.oracle_u01_sequence.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_float)]
+        L.oracle_u01_sequence.restype = C.c_float
+        L.oracle_build_transform.argtypes = [P, P, P, P, P, P]
+        L.oracle_camera.argtypes = [C.c_int, C.c_int, C.c_float, P, P, P, C.POINTER(OCamera)]
+        L.oracle_render_pass.argtypes = [C.POINTER(OGeom), C.c_int, C.POINTER(OMaterial), C.c_int,
+                                         P, C.c_int, P, C.c_int, P, C.c_int,
+                                         C.POINTER(OCamera), C.c_int, C.POINTER(OFlags),
+                                         C.c_int, C.c_int, C.c_int, C.c_int, P, P]
+        L.oracle_render_pass.restype = C.c_int
+        L.oracle_render.argtypes = [C.POINTER(OGeom), C.c_int, C.POINTER(OMaterial), C.c_int,
+                                    P, C.c_int, P, C.c_int, P, C.c_int,
+                                    C.POINTER(OCamera), C.c_int, C.POINTER(OFlags), C.c_int, C.c_int, P, P]
+        L.oracle_render.restype = C.c_double
+        L.oracle_tonemap.argtypes = [P, C.c_int, C.c_int, C.c_float, P]
+        L.oracle_preview.argtypes = [P, C.c_int, C.c_int, C.c_int, P]
+        _lib = L
+    return _lib
+
+
+# ---- stream compaction ---------------------------------------------------------------------
+def _i32(a) -> np.ndarray:
+    return np.ascontiguousarray(a, dtype=np.int32)
+
+
+def scan(a) -> np.ndarray:
+    a = _i32(a)
+    out = np.zeros_like(a)
+    lib().oracle_scan(len(a), out.ctypes.data, a.ctypes.data)
+    return out
+
+
+def compact_without_scan(a) -> np.ndarray:
+    a = _i32(a)
+    out = np.zeros_like(a)
+    n = lib().oracle_compact_without_scan(len(a), out.ctypes.data, a.ctypes.data)
+    return out[:n]
+
+
+def compact_with_scan(a) -> np.ndarray:
+    a = _i32(a)
+    out = np.zeros_like(a)
+    n = lib().oracle_compact_with_scan(len(a), out.ctypes.data, a.ctypes.data)
+    return out[:n]
+
+
+def partition_indices(flags):
+    f = _i32(flags)
+    out = np.zeros_like(f)
+    live = lib().oracle_partition_indices(len(f), f.ctypes.data, out.ctypes.data)
+    return out, int(live)
+
+
+# ---- scene (scene.cpp:33-219 restated) -----------------------------------------------------
+def build_transform(t, r, s):
+    T = np.zeros(16, np.float32); Inv = np.zeros(16, np.float32); InvT = np.zeros(16, np.float32)
+    f = [np.asarray(x, np.float32) for x in (t, r, s)]
+    lib().oracle_build_transform(f[0].ctypes.data, f[1].ctypes.data, f[2].ctypes.data,
+                                 T.ctypes.data, Inv.ctypes.data, InvT.ctypes.data)
+    return T, Inv, InvT
+
+
+def camera(res, fovy, eye, lookat, up) -> OCamera:
+    cam = OCamera()
+    e, l, u = (np.asarray(x, np.float32) for x in (eye, lookat, up))
+    lib().oracle_camera(int(res[0]), int(res[1]), float(np.float32(fovy)), e.ctypes.data, l.ctypes.data,
+                        u.ctypes.data, C.byref(cam))
+    return cam
+
+
+class OracleScene:
+    def __init__(self):
+        self.geoms: list[OGeom] = []
+        self.materials: list[OMaterial] = []
+        self.cam: OCamera | None = None
+        self.depth = 8
+        self.iterations = 1
+        self.file = "render"
+
+    def add_material(self, rgb=(0, 0, 0), specrgb=None, specex=1.0, reflective=0.0, refractive=0.0, ior=0.0,
+                     emittance=0.0, texture_id=-1) -> int:
+        m = OMaterial()
+        m.color[:] = [float(np.float32(v)) for v in rgb]
+        m.spec_color[:] = [float(np.float32(v)) for v in (specrgb if specrgb is not None else rgb)]
+        m.spec_exponent, m.has_reflective, m.has_refractive = specex, reflective, refractive
+        m.ior, m.emittance, m.texture_id = ior, emittance, texture_id
+        self.materials.append(m)
+        return len(self.materials) - 1
+
+    def add_geom(self, type_, material, t, r, s) -> int:
+        g = OGeom()
+        g.type, g.materialid = type_, material
+        g.translation[:], g.rotation[:], g.scale[:] = list(t), list(r), list(s)
+        T, Inv, InvT = build_transform(t, r, s)
+        g.transform[:], g.inverse_transform[:], g.inv_transpose[:] = T.tolist(), Inv.tolist(), InvT.tolist()
+        g.bbox_idx = -1
+        self.geoms.append(g)
+        return len(self.geoms) - 1
+
+    def set_camera(self, res, fovy, eye, lookat, up=(0, 1, 0)):
+        self.cam = camera(res, fovy, eye, lookat, up)
+
+    @classmethod
+    def from_json(cls, path) -> "OracleScene":
+        data = json.loads(Path(path).read_text())
+        sc = cls()
+        ids = {}
+        for name in sorted(data["Materials"]):           # nlohmann::json objects are std::map
+            p = data["Materials"][name]
+            rgb = p.get("RGB", [0.0, 0.0, 0.0])
+            ids[name] = sc.add_material(rgb=rgb, specrgb=p.get("SPECRGB", rgb), specex=p.get("SPECEX", 1.0),
+                                        reflective=p.get("REFLECTIVE", 0.0), emittance=p.get("EMITTANCE", 0.0),
+                                        refractive=p.get("REFRACTIVE", 0.0), ior=p.get("IOR", 0.0))
+        for o in data["Objects"]:
+            typ = {"sphere": 0, "cube": 1, "mesh": 2}[o["TYPE"]]
+            if typ == 2:
+                raise NotImplementedError("oracle: mesh objects")
+            sc.add_geom(typ, ids.get(o["MATERIAL"], 0), o["TRANS"], o["ROTAT"], o["SCALE"])
+        c = data["Camera"]
+        sc.set_camera(c["RES"], c["FOVY"], c["EYE"], c["LOOKAT"], c["UP"])
+        sc.depth, sc.iterations, sc.file = int(c["DEPTH"]), int(c["ITERATIONS"]), c["FILE"]
+        return sc
+
+
+def flags(russian_roulette=True, use_bvh=True, use_bbox=True, sort_by_material=False, use_thrust_partition=False,
+          ssaa=True, dof=True, aperture=0.1, focal_dist=10.0) -> OFlags:
+    return OFlags(int(russian_roulette), int(use_bvh), int(use_bbox), int(sort_by_material),
+                  int(use_thrust_partition), int(ssaa), int(dof), float(aperture), float(focal_dist))
+
+
+def render_pass(sc: OracleScene, fl: OFlags, iter_first: int, spp: int = 1, rank: int = 0, world: int = 1,
+                image: np.ndarray | None = None, depth: int | None = None):
+    """One pass on the tile; returns (image (rows, W, 3) float32, bounce_live list)."""
+    W, H = sc.cam.res[0], sc.cam.res[1]
+    rows = (H - rank + world - 1) // world
+    if image is None:
+        image = np.zeros((rows, W, 3), np.float32)
+    d = depth if depth is not None else sc.depth
+    live = np.zeros(64, np.uint64)
+    G = (OGeom * len(sc.geoms))(*sc.geoms)
+    M = (OMaterial * len(sc.materials))(*sc.materials)
+    lib().oracle_render_pass(G, len(sc.geoms), M, len(sc.materials), None, 0, None, 0, None, 0,
+                             C.byref(sc.cam), d, C.byref(fl), iter_first, spp, rank, world,
+                             image.ctypes.data, live.ctypes.data)
+    return image, [int(x) for x in live[:d]]
+
+
+def render(sc: OracleScene, fl: OFlags, iters: int, iter_first: int = 1):
+    W, H = sc.cam.res[0], sc.cam.res[1]
+    image = np.zeros((H, W, 3), np.float32)
+    live = np.zeros(64, np.uint64)
+    G = (OGeom * len(sc.geoms))(*sc.geoms)
+    M = (OMaterial * len(sc.materials))(*sc.materials)
+    secs = lib().oracle_render(G, len(sc.geoms), M, len(sc.materials), None, 0, None, 0, None, 0,
+                               C.byref(sc.cam), sc.depth, C.byref(fl), iter_first, iters, image.ctypes.data,
+                               live.ctypes.data)
+    return image, [int(x) for x in live[:sc.depth]], secs
+
+
+def tonemap(image: np.ndarray, samples: float) -> np.ndarray:
+    img = np.ascontiguousarray(image, np.float32)
+    H, W = img.shape[:2]
+    out = np.zeros((H, W, 3), np.uint8)
+    lib().oracle_tonemap(img.ctypes.data, W, H, float(samples), out.ctypes.data)
+    return out
+
+
+def u01_sequence(it, index, depth, count) -> np.ndarray:
+    out = (C.c_float * count)()
+    lib().oracle_u01_sequence(it, index, depth, count, out)
+    return np.frombuffer(out, dtype=np.float32).copy()
+
+
+def sincos(x: float):
+    s, c = C.c_float(), C.c_float()
+    lib().oracle_sincos(float(x), C.byref(s), C.byref(c))
+    return s.value, c.value

@@ -1,0 +1,148 @@
+"""GPU parity of the stream-compaction kernels against the serial CPU oracle (bit-exact).
+
+Reference behaviour: path_tracer/stream_compaction/cpu.cu:16-79 (oracle), efficient.cu:150-219
+(product API), stream_compaction/src/main.cpp:14-146 (test shape: POT and NPOT sizes, last element
+forced to 0, values rand()%50 for scan and rand()%4 for compaction).
+"""
+import numpy as np
+import pytest
+
+from oracle import binding as O
+
+pytestmark = pytest.mark.gpu
+
+SIZES = [1, 2, 3, 5, 63, 64, 65, 127, 128, 129, 255, 256, 257, 1000, 4095, 4096, 4097, 8191, 65536 + 17,
+         (1 << 20) - 3, 1 << 20]
+
+
+def _gen(n, maxval, seed):
+    rng = np.random.default_rng(seed)
+    a = rng.integers(0, maxval, size=n, dtype=np.int32)
+    if n:
+        a[-1] = 0          # main.cpp:23,98 "leave a 0 at the end"
+    return a
+
+
+@pytest.mark.parametrize("n", SIZES)
+def test_scan_matches_oracle(gpu_device, n):
+    import torch
+    from cuda_pathtracer_amd import scan_device
+    a = _gen(n, 50, n)
+    d = torch.from_numpy(a).to(gpu_device)
+    out = scan_device(d)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out.cpu().numpy(), O.scan(a))
+
+
+@pytest.mark.parametrize("n", [1, 3, 129, 4097, 100003])
+def test_scan_wraps_and_negatives(gpu_device, n):
+    import torch
+    from cuda_pathtracer_amd import scan_device
+    rng = np.random.default_rng(7)
+    a = rng.integers(-2**31, 2**31 - 1, size=n, dtype=np.int64).astype(np.int32)
+    out = scan_device(torch.from_numpy(a).to(gpu_device)).cpu().numpy()
+    np.testing.assert_array_equal(out, O.scan(a))
+
+
+def test_scan_inplace_and_unaligned(gpu_device):
+    import torch
+    from cuda_pathtracer_amd import scan_device
+    a = _gen(10000 + 3, 50, 3)
+    d = torch.from_numpy(a).to(gpu_device)
+    scan_device(d, d)                                    # in place
+    np.testing.assert_array_equal(d.cpu().numpy(), O.scan(a))
+    big = torch.from_numpy(np.concatenate([np.array([9], np.int32), a])).to(gpu_device)
+    sub = big[1:]                                        # 4-byte aligned, not 16
+    out = torch.empty_like(sub)
+    scan_device(sub, out)
+    np.testing.assert_array_equal(out.cpu().numpy(), O.scan(a))
+
+
+@pytest.mark.parametrize("n", SIZES)
+def test_compact_matches_oracle(gpu_device, n):
+    import torch
+    from cuda_pathtracer_amd import compact_device
+    a = _gen(n, 4, n + 1)
+    out, cnt = compact_device(torch.from_numpy(a).to(gpu_device))
+    c = int(cnt.item())
+    ref = O.compact_without_scan(a)
+    assert c == len(ref)
+    np.testing.assert_array_equal(out[:c].cpu().numpy(), ref)
+    np.testing.assert_array_equal(ref, O.compact_with_scan(a))
+
+
+@pytest.mark.parametrize("n", [1, 2, 65, 4097, 100000])
+def test_partition_matches_keep(gpu_device, n):
+    import torch
+    from cuda_pathtracer_amd import partition_device
+    f = _gen(n, 2, n + 5)
+    perm, live = partition_device(torch.from_numpy(f).to(gpu_device))
+    ref, ref_live = O.partition_indices(f)
+    assert int(live.item()) == ref_live
+    np.testing.assert_array_equal(perm.cpu().numpy(), ref)
+
+
+def test_edge_cases(gpu_device):
+    import torch
+    from cuda_pathtracer_amd import compact_device, scan_device
+    empty = torch.zeros(0, dtype=torch.int32, device=gpu_device)
+    assert scan_device(empty).numel() == 0
+    _, cnt = compact_device(empty)
+    assert int(cnt.item()) == 0
+    zeros = torch.zeros(5000, dtype=torch.int32, device=gpu_device)
+    _, cnt = compact_device(zeros)
+    assert int(cnt.item()) == 0
+    ones = torch.ones(5000, dtype=torch.int32, device=gpu_device)
+    np.testing.assert_array_equal(scan_device(ones).cpu().numpy(), np.arange(5000, dtype=np.int32))
+    out, cnt = compact_device(ones)
+    assert int(cnt.item()) == 5000
+
+
+def test_host_api_reference_semantics(gpu_device):
+    """Efficient::scan / compact with host arrays (efficient.cu:150-219), incl. n == 1."""
+    from cuda_pathtracer_amd import Efficient
+    for n in (1, 2, 7, 1 << 16, (1 << 16) - 3):
+        a = _gen(n, 50, n)
+        o = np.zeros(n, np.int32)
+        Efficient.scan(n, o, a)
+        np.testing.assert_array_equal(o, O.scan(a))
+        assert Efficient.timer().getGpuElapsedTimeForPreviousOperation() >= 0.0
+        b = _gen(n, 4, n + 9)
+        o2 = np.zeros(n, np.int32)
+        cnt = Efficient.compact(n, o2, b)
+        ref = O.compact_without_scan(b)
+        assert cnt == len(ref)
+        np.testing.assert_array_equal(o2[:cnt], ref)
+    # the reference's known-answer vectors (stream_compaction/INSTRUCTION.md:262-302)
+    a = np.array([1, 5, 0, 1, 2, 0, 3], np.int32)
+    o = np.zeros(7, np.int32)
+    Efficient.scan(7, o, a)
+    assert o.tolist() == [0, 1, 6, 6, 7, 9, 9]
+    assert Efficient.compact(7, o, a) == 5 and o[:5].tolist() == [1, 5, 1, 2, 3]
+
+
+@pytest.mark.slow
+def test_reference_size_2e28_properties(gpu_device):
+    """SIZE = 1<<28 and NPOT = SIZE-3 (main.cpp:8-9): size-independent checks on the device."""
+    import torch
+    from cuda_pathtracer_amd import compact_device, scan_device
+    for n in ((1 << 28), (1 << 28) - 3):
+        g = torch.Generator(device=gpu_device).manual_seed(1234)
+        a = torch.randint(0, 50, (n,), dtype=torch.int32, device=gpu_device, generator=g)
+        a[-1] = 0
+        s = scan_device(a)
+        # exclusive scan: s[i+1] - s[i] == a[i] (int32 wrap), s[0] == 0
+        assert int(s[0].item()) == 0
+        diff = (s[1:] - s[:-1])
+        assert bool(torch.equal(diff, a[:-1]))
+        # spot-check against the oracle on a prefix and a window
+        head = a[:100000].cpu().numpy()
+        np.testing.assert_array_equal(s[:100000].cpu().numpy(), O.scan(head))
+        del s, diff
+        f = (a % 4).to(torch.int32)
+        out, cnt = compact_device(f)
+        nz = int((f != 0).sum().item())
+        assert int(cnt.item()) == nz
+        assert bool(torch.equal(out[:nz], f[f != 0]))
+        del a, f, out
+        torch.cuda.empty_cache()
