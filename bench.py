@@ -1,0 +1,273 @@
+"""Benchmark: Mray/s (paths x bounces / s) on the bundled Cornell scene + scan GB/s vs HBM peak.
+
+Workload (BASELINE.json configs[1]): path_tracer/scenes/cornell.json as-is — 800x800, DEPTH 8,
+default flags.  A step is one render pass.  On N GPUs (one process per GPU, torchrun) rank r owns
+the image rows y % N == r and traces N samples per pixel per pass (spp = N), so every GPU traces
+800*800 camera paths per step (weak scaling; N = 1 is exactly the reference's pathtrace()).
+After the timed passes the float tiles are gathered to rank 0 with one RCCL gather (inside the
+timed region).  value = all ranks' traced segments / max-over-ranks wall time / 1e6.
+
+Roofline: the dominant kernel is the fused bounce kernel k_bounce<false,true> (bounces >= 1).
+Its average launch time comes from HIP events recorded on its launch stream over the timed
+passes; its algorithmic bytes per launch are path-state SoA read 44 B x paths in + write
+44 B x survivors + framebuffer read-modify-write 24 B x emissive terminations.
+The scan kernel is measured separately at n = 2^28 (8 B/element, 2 GiB, beyond the 256 MiB MALL).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+METRIC = "Mray/s (paths×bounces/s) on Cornell scene + scan GB/s vs HBM peak, 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+PATH_BYTES = 44                # o(12) d(12) c(12) slot(4) bounces(4)
+FB_RMW_BYTES = 24              # float3 read + write
+
+
+def _log(rank, *a):
+    if rank == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def _traffic_from_profiles(kernel_key: str):
+    """HBM bytes per launch from the committed rocprofv3 PMC measurement (profiles/*traffic*.json)."""
+    best = None
+    for p in sorted((ROOT / "profiles").glob("*traffic*.json")):
+        try:
+            d = json.loads(p.read_text())
+        except Exception:
+            continue
+        if kernel_key in d:
+            best = d[kernel_key]
+    return best
+
+
+def cpu_baseline_render(seconds_target: float) -> dict:
+    """The oracle (serial C++ restatement of the reference renderer) on this host, 1 thread."""
+    from oracle import binding as O
+    sc = O.OracleScene.from_json(ROOT / "tests" / "scenes" / "cornell.json")
+    fl = O.flags()
+    total_seg, total_t, iters = 0, 0.0, 0
+    while total_t < seconds_target and iters < 64:
+        _, live, secs = O.render(sc, fl, 1, iter_first=iters + 1)
+        total_seg += sum(live)
+        total_t += secs
+        iters += 1
+    return {"value": total_seg / total_t / 1e6, "unit": "Mray/s", "cores": 1, "kind": "port",
+            "sample": f"{iters} iteration(s) of cornell.json 800x800 DEPTH 8 default flags, "
+                      f"{total_seg} segments in {total_t:.2f} s (oracle/pt_oracle.cpp, g++ -O2, 1 thread)"}
+
+
+def cpu_baseline_scan(n: int = 1 << 20, reps: int = 50) -> dict:
+    from oracle import binding as O
+    a = np.random.default_rng(1234).integers(0, 50, n, dtype=np.int32)
+    a[-1] = 0
+    out = np.zeros_like(a)
+    O.lib().oracle_scan(n, out.ctypes.data, a.ctypes.data)  # warm
+    ms = O.lib().oracle_time_scan_ms(n, a.ctypes.data, out.ctypes.data, reps) / reps
+    return {"n": n, "ms": ms, "GB/s": 8.0 * n / (ms * 1e-3) / 1e9, "cores": 1, "kind": "port",
+            "sample": f"CPU::scan restated (oracle/sc_oracle.cpp), {reps} reps, U[0,50) seed 1234"}
+
+
+def scan_bench(torch, dev, n: int, reps: int) -> dict:
+    import cuda_pathtracer_amd as P
+    from cuda_pathtracer_amd._native import check_sc, lib
+    g = torch.Generator(device=dev).manual_seed(1234)
+    a = torch.randint(0, 50, (n,), dtype=torch.int32, device=dev, generator=g)
+    out = torch.empty_like(a)
+    ws = torch.empty(int(lib().sc_workspace_bytes(n)), dtype=torch.uint8, device=dev)
+    st = torch.cuda.current_stream()
+    for _ in range(3):
+        check_sc(lib().sc_scan_exclusive_i32(a.data_ptr(), out.data_ptr(), n, ws.data_ptr(), st.cuda_stream))
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for e0, e1 in ev:
+        e0.record(st)
+        check_sc(lib().sc_scan_exclusive_i32(a.data_ptr(), out.data_ptr(), n, ws.data_ptr(), st.cuda_stream))
+        e1.record(st)
+    torch.cuda.synchronize()
+    times = sorted(e0.elapsed_time(e1) for e0, e1 in ev)
+    ms = float(np.mean(times))
+    # correctness of the timed output: exclusive-scan identity on the device
+    ok = bool(torch.equal(out[1:] - out[:-1], a[:-1])) and int(out[0].item()) == 0
+    del P
+    gbs = 8.0 * n / (ms * 1e-3) / 1e9
+    traffic = _traffic_from_profiles("scan")
+    return {"n": n, "ms": ms, "ms_min": times[0], "GB/s": gbs, "verified": ok,
+            "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": gbs / HBM_PEAK_GBS, "traffic": traffic}}
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--scan-n", type=int, default=1 << 28)
+    ap.add_argument("--scan-reps", type=int, default=20)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-scan", action="store_true")
+    ap.add_argument("--scene", default=str(ROOT / "tests" / "scenes" / "cornell.json"))
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+
+    import torch
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    import cuda_pathtracer_amd as P
+    P.lib()
+
+    scene = P.Scene(args.scene)
+    st_r = scene.state()
+    spp = world
+    pt = P.PathTracer(scene, P.GuiDataContainer(), rank=rank, world=world, spp=spp)
+    stream = torch.cuda.current_stream()
+    _log(rank, f"[bench] tile rows={pt.rows} npix={pt.npix} paths/pass={pt.npaths} depth={st_r.traceDepth}")
+
+    it = 1
+    for _ in range(args.warmup):
+        pt.render_pass(it, stream)
+        it += spp
+    torch.cuda.synchronize()
+    s0 = pt.stats()
+
+    rows_all = None
+    tile = torch.empty((pt.rows, pt.width, 3), dtype=torch.float32, device=dev)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        pt.render_pass(it, stream)
+        it += spp
+    # single RCCL gather of the framebuffer tiles to rank 0
+    pt.copy_image_to(tile.data_ptr(), stream)
+    if dist is not None:
+        max_rows = (scene.camera().res[1] + world - 1) // world
+        send = torch.zeros((max_rows, pt.width, 3), dtype=torch.float32, device=dev)
+        send[:pt.rows] = tile
+        gather = [torch.empty_like(send) for _ in range(world)] if rank == 0 else None
+        dist.gather(send, gather, dst=0)
+        if rank == 0:
+            rows_all = gather
+    barrier()
+    elapsed = time.perf_counter() - t0
+    s1 = pt.stats()
+
+    # Kernel-level timing for the roofline: a profiled segment of the same workload right after
+    # the timed region (HIP events bracket every launch on its stream; events inside the timed
+    # region would add inter-kernel gaps to `value`).
+    prof_passes = min(args.steps, 50)
+    pt.profile(True)
+    pt.profile_read()
+    sp0 = pt.stats()
+    for _ in range(prof_passes):
+        pt.render_pass(it, stream)
+        it += spp
+    prof = pt.profile_read()
+    pt.profile(False)
+    sp1 = pt.stats()
+
+    seg = s1["segments"] - s0["segments"]
+    live = [b - a for a, b in zip(s0["bounce_live"], s1["bounce_live"])]
+    emit = [b - a for a, b in zip(s0["bounce_emit"], s1["bounce_emit"])]
+    t_max = elapsed
+    seg_all = seg
+    if dist is not None:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t_max = float(tt.item())
+        ss = torch.tensor([seg], dtype=torch.int64, device=dev)
+        dist.all_reduce(ss, op=dist.ReduceOp.SUM)
+        seg_all = int(ss.item())
+
+    # roofline of the dominant kernel (bounces >= 1), over the profiled segment
+    b_ms, b_n = prof["bounce"]
+    f_ms, f_n = prof["first_bounce"]
+    depth = st_r.traceDepth
+    plive = [b - a for a, b in zip(sp0["bounce_live"], sp1["bounce_live"])]
+    pemit = [b - a for a, b in zip(sp0["bounce_emit"], sp1["bounce_emit"])]
+    bytes_bounce = 0
+    for b in range(1, depth):
+        n_in = plive[b]
+        n_out = plive[b + 1] if b + 1 < depth else 0
+        bytes_bounce += PATH_BYTES * n_in + PATH_BYTES * n_out + FB_RMW_BYTES * pemit[b]
+    per_launch_bytes = bytes_bounce / max(b_n, 1)
+    avg_ms = b_ms / max(b_n, 1)
+    achieved = per_launch_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": _traffic_from_profiles("k_bounce"),
+                "kernel": "k_bounce<false,true>", "avg_launch_ms": avg_ms, "launches": b_n,
+                "algorithmic_bytes_per_launch": per_launch_bytes}
+
+    result = None
+    if rank == 0:
+        if rows_all is not None:
+            H = scene.camera().res[1]
+            full = np.zeros((H, pt.width, 3), np.float32)
+            for r, t in enumerate(rows_all):
+                rows_r = (H - r + world - 1) // world
+                full[r::world] = t[:rows_r].cpu().numpy()
+            assert np.isfinite(full).all()
+        value = seg_all / t_max / 1e6
+        result = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "Mray/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": t_max / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (bundled cornell.json scene; camera rays generated on device)",
+            "config": {"workload": "cornell.json 800x800 DEPTH 8 default flags; per GPU 640000 camera paths "
+                                   "per step (rows y%N==rank, N spp per pass); fused bounce kernel",
+                       "scene": "cornell.json", "resolution": [800, 800], "depth": depth, "spp_per_step": spp,
+                       "paths_per_gpu_per_step": pt.npaths, "parallelism": f"pixel-tile x{world} + RCCL gather"},
+            "roofline": roofline,
+            "segments": seg_all,
+            "bounce_live_per_pass": [x / args.steps for x in live],
+            "first_bounce_avg_ms": f_ms / max(f_n, 1),
+        }
+        if not args.no_scan:
+            result["scan"] = scan_bench(torch, dev, args.scan_n, args.scan_reps)
+        if world == 1 and not args.no_cpu_baseline:
+            result["cpu_baseline"] = cpu_baseline_render(args.cpu_seconds)
+            result["cpu_baseline_scan"] = cpu_baseline_scan()
+        else:
+            result["cpu_baseline"] = None
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+    pt.free()
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -67,7 +67,8 @@ class Shard(C.Structure):
 
 class Stats(C.Structure):
     _fields_ = [("segments", C.c_uint64), ("passes", C.c_uint64), ("bounce_live", C.c_uint64 * 64),
-                ("emissive_hits", C.c_uint64), ("device_error", C.c_uint32), ("reserved", C.c_uint32)]
+                ("emissive_hits", C.c_uint64), ("bounce_emit", C.c_uint64 * 64), ("device_error", C.c_uint32),
+                ("reserved", C.c_uint32)]
 
 
 assert C.sizeof(Geom) == 272 and C.sizeof(Material) == 48 and C.sizeof(Triangle) == 124
@@ -123,7 +124,7 @@ SIGNATURES = {
     "pt_reset_image": (_I, [_P, _P]),
     "pt_stats": (_I, [_P, C.POINTER(Stats)]),
     "pt_profile_enable": (_I, [_P, _I]),
-    "pt_profile_read": (_I, [_P, C.POINTER(C.c_double), C.POINTER(C.c_uint64), C.POINTER(C.c_double)]),
+    "pt_profile_read": (_I, [_P, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
     "pt_tonemap": (_I, [_P, _I, _I, _F, _P]),
     "pt_save_png": (_I, [C.c_char_p, _P, _I, _I, _F]),
 }

@@ -3,12 +3,16 @@
 // Each tile publishes one 64-bit status word {flag:2 @ bit 62 | value:32 @ bit 0} with ONE
 // relaxed agent-scope atomic store (the "granule" form: the value is its own flag, so no
 // release/acquire fence is needed — cdna_hip_programming.md §6 Guideline 16, R2), first the
-// tile AGGREGATE, later the INCLUSIVE prefix.  A successor's wave 0 reads 64 predecessors per
-// step with relaxed agent-scope loads (sc1: bypass the stale per-CU L1) and stops at the
-// nearest inclusive prefix.  Tile ids come from an atomic ticket so every predecessor of a
-// running tile is already resident (forward progress without co-residency assumptions).
-// Every spin is bounded; on timeout the tile proceeds and raises *err (results then wrong,
-// but the kernel always drains — a hung wave would take the GPU down).
+// tile AGGREGATE, later the INCLUSIVE prefix.  A successor's wave 0 reads 4 x 64 predecessors
+// per round trip with relaxed agent-scope loads and stops at the nearest inclusive prefix.
+//
+// Tile assignment is STATIC and persistent: a grid of G co-resident workgroups, workgroup b
+// owns tiles b, b+G, b+2G, ... and processes them in increasing order.  There is no ticket
+// counter (a single returning atomic saturates at ~88 dequeues/us on MI355X, which made the
+// ticket the bottleneck).  Forward progress: the lowest unpublished tile's predecessors are all
+// published and its workgroup is resident (G <= resident capacity, see grid_for()), so it
+// completes.  Every spin is still bounded; on timeout the tile proceeds and raises *err
+// (results then wrong, but the kernel always drains — a hung wave would take the GPU down).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -17,7 +21,8 @@ namespace lb {
 
 constexpr uint64_t kFlagAgg = 1ull << 62;
 constexpr uint64_t kFlagPre = 2ull << 62;
-constexpr uint32_t kSpinLimit = 1u << 22;
+constexpr uint32_t kSpinLimit = 1u << 21;
+constexpr int kWindows = 4;
 
 __device__ __forceinline__ void publish(uint64_t* st, int tile, uint64_t flag, uint32_t v) {
     __hip_atomic_store(st + tile, flag | (uint64_t)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -42,34 +47,45 @@ __device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t v) {
     return v;
 }
 
+__device__ __forceinline__ uint64_t poll(const uint64_t* st, int j) {
+    return j >= 0 ? __hip_atomic_load(st + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kFlagPre;
+}
+
 // Called by one full wave (all 64 lanes).  Returns the exclusive prefix of `tile` (> 0).
+// Window w of a round covers predecessors base - 64w - lane; windows are consumed in order.
 __device__ __forceinline__ uint32_t lookback(uint64_t* st, int tile, int lane, uint32_t* err) {
     uint32_t excl = 0;
     int base = tile - 1;
+    uint32_t spins = 0;
     for (;;) {
-        const int j = base - lane;
-        uint64_t w;
-        uint32_t spins = 0;
-        int first_pre;
-        for (;;) {
-            w = j >= 0 ? __hip_atomic_load(st + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kFlagPre;
-            const uint64_t not_ready = __ballot((w >> 62) == 0);
-            const uint64_t pre = __ballot((w >> 62) == 2);
-            first_pre = pre ? __builtin_ctzll(pre) : 64;
-            const int first_nr = not_ready ? __builtin_ctzll(not_ready) : 64;
-            if (first_nr > first_pre || first_nr == 64) break;
+        uint64_t w[kWindows];
+#pragma unroll
+        for (int k = 0; k < kWindows; ++k) w[k] = poll(st, base - 64 * k - lane);
+        int consumed = 0;   // windows fully summed this round
+        bool stalled = false;
+#pragma unroll
+        for (int k = 0; k < kWindows; ++k) {
+            if (stalled) break;
+            const uint64_t nr = __ballot((w[k] >> 62) == 0);
+            const uint64_t pre = __ballot((w[k] >> 62) == 2);
+            const int first_pre = pre ? __builtin_ctzll(pre) : 64;
+            const int first_nr = nr ? __builtin_ctzll(nr) : 64;
+            if (first_pre < first_nr) {
+                excl += wave_sum(lane <= first_pre ? (uint32_t)w[k] : 0u);
+                return excl;
+            }
+            if (first_nr < 64) { stalled = true; break; }
+            excl += wave_sum((uint32_t)w[k]);
+            ++consumed;
+        }
+        base -= 64 * consumed;
+        if (stalled) {
             if (++spins > kSpinLimit) {
                 if (lane == 0) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                first_pre = first_nr;   // give up: treat the unready word as a zero prefix
-                w = (lane == first_nr) ? kFlagPre : w;
-                break;
+                return excl;   // give up (flagged): results are wrong but the grid drains
             }
             __builtin_amdgcn_s_sleep(1);
         }
-        const uint32_t v = (lane <= first_pre) ? (uint32_t)w : 0u;
-        excl += wave_sum(v);
-        if (first_pre < 64) return excl;
-        base -= 64;
     }
 }
 

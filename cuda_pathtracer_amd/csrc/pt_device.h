@@ -44,12 +44,21 @@ struct Affine {
     float c[4][3];
     float z3[3];
 };
-__device__ __forceinline__ f3 xform_point(const Affine& m, f3 v) {
+// Scene tables that every lane of a wave reads at the same address are accessed through the
+// constant address space so hipcc emits scalar (s_load) reads into SGPRs instead of 64 copies.
+#define PT_CONST_AS __attribute__((address_space(4)))
+template <class T>
+__device__ __forceinline__ const T PT_CONST_AS* as_const(const T* p) {
+    return (const T PT_CONST_AS*)(p);
+}
+template <class M>
+__device__ __forceinline__ f3 xform_point(const M& m, f3 v) {
     return F3((m.c[0][0] * v.x + m.c[1][0] * v.y) + (m.c[2][0] * v.z + m.c[3][0]),
               (m.c[0][1] * v.x + m.c[1][1] * v.y) + (m.c[2][1] * v.z + m.c[3][1]),
               (m.c[0][2] * v.x + m.c[1][2] * v.y) + (m.c[2][2] * v.z + m.c[3][2]));
 }
-__device__ __forceinline__ f3 xform_vector(const Affine& m, f3 v) {
+template <class M>
+__device__ __forceinline__ f3 xform_vector(const M& m, f3 v) {
     return F3((m.c[0][0] * v.x + m.c[1][0] * v.y) + (m.c[2][0] * v.z + m.z3[0]),
               (m.c[0][1] * v.x + m.c[1][1] * v.y) + (m.c[2][1] * v.z + m.z3[1]),
               (m.c[0][2] * v.x + m.c[1][2] * v.y) + (m.c[2][2] * v.z + m.z3[2]));

@@ -10,6 +10,7 @@
 //   (lookback.h).  Algorithmic traffic: 8 B/element for scan (4 read + 4 write), 4 B/element +
 //   4 B/kept for compaction.
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -23,7 +24,7 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kChunks = 4;                       // int4 chunks per thread
 constexpr int kTile = kThreads * kChunks * 4;    // 4096 elements
-constexpr size_t kCtlBytes = 256;                // ticket, error word (padded)
+constexpr size_t kCtlBytes = 256;                // [0] unused, [1] device error word (padded)
 
 thread_local std::string g_err;
 thread_local float g_timer_ms = 0.f;
@@ -34,6 +35,7 @@ int hip_fail(hipError_t e, const char* where) {
 }
 
 enum Mode { kScan = 0, kCompact = 1, kPartition = 2 };
+typedef int v4i __attribute__((ext_vector_type(4)));
 
 template <int MODE, bool ALIGNED>
 __global__ __launch_bounds__(kThreads) void k_scan_tiles(const int32_t* __restrict__ in,
@@ -42,99 +44,103 @@ __global__ __launch_bounds__(kThreads) void k_scan_tiles(const int32_t* __restri
                                                          uint32_t* __restrict__ ctl,
                                                          int64_t* __restrict__ d_count,
                                                          int32_t* __restrict__ dead) {
-    __shared__ uint32_t s_tile;
     __shared__ uint32_t s_wsum[kChunks][4];
     __shared__ uint32_t s_excl;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    if (tid == 0) s_tile = atomicAdd(&ctl[0], 1u);
-    __syncthreads();
-    const int tile = (int)s_tile;
-    const int64_t base = (int64_t)tile * kTile;
-    const bool full = base + kTile <= n;
+    const int num_tiles = (int)((n + kTile - 1) / kTile);
+    // Persistent, statically assigned tiles (lookback.h: no ticket counter).
+    for (int tile = blockIdx.x; tile < num_tiles; tile += gridDim.x) {
+        const int64_t base = (int64_t)tile * kTile;
+        const bool full = base + kTile <= n;
 
-    int32_t v[kChunks][4];
+        int32_t v[kChunks][4];
 #pragma unroll
-    for (int k = 0; k < kChunks; ++k) {
-        const int64_t e0 = base + (int64_t)k * (kThreads * 4) + 4 * tid;
-        if (ALIGNED && full) {
-            const int4 q = *reinterpret_cast<const int4*>(in + e0);
-            v[k][0] = q.x; v[k][1] = q.y; v[k][2] = q.z; v[k][3] = q.w;
-        } else {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[k][e] = (e0 + e < n) ? in[e0 + e] : 0;
-        }
-    }
-    uint32_t s[kChunks], incl[kChunks];
-#pragma unroll
-    for (int k = 0; k < kChunks; ++k) {
-        if (MODE == kScan)
-            s[k] = ((uint32_t)v[k][0] + (uint32_t)v[k][1]) + ((uint32_t)v[k][2] + (uint32_t)v[k][3]);
-        else
-            s[k] = (uint32_t)(v[k][0] != 0) + (uint32_t)(v[k][1] != 0) + (uint32_t)(v[k][2] != 0) +
-                   (uint32_t)(v[k][3] != 0);
-        incl[k] = lb::wave_inclusive_scan(s[k]);
-        if (lane == 63) s_wsum[k][wave] = incl[k];
-    }
-    __syncthreads();
-    uint32_t off[kChunks];
-    uint32_t run = 0;
-#pragma unroll
-    for (int k = 0; k < kChunks; ++k) {
-        uint32_t before = 0;
-#pragma unroll
-        for (int w = 0; w < 4; ++w) {
-            const uint32_t x = s_wsum[k][w];
-            before += (w < wave) ? x : 0u;
-        }
-        off[k] = run + before;
-#pragma unroll
-        for (int w = 0; w < 4; ++w) run += s_wsum[k][w];
-    }
-    const uint32_t total = run;
-    if (wave == 0) {
-        uint32_t excl = 0;
-        if (tile == 0) {
-            if (lane == 0) lb::publish(status, 0, lb::kFlagPre, total);
-        } else {
-            if (lane == 0) lb::publish(status, tile, lb::kFlagAgg, total);
-            excl = lb::lookback(status, tile, lane, &ctl[1]);
-            if (lane == 0) lb::publish(status, tile, lb::kFlagPre, excl + total);
-        }
-        if (lane == 0) s_excl = excl;
-    }
-    __syncthreads();
-    const uint32_t excl = s_excl;
-#pragma unroll
-    for (int k = 0; k < kChunks; ++k) {
-        const int64_t e0 = base + (int64_t)k * (kThreads * 4) + 4 * tid;
-        uint32_t run_k = excl + off[k] + (incl[k] - s[k]);
-        if (MODE == kScan) {
-            int32_t o[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) { o[e] = (int32_t)run_k; run_k += (uint32_t)v[k][e]; }
+        for (int k = 0; k < kChunks; ++k) {
+            const int64_t e0 = base + (int64_t)k * (kThreads * 4) + 4 * tid;
             if (ALIGNED && full) {
-                *reinterpret_cast<int4*>(out + e0) = make_int4(o[0], o[1], o[2], o[3]);
+                const v4i q = __builtin_nontemporal_load(reinterpret_cast<const v4i*>(in + e0));
+                v[k][0] = q.x; v[k][1] = q.y; v[k][2] = q.z; v[k][3] = q.w;
             } else {
 #pragma unroll
-                for (int e = 0; e < 4; ++e)
-                    if (e0 + e < n) out[e0 + e] = o[e];
+                for (int e = 0; e < 4; ++e) v[k][e] = (e0 + e < n) ? in[e0 + e] : 0;
             }
-        } else if (MODE == kCompact) {
+        }
+        uint32_t s[kChunks], incl[kChunks];
 #pragma unroll
-            for (int e = 0; e < 4; ++e)
-                if (v[k][e] != 0) out[run_k++] = v[k][e];
-        } else {
+        for (int k = 0; k < kChunks; ++k) {
+            if (MODE == kScan)
+                s[k] = ((uint32_t)v[k][0] + (uint32_t)v[k][1]) + ((uint32_t)v[k][2] + (uint32_t)v[k][3]);
+            else
+                s[k] = (uint32_t)(v[k][0] != 0) + (uint32_t)(v[k][1] != 0) + (uint32_t)(v[k][2] != 0) +
+                       (uint32_t)(v[k][3] != 0);
+            incl[k] = lb::wave_inclusive_scan(s[k]);
+        }
+        __syncthreads();   // previous tile's readers of s_wsum / s_excl are done
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int64_t idx = e0 + e;
-                if (idx < n) {
-                    if (v[k][e] != 0) out[run_k++] = (int32_t)idx;
-                    else dead[idx - (int64_t)run_k] = (int32_t)idx;
+        for (int k = 0; k < kChunks; ++k)
+            if (lane == 63) s_wsum[k][wave] = incl[k];
+        __syncthreads();
+        uint32_t off[kChunks];
+        uint32_t run = 0;
+#pragma unroll
+        for (int k = 0; k < kChunks; ++k) {
+            uint32_t before = 0;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                const uint32_t x = s_wsum[k][w];
+                before += (w < wave) ? x : 0u;
+            }
+            off[k] = run + before;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) run += s_wsum[k][w];
+        }
+        const uint32_t total = run;
+        if (wave == 0) {
+            uint32_t excl = 0;
+            if (tile == 0) {
+                if (lane == 0) lb::publish(status, 0, lb::kFlagPre, total);
+            } else {
+                if (lane == 0) lb::publish(status, tile, lb::kFlagAgg, total);
+                excl = lb::lookback(status, tile, lane, &ctl[1]);
+                if (lane == 0) lb::publish(status, tile, lb::kFlagPre, excl + total);
+            }
+            if (lane == 0) s_excl = excl;
+        }
+        __syncthreads();
+        const uint32_t excl = s_excl;
+#pragma unroll
+        for (int k = 0; k < kChunks; ++k) {
+            const int64_t e0 = base + (int64_t)k * (kThreads * 4) + 4 * tid;
+            uint32_t run_k = excl + off[k] + (incl[k] - s[k]);
+            if (MODE == kScan) {
+                int32_t o[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) { o[e] = (int32_t)run_k; run_k += (uint32_t)v[k][e]; }
+                if (ALIGNED && full) {
+                    const v4i q = {o[0], o[1], o[2], o[3]};
+                    __builtin_nontemporal_store(q, reinterpret_cast<v4i*>(out + e0));
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        if (e0 + e < n) out[e0 + e] = o[e];
+                }
+            } else if (MODE == kCompact) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if (v[k][e] != 0) out[run_k++] = v[k][e];
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int64_t idx = e0 + e;
+                    if (idx < n) {
+                        if (v[k][e] != 0) out[run_k++] = (int32_t)idx;
+                        else dead[idx - (int64_t)run_k] = (int32_t)idx;
+                    }
                 }
             }
         }
+        if (MODE != kScan && tid == 0 && tile == num_tiles - 1) *d_count = (int64_t)(excl + total);
     }
-    if (MODE != kScan && tid == 0 && base + kTile >= n) *d_count = (int64_t)(excl + total);
 }
 
 __global__ void k_append_dead(const int32_t* __restrict__ dead, int32_t* __restrict__ perm,
@@ -144,6 +150,26 @@ __global__ void k_append_dead(const int32_t* __restrict__ dead, int32_t* __restr
     for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < ndead;
          j += (int64_t)gridDim.x * blockDim.x)
         perm[live + j] = dead[j];
+}
+
+// Co-resident persistent grid for a 256-thread kernel: CUs x blocks/CU, one block/CU below the
+// occupancy API's answer (it can over-report by one for SGPR-heavy kernels, MI355X_MICROARCH.md
+// "Residency and cooperative launch"), at most 8.
+int resident_grid(const void* kernel) {
+    static std::mutex mu;
+    static std::vector<std::pair<const void*, int>> cache;
+    std::lock_guard<std::mutex> lk(mu);
+    for (auto& e : cache)
+        if (e.first == kernel) return e.second;
+    int dev = 0, cus = 256, per_cu = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kThreads, 0) != hipSuccess || per_cu <= 0)
+        per_cu = 2;
+    per_cu = std::max(1, std::min(per_cu, 8) - 1);
+    const int g = cus * per_cu;
+    cache.push_back({kernel, g});
+    return g;
 }
 
 size_t status_bytes(int64_t n) {
@@ -203,12 +229,15 @@ int launch(const int32_t* d_in, int32_t* d_out, int64_t n, int64_t* d_count, voi
     if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(workspace)");
     const int64_t tiles = (n + kTile - 1) / kTile;
     const bool aligned = ((reinterpret_cast<uintptr_t>(d_in) | reinterpret_cast<uintptr_t>(d_out)) & 15) == 0;
-    if (aligned)
-        hipLaunchKernelGGL((k_scan_tiles<MODE, true>), dim3((unsigned)tiles), dim3(kThreads), 0, stream,
+    if (aligned) {
+        const int g = (int)std::min<int64_t>(tiles, resident_grid((const void*)k_scan_tiles<MODE, true>));
+        hipLaunchKernelGGL((k_scan_tiles<MODE, true>), dim3(g), dim3(kThreads), 0, stream,
                            d_in, d_out, n, status, ctl, d_count, dead);
-    else
-        hipLaunchKernelGGL((k_scan_tiles<MODE, false>), dim3((unsigned)tiles), dim3(kThreads), 0, stream,
+    } else {
+        const int g = (int)std::min<int64_t>(tiles, resident_grid((const void*)k_scan_tiles<MODE, false>));
+        hipLaunchKernelGGL((k_scan_tiles<MODE, false>), dim3(g), dim3(kThreads), 0, stream,
                            d_in, d_out, n, status, ctl, d_count, dead);
+    }
     e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "k_scan_tiles launch");
     if (MODE == kPartition) {

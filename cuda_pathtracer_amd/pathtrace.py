@@ -229,15 +229,20 @@ class PathTracer:
         depth = self.scene.state().traceDepth
         return {"segments": int(s.segments), "passes": int(s.passes),
                 "bounce_live": [int(s.bounce_live[k]) for k in range(depth)],
+                "bounce_emit": [int(s.bounce_emit[k]) for k in range(depth)],
                 "emissive_hits": int(s.emissive_hits)}
 
     def profile(self, on: bool = True) -> None:
         check_pt(lib().pt_profile_enable(self._h, int(on)))
 
+    KINDS = ("first_bounce", "bounce", "compact", "sort")
+
     def profile_read(self) -> dict:
-        bms, n, tms = C.c_double(), C.c_uint64(), C.c_double()
-        check_pt(lib().pt_profile_read(self._h, C.byref(bms), C.byref(n), C.byref(tms)))
-        return {"bounce_ms": bms.value, "bounce_launches": int(n.value), "total_ms": tms.value}
+        """{kind: (summed ms, launches)} since the previous read (HIP events on the launch stream)."""
+        ms = (C.c_double * 4)()
+        n = (C.c_uint64 * 4)()
+        check_pt(lib().pt_profile_read(self._h, ms, n))
+        return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(self.KINDS)}
 
 
 def tonemap(image: np.ndarray, samples: float) -> np.ndarray:

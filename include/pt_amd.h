@@ -121,6 +121,7 @@ typedef struct pt_stats_t {
     uint64_t passes;
     uint64_t bounce_live[64];     /* live paths entering bounce k (k < depth) */
     uint64_t emissive_hits;       /* paths that terminated with non-zero radiance (framebuffer adds) */
+    uint64_t bounce_emit[64];     /* of those, per bounce */
     uint32_t device_error;        /* nonzero: a device-side bound was hit */
     uint32_t reserved;
 } pt_stats_t;
@@ -182,11 +183,15 @@ int pt_get_image(pt_ctx* c, float* host_rgb);               /* tile accumulator,
 int pt_copy_image(pt_ctx* c, float* d_rgb, void* stream);   /* device-to-device copy */
 int pt_reset_image(pt_ctx* c, void* stream);
 int pt_stats(pt_ctx* c, pt_stats_t* out);                   /* synchronises the context stream */
-/* Per-kernel device timing with hipEvents on the launch stream (for the roofline).  When
- * enabled, pt_render_pass records events around every bounce kernel; pt_profile_read returns
- * the summed milliseconds and launch count of the fused bounce kernels and of everything. */
+/* Per-kernel device timing with hipEvents recorded on the launch stream (for the roofline).  When
+ * enabled, pt_render_pass brackets every launch with pooled events; pt_profile_read synchronises
+ * and returns, per kernel kind, the summed milliseconds and launch counts since the last read. */
+#define PT_KIND_FIRST_BOUNCE 0   /* k_trace<FIRST>: raygen + intersect + shade (bounce 0)      */
+#define PT_KIND_BOUNCE 1         /* k_trace: intersect + shade (bounces >= 1)                  */
+#define PT_KIND_COMPACT 2        /* k_compact_paths: stable compaction of the survivors        */
+#define PT_KIND_SORT 3           /* material-sorted mode: raygen/isect/scan/scatter/shade      */
 int pt_profile_enable(pt_ctx* c, int32_t on);
-int pt_profile_read(pt_ctx* c, double* bounce_ms, uint64_t* bounce_launches, double* total_ms);
+int pt_profile_read(pt_ctx* c, double ms[4], uint64_t launches[4]);
 
 /* ---- image output ---------------------------------------------------------------------- */
 /* saveImage + Image::savePNG pixel math: out[3*(y*W + (W-1-x)) + k] = uchar(clamp(rgb/spp,0,1)*255). */
