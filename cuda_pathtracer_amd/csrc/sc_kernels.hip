@@ -4,7 +4,7 @@
 // Common::kernMapToBoolean / kernScatter (common.cu:25-46).  The reference runs a recursive
 // Blelloch scan with 64 elements per block (blockDim = warpSize = 32), pads n to a power of two
 // and allocates/frees device memory on every call.  Here one launch streams each element once:
-//   tile = 256 threads x 4 x int4 = 4096 elements, loaded as wave-contiguous 16-byte vectors
+//   tile = 256 threads x 8 x int4 = 8192 elements, loaded as wave-contiguous 16-byte vectors
 //   (chunk k of a tile is 1 KiB per wave-instruction), per-thread 4-element scan, wave64 DPP scan
 //   of the per-thread sums, 16 wave totals through LDS, then a decoupled look-back across tiles
 //   (lookback.h).  Algorithmic traffic: 8 B/element for scan (4 read + 4 write), 4 B/element +
@@ -14,6 +14,7 @@
 #include <mutex>
 #include <string>
 #include <vector>
+#include <cstdlib>
 #include <cstring>
 
 #include "lookback.h"
@@ -22,9 +23,10 @@
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kChunks = 4;                       // int4 chunks per thread
-constexpr int kTile = kThreads * kChunks * 4;    // 4096 elements
-constexpr size_t kCtlBytes = 256;                // [0] unused, [1] device error word (padded)
+constexpr int kChunks = 8;                       // int4 chunks per thread
+constexpr int kTile = kThreads * kChunks * 4;    // 8192 elements (32 KiB)
+constexpr size_t kCtlBytes = 256;
+constexpr int64_t kMallMinElems = (int64_t)1 << 26;   // >= 256 MiB of int32 input                // [0] unused, [1] device error word (padded)
 
 thread_local std::string g_err;
 thread_local float g_timer_ms = 0.f;
@@ -37,6 +39,123 @@ int hip_fail(hipError_t e, const char* where) {
 enum Mode { kScan = 0, kCompact = 1, kPartition = 2 };
 typedef int v4i __attribute__((ext_vector_type(4)));
 
+// LDS-only workgroup barrier: waits for this wave's LDS traffic, not for its outstanding global
+// loads, so a prefetched tile stays in flight across it (cdna_hip_programming.md §5 "Pipelining
+// across barriers").
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ void load_full(const int32_t* __restrict__ in, int64_t base, int tid, v4i (&v)[kChunks]) {
+#pragma unroll
+    for (int k = 0; k < kChunks; ++k)
+        v[k] = __builtin_nontemporal_load(reinterpret_cast<const v4i*>(in + base + (int64_t)k * (kThreads * 4) + 4 * tid));
+}
+__device__ __forceinline__ void load_guarded(const int32_t* __restrict__ in, int64_t n, int64_t base, int tid,
+                                             v4i (&v)[kChunks]) {
+#pragma unroll
+    for (int k = 0; k < kChunks; ++k) {
+        const int64_t e0 = base + (int64_t)k * (kThreads * 4) + 4 * tid;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int64_t j = e0 + e < n ? e0 + e : n - 1;   // branch-free: clamp, then mask
+            const int32_t x = in[j];
+            v[k][e] = e0 + e < n ? x : 0;
+        }
+    }
+}
+
+// Everything after the loads: local + wave scans, block offsets, decoupled look-back, outputs.
+template <int MODE, bool VEC_STORE>
+__device__ __forceinline__ void process_tile(const v4i (&cur)[kChunks], int tile, int num_tiles, int64_t n,
+                                             int32_t* __restrict__ out, uint64_t* __restrict__ status,
+                                             uint32_t* __restrict__ ctl, int64_t* __restrict__ d_count,
+                                             int32_t* __restrict__ dead, uint32_t (&s_wsum)[kChunks][4],
+                                             uint32_t* s_excl) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t base = (int64_t)tile * kTile;
+    uint32_t s[kChunks], incl[kChunks];
+#pragma unroll
+    for (int k = 0; k < kChunks; ++k) {
+        if (MODE == kScan)
+            s[k] = ((uint32_t)cur[k][0] + (uint32_t)cur[k][1]) + ((uint32_t)cur[k][2] + (uint32_t)cur[k][3]);
+        else
+            s[k] = (uint32_t)(cur[k][0] != 0) + (uint32_t)(cur[k][1] != 0) + (uint32_t)(cur[k][2] != 0) +
+                   (uint32_t)(cur[k][3] != 0);
+        incl[k] = lb::wave_inclusive_scan(s[k]);
+    }
+    lds_barrier();   // previous tile's readers of s_wsum / s_excl are done
+    if (lane == 63) {
+#pragma unroll
+        for (int k = 0; k < kChunks; ++k) s_wsum[k][wave] = incl[k];
+    }
+    lds_barrier();
+    uint32_t off[kChunks];
+    uint32_t run = 0;
+#pragma unroll
+    for (int k = 0; k < kChunks; ++k) {
+        uint32_t before = 0;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            const uint32_t x = s_wsum[k][w];
+            before += (w < wave) ? x : 0u;
+        }
+        off[k] = run + before;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) run += s_wsum[k][w];
+    }
+    const uint32_t total = run;
+    if (wave == 0) {
+        uint32_t excl = 0;
+        if (tile == 0) {
+            if (lane == 0) lb::publish(status, 0, lb::kFlagPre, total);
+        } else {
+            if (lane == 0) lb::publish(status, tile, lb::kFlagAgg, total);
+            excl = lb::lookback(status, tile, lane, &ctl[1]);
+            if (lane == 0) lb::publish(status, tile, lb::kFlagPre, excl + total);
+        }
+        if (lane == 0) *s_excl = excl;
+    }
+    lds_barrier();
+    const uint32_t excl = *s_excl;
+#pragma unroll
+    for (int k = 0; k < kChunks; ++k) {
+        const int64_t e0 = base + (int64_t)k * (kThreads * 4) + 4 * tid;
+        uint32_t run_k = excl + off[k] + (incl[k] - s[k]);
+        if (MODE == kScan) {
+            v4i o;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) { o[e] = (int32_t)run_k; run_k += (uint32_t)cur[k][e]; }
+            if (VEC_STORE) {
+                __builtin_nontemporal_store(o, reinterpret_cast<v4i*>(out + e0));
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if (e0 + e < n) out[e0 + e] = o[e];
+            }
+        } else if (MODE == kCompact) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if (cur[k][e] != 0) out[run_k++] = cur[k][e];
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int64_t idx = e0 + e;
+                if (idx < n) {
+                    if (cur[k][e] != 0) out[run_k++] = (int32_t)idx;
+                    else dead[idx - (int64_t)run_k] = (int32_t)idx;
+                }
+            }
+        }
+    }
+    if (MODE != kScan && tid == 0 && tile == num_tiles - 1) *d_count = (int64_t)(excl + total);
+}
+
+// Persistent, statically assigned tiles (lookback.h), software-pipelined: the next full tile's
+// loads are issued before this tile's look-back so HBM stays busy while the prefix propagates.
+// The (single) partial tail tile is processed after the loop with guarded scalar loads.
 template <int MODE, bool ALIGNED>
 __global__ __launch_bounds__(kThreads) void k_scan_tiles(const int32_t* __restrict__ in,
                                                          int32_t* __restrict__ out, int64_t n,
@@ -46,101 +165,198 @@ __global__ __launch_bounds__(kThreads) void k_scan_tiles(const int32_t* __restri
                                                          int32_t* __restrict__ dead) {
     __shared__ uint32_t s_wsum[kChunks][4];
     __shared__ uint32_t s_excl;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x;
     const int num_tiles = (int)((n + kTile - 1) / kTile);
-    // Persistent, statically assigned tiles (lookback.h: no ticket counter).
-    for (int tile = blockIdx.x; tile < num_tiles; tile += gridDim.x) {
-        const int64_t base = (int64_t)tile * kTile;
-        const bool full = base + kTile <= n;
+    const int num_full = ALIGNED ? (int)(n / kTile) : 0;
+    int tile = blockIdx.x;
+    const int G = (int)gridDim.x;
+    if (tile < num_full) {
+        // Unrolled by two with named buffers (no loop-carried register copy, so the compiler's
+        // wait counts keep the prefetched tile in flight across process_tile).
+        v4i bufA[kChunks], bufB[kChunks];
+        load_full(in, (int64_t)tile * kTile, tid, bufA);
+        for (;;) {
+            // unconditional (clamped) prefetch: a branch here would make the wait-count pass merge
+            // "issued"/"skipped" states and drain the prefetch at the first use of bufA
+            const int t1 = tile + G;
+            load_full(in, (int64_t)(t1 < num_full ? t1 : tile) * kTile, tid, bufB);
+            process_tile<MODE, true>(bufA, tile, num_tiles, n, out, status, ctl, d_count, dead, s_wsum, &s_excl);
+            tile = t1;
+            if (tile >= num_full) break;
+            const int t2 = tile + G;
+            load_full(in, (int64_t)(t2 < num_full ? t2 : tile) * kTile, tid, bufA);
+            process_tile<MODE, true>(bufB, tile, num_tiles, n, out, status, ctl, d_count, dead, s_wsum, &s_excl);
+            tile = t2;
+            if (tile >= num_full) break;
+        }
+    }
+    for (; tile < num_tiles; tile += gridDim.x) {   // tail (and everything when unaligned)
+        v4i cur[kChunks];
+        load_guarded(in, n, (int64_t)tile * kTile, tid, cur);
+        process_tile<MODE, false>(cur, tile, num_tiles, n, out, status, ctl, d_count, dead, s_wsum, &s_excl);
+    }
+}
 
-        int32_t v[kChunks][4];
+// ---- large inputs: super-rounds that re-read from the Infinity Cache -------------------------
+// For n beyond the MALL, each super-round covers G blocks x S elements (S = mt tiles,
+// ~64 MiB per round).  Block b: pass 1 streams its sub-chunk from HBM and reduces it; ONE
+// look-back per block per round (status index r*G + b); pass 2 re-reads the same sub-chunk —
+// still resident in the 256 MiB MALL, since only ~64 MiB of other traffic happened since — and
+// writes the scanned output.  HBM moves 8 B/element; the look-back chain is per sub-chunk, not
+// per 32 KiB tile.
+constexpr int64_t kMallRoundBytes = (int64_t)64 << 20;   // per super-round, well below the MALL
+
+template <int MODE>
+__device__ __forceinline__ uint32_t tile_reduce(const v4i (&v)[kChunks]) {
+    uint32_t acc = 0;
 #pragma unroll
-        for (int k = 0; k < kChunks; ++k) {
-            const int64_t e0 = base + (int64_t)k * (kThreads * 4) + 4 * tid;
-            if (ALIGNED && full) {
-                const v4i q = __builtin_nontemporal_load(reinterpret_cast<const v4i*>(in + e0));
-                v[k][0] = q.x; v[k][1] = q.y; v[k][2] = q.z; v[k][3] = q.w;
-            } else {
+    for (int k = 0; k < kChunks; ++k) {
+        if (MODE == kScan)
+            acc += ((uint32_t)v[k][0] + (uint32_t)v[k][1]) + ((uint32_t)v[k][2] + (uint32_t)v[k][3]);
+        else
+            acc += (uint32_t)(v[k][0] != 0) + (uint32_t)(v[k][1] != 0) + (uint32_t)(v[k][2] != 0) +
+                   (uint32_t)(v[k][3] != 0);
+    }
+    return acc;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kThreads) void k_scan_mall(const int32_t* __restrict__ in, int32_t* __restrict__ out,
+                                                        int64_t n, uint64_t* __restrict__ status,
+                                                        uint32_t* __restrict__ ctl, int64_t* __restrict__ d_count,
+                                                        int32_t* __restrict__ dead, int mt, int xp) {
+    __shared__ uint32_t s_wsum[kChunks][4];
+    __shared__ uint32_t s_red[4];
+    __shared__ uint32_t s_excl;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int G = (int)gridDim.x, b = (int)blockIdx.x;
+    const int64_t S = (int64_t)mt * kTile;   // mt even
+    const int64_t round_elems = S * G;
+    const int rounds = (int)((n + round_elems - 1) / round_elems);
+    const int num_units = rounds * G;           // look-back index space
+    uint32_t sink = 0;                          // timing ablations only (xp != 0)
+    for (int r = 0; r < rounds; ++r) {
+        const int64_t lo = (int64_t)r * round_elems + (int64_t)b * S;
+        const int unit = r * G + b;
+        // pass 1: aggregate of the sub-chunk (HBM), two tiles in flight
+        uint32_t acc = 0;
+        if (xp & 4) {
+        } else if (lo + S <= n) {
+            v4i x[kChunks], y[kChunks];
+            load_full(in, lo, tid, x);
 #pragma unroll
-                for (int e = 0; e < 4; ++e) v[k][e] = (e0 + e < n) ? in[e0 + e] : 0;
+            for (int t = 0; t < mt; t += 2) {
+                load_full(in, lo + (int64_t)(t + 1) * kTile, tid, y);
+                acc += tile_reduce<MODE>(x);
+                if (t + 2 < mt) load_full(in, lo + (int64_t)(t + 2) * kTile, tid, x);
+                acc += tile_reduce<MODE>(y);
+            }
+        } else {
+            for (int t = 0; t < mt; ++t) {
+                const int64_t tb = lo + (int64_t)t * kTile;
+                if (tb >= n) break;
+                v4i x[kChunks];
+                load_guarded(in, n, tb, tid, x);
+                acc += tile_reduce<MODE>(x);
             }
         }
-        uint32_t s[kChunks], incl[kChunks];
-#pragma unroll
-        for (int k = 0; k < kChunks; ++k) {
-            if (MODE == kScan)
-                s[k] = ((uint32_t)v[k][0] + (uint32_t)v[k][1]) + ((uint32_t)v[k][2] + (uint32_t)v[k][3]);
-            else
-                s[k] = (uint32_t)(v[k][0] != 0) + (uint32_t)(v[k][1] != 0) + (uint32_t)(v[k][2] != 0) +
-                       (uint32_t)(v[k][3] != 0);
-            incl[k] = lb::wave_inclusive_scan(s[k]);
-        }
-        __syncthreads();   // previous tile's readers of s_wsum / s_excl are done
-#pragma unroll
-        for (int k = 0; k < kChunks; ++k)
-            if (lane == 63) s_wsum[k][wave] = incl[k];
-        __syncthreads();
-        uint32_t off[kChunks];
-        uint32_t run = 0;
-#pragma unroll
-        for (int k = 0; k < kChunks; ++k) {
-            uint32_t before = 0;
-#pragma unroll
-            for (int w = 0; w < 4; ++w) {
-                const uint32_t x = s_wsum[k][w];
-                before += (w < wave) ? x : 0u;
-            }
-            off[k] = run + before;
-#pragma unroll
-            for (int w = 0; w < 4; ++w) run += s_wsum[k][w];
-        }
-        const uint32_t total = run;
+        // block reduce -> publish aggregate -> look-back
+        uint32_t wacc = lb::wave_sum(acc);
+        lds_barrier();
+        if (lane == 0) s_red[wave] = wacc;
+        lds_barrier();
+        const uint32_t agg = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
         if (wave == 0) {
             uint32_t excl = 0;
-            if (tile == 0) {
-                if (lane == 0) lb::publish(status, 0, lb::kFlagPre, total);
+            if (unit == 0 || (xp & 1)) {
+                if (lane == 0) lb::publish(status, unit, lb::kFlagPre, agg);
             } else {
-                if (lane == 0) lb::publish(status, tile, lb::kFlagAgg, total);
-                excl = lb::lookback(status, tile, lane, &ctl[1]);
-                if (lane == 0) lb::publish(status, tile, lb::kFlagPre, excl + total);
+                if (lane == 0) lb::publish(status, unit, lb::kFlagAgg, agg);
+                excl = lb::lookback(status, unit, lane, &ctl[1]);
+                if (lane == 0) lb::publish(status, unit, lb::kFlagPre, excl + agg);
             }
             if (lane == 0) s_excl = excl;
         }
-        __syncthreads();
-        const uint32_t excl = s_excl;
+        lds_barrier();
+        uint32_t running = s_excl;
+        // pass 2: re-read (MALL), scan, write
+        for (int t = 0; t < mt; ++t) {
+            const int64_t tb = lo + (int64_t)t * kTile;
+            if (tb >= n) break;
+            const bool full = tb + kTile <= n;
+            v4i cur[kChunks];
+            if (xp & 2) {
 #pragma unroll
-        for (int k = 0; k < kChunks; ++k) {
-            const int64_t e0 = base + (int64_t)k * (kThreads * 4) + 4 * tid;
-            uint32_t run_k = excl + off[k] + (incl[k] - s[k]);
-            if (MODE == kScan) {
-                int32_t o[4];
+                for (int k = 0; k < kChunks; ++k) cur[k] = v4i{tid, k, r, t};
+            } else if (full) load_full(in, tb, tid, cur);
+            else load_guarded(in, n, tb, tid, cur);
+            uint32_t sv[kChunks], incl[kChunks];
 #pragma unroll
-                for (int e = 0; e < 4; ++e) { o[e] = (int32_t)run_k; run_k += (uint32_t)v[k][e]; }
-                if (ALIGNED && full) {
-                    const v4i q = {o[0], o[1], o[2], o[3]};
-                    __builtin_nontemporal_store(q, reinterpret_cast<v4i*>(out + e0));
-                } else {
+            for (int k = 0; k < kChunks; ++k) {
+                if (MODE == kScan)
+                    sv[k] = ((uint32_t)cur[k][0] + (uint32_t)cur[k][1]) + ((uint32_t)cur[k][2] + (uint32_t)cur[k][3]);
+                else
+                    sv[k] = (uint32_t)(cur[k][0] != 0) + (uint32_t)(cur[k][1] != 0) + (uint32_t)(cur[k][2] != 0) +
+                            (uint32_t)(cur[k][3] != 0);
+                incl[k] = lb::wave_inclusive_scan(sv[k]);
+            }
+            lds_barrier();
+            if (lane == 63) {
+#pragma unroll
+                for (int k = 0; k < kChunks; ++k) s_wsum[k][wave] = incl[k];
+            }
+            lds_barrier();
+            uint32_t run = 0;
+            uint32_t off[kChunks];
+#pragma unroll
+            for (int k = 0; k < kChunks; ++k) {
+                uint32_t before = 0;
+#pragma unroll
+                for (int w = 0; w < 4; ++w) {
+                    const uint32_t xw = s_wsum[k][w];
+                    before += (w < wave) ? xw : 0u;
+                }
+                off[k] = run + before;
+#pragma unroll
+                for (int w = 0; w < 4; ++w) run += s_wsum[k][w];
+            }
+#pragma unroll
+            for (int k = 0; k < kChunks; ++k) {
+                const int64_t e0 = tb + (int64_t)k * (kThreads * 4) + 4 * tid;
+                uint32_t run_k = running + off[k] + (incl[k] - sv[k]);
+                if (MODE == kScan) {
+                    v4i o;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) { o[e] = (int32_t)run_k; run_k += (uint32_t)cur[k][e]; }
+                    if (xp & 8) {
+                        sink += (uint32_t)(o[0] ^ o[1] ^ o[2] ^ o[3]);
+                    } else if (full) {
+                        __builtin_nontemporal_store(o, reinterpret_cast<v4i*>(out + e0));
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+                            if (e0 + e < n) out[e0 + e] = o[e];
+                    }
+                } else if (MODE == kCompact) {
 #pragma unroll
                     for (int e = 0; e < 4; ++e)
-                        if (e0 + e < n) out[e0 + e] = o[e];
-                }
-            } else if (MODE == kCompact) {
+                        if (cur[k][e] != 0) out[run_k++] = cur[k][e];
+                } else {
 #pragma unroll
-                for (int e = 0; e < 4; ++e)
-                    if (v[k][e] != 0) out[run_k++] = v[k][e];
-            } else {
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const int64_t idx = e0 + e;
-                    if (idx < n) {
-                        if (v[k][e] != 0) out[run_k++] = (int32_t)idx;
-                        else dead[idx - (int64_t)run_k] = (int32_t)idx;
+                    for (int e = 0; e < 4; ++e) {
+                        const int64_t idx = e0 + e;
+                        if (idx < n) {
+                            if (cur[k][e] != 0) out[run_k++] = (int32_t)idx;
+                            else dead[idx - (int64_t)run_k] = (int32_t)idx;
+                        }
                     }
                 }
             }
+            running += run;
         }
-        if (MODE != kScan && tid == 0 && tile == num_tiles - 1) *d_count = (int64_t)(excl + total);
+        if (MODE != kScan && tid == 0 && unit == num_units - 1) *d_count = (int64_t)running;
     }
+    if (xp & 8) dead[(int64_t)b * kThreads + tid] = (int32_t)sink;   // keeps the ablated work live
 }
 
 __global__ void k_append_dead(const int32_t* __restrict__ dead, int32_t* __restrict__ perm,
@@ -172,9 +388,22 @@ int resident_grid(const void* kernel) {
     return g;
 }
 
+int env_int(const char* name, int dflt) {
+    const char* v = getenv(name);
+    return v && *v ? atoi(v) : dflt;
+}
+int cu_count() {
+    int dev = 0, cus = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    return cus;
+}
+
 size_t status_bytes(int64_t n) {
-    const int64_t tiles = (n + kTile - 1) / kTile;
-    return (size_t)(tiles > 0 ? tiles : 1) * sizeof(uint64_t);
+    // per-tile words for k_scan_tiles; k_scan_mall uses rounds x G <= n / (2 kTile) + G
+    // words, which is below this bound for n >= kMallMinElems; the +2048 covers G anyway.
+    const int64_t tiles = (n + kTile - 1) / kTile + 2048;
+    return (size_t)tiles * sizeof(uint64_t);
 }
 
 struct Workspace {
@@ -229,7 +458,21 @@ int launch(const int32_t* d_in, int32_t* d_out, int64_t n, int64_t* d_count, voi
     if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(workspace)");
     const int64_t tiles = (n + kTile - 1) / kTile;
     const bool aligned = ((reinterpret_cast<uintptr_t>(d_in) | reinterpret_cast<uintptr_t>(d_out)) & 15) == 0;
-    if (aligned) {
+    // Infinity-Cache two-pass scheme for inputs well beyond the 256 MiB MALL (and out of place:
+    // pass 2 re-reads the input after other blocks have written outputs).
+    static const bool use_mall = env_int("SC_MALL", 1) != 0;
+    if (use_mall && aligned && d_in != d_out && n >= kMallMinElems) {
+        // SC_EXPERIMENT / SC_PER_CU / SC_ROUND_MB: timing ablations for tuning (results are not
+        // valid when SC_EXPERIMENT is set); unset in production.
+        static const int xp = env_int("SC_EXPERIMENT", 0);
+        static const int per_cu_env = env_int("SC_PER_CU", 0);
+        static const int64_t round_bytes = (int64_t)env_int("SC_ROUND_MB", (int)(kMallRoundBytes >> 20)) << 20;
+        int g = resident_grid((const void*)k_scan_mall<MODE>);
+        if (per_cu_env > 0) g = cu_count() * per_cu_env;
+        const int mt = std::max<int>(2, (int)(round_bytes / ((int64_t)g * kTile * 4)) & ~1);
+        hipLaunchKernelGGL((k_scan_mall<MODE>), dim3(g), dim3(kThreads), 0, stream, d_in, d_out, n, status, ctl,
+                           d_count, dead, mt, xp);
+    } else if (aligned) {
         const int g = (int)std::min<int64_t>(tiles, resident_grid((const void*)k_scan_tiles<MODE, true>));
         hipLaunchKernelGGL((k_scan_tiles<MODE, true>), dim3(g), dim3(kThreads), 0, stream,
                            d_in, d_out, n, status, ctl, d_count, dead);

@@ -1,0 +1,62 @@
+"""Pixel sharding across GPUs: one process per GPU, rows y % world == rank, one gather at the end.
+
+The reference renders on one GPU (PT/src/pathtrace.cu:437-525); SURVEY.md §8e: pixels are
+independent, so rank r owns the rows y with y % world == r (row-interleaved for load balance:
+the light and the open front make per-row cost uneven), scene data is replicated, and the only
+collective is ONE gather of the float accumulators to rank 0 when the image is saved.  Message
+per rank: ceil(H / world) * W * 12 bytes.
+
+The device side of the partition lives in pt_kernels.hip (TileDev: global pixel index of a tile
+row); this module is the host side: row bookkeeping, padding and the gather.  It is backend
+agnostic — RCCL ("nccl") on the GPU box, gloo in the CPU tests.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def shard_rows(height: int, rank: int, world: int) -> int:
+    """Number of image rows rank `rank` owns (rows y with y % world == rank)."""
+    if world < 1 or not (0 <= rank < world):
+        raise ValueError(f"bad shard rank={rank} world={world}")
+    return max(0, (height - rank + world - 1) // world)
+
+
+def max_shard_rows(height: int, world: int) -> int:
+    return (height + world - 1) // world
+
+
+def row_of(tile_row: int, rank: int, world: int) -> int:
+    """Global image row of local tile row `tile_row`."""
+    return tile_row * world + rank
+
+
+def assemble(tiles, height: int, world: int) -> np.ndarray:
+    """Interleave per-rank tiles ((>= rows_r, W, 3) arrays, rank order) into the (H, W, 3) image."""
+    if len(tiles) != world:
+        raise ValueError(f"expected {world} tiles, got {len(tiles)}")
+    width = np.asarray(tiles[0]).shape[1]
+    full = np.zeros((height, width, 3), np.float32)
+    for r, t in enumerate(tiles):
+        rows = shard_rows(height, r, world)
+        full[r::world] = np.asarray(t)[:rows]
+    return full
+
+
+def gather_image(torch, dist, tile, height: int, group=None):
+    """Gather every rank's (rows_r, W, 3) float32 tile to rank 0; returns the (H, W, 3) numpy
+    image on rank 0 and None elsewhere.  `tile` is a torch tensor on the collective's device
+    (cuda for RCCL, cpu for gloo).  Tiles are padded to ceil(H / world) rows so a single
+    fixed-size gather suffices."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    rows = shard_rows(height, rank, world)
+    if tile.dim() != 3 or tile.shape[0] < rows or tile.shape[2] != 3:
+        raise ValueError(f"tile shape {tuple(tile.shape)} does not hold {rows} rows of RGB")
+    send = torch.zeros((max_shard_rows(height, world), tile.shape[1], 3), dtype=torch.float32, device=tile.device)
+    send[:rows] = tile[:rows]
+    recv = [torch.empty_like(send) for _ in range(world)] if rank == 0 else None
+    dist.gather(send, recv, dst=0, group=group)
+    if rank != 0:
+        return None
+    return assemble([t.cpu().numpy() for t in recv], height, world)

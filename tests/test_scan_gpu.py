@@ -121,6 +121,30 @@ def test_host_api_reference_semantics(gpu_device):
     assert Efficient.compact(7, o, a) == 5 and o[:5].tolist() == [1, 5, 1, 2, 3]
 
 
+@pytest.mark.parametrize("n", [1 << 26, (1 << 26) + 12345, (1 << 27) + 5])
+def test_large_inputs_match_oracle(gpu_device, n):
+    """Inputs past the 256 MiB Infinity Cache take the two-pass super-round kernel
+    (sc_kernels.hip k_scan_mall): full-array parity for scan, compaction and partition."""
+    import torch
+    from cuda_pathtracer_amd import compact_device, partition_device, scan_device
+    a = _gen(n, 50, n)
+    d = torch.from_numpy(a).to(gpu_device)
+    np.testing.assert_array_equal(scan_device(d).cpu().numpy(), O.scan(a))
+    f = (a % 4).astype(np.int32)
+    df = torch.from_numpy(f).to(gpu_device)
+    out, cnt = compact_device(df)
+    ref = O.compact_without_scan(f)
+    assert int(cnt.item()) == len(ref)
+    np.testing.assert_array_equal(out[:len(ref)].cpu().numpy(), ref)
+    del out
+    perm, live = partition_device(df)
+    ref_perm, ref_live = O.partition_indices(f)
+    assert int(live.item()) == ref_live
+    np.testing.assert_array_equal(perm.cpu().numpy(), ref_perm)
+    del d, df, perm
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.slow
 def test_reference_size_2e28_properties(gpu_device):
     """SIZE = 1<<28 and NPOT = SIZE-3 (main.cpp:8-9): size-independent checks on the device."""
