@@ -7,10 +7,12 @@ the image rows y % N == r and traces N samples per pixel per pass (spp = N), so 
 After the timed passes the float tiles are gathered to rank 0 with one RCCL gather (inside the
 timed region).  value = all ranks' traced segments / max-over-ranks wall time / 1e6.
 
-Roofline: the dominant kernel is the fused bounce kernel k_bounce<false,true> (bounces >= 1).
-Its average launch time comes from HIP events recorded on its launch stream over the timed
-passes; its algorithmic bytes per launch are path-state SoA read 44 B x paths in + write
-44 B x survivors + framebuffer read-modify-write 24 B x emissive terminations.
+Roofline: the dominant kernel is the fused bounce kernel k_bounce<false,...> (bounces >= 1).
+Its average launch time comes from HIP events recorded on its launch stream over a profiled
+segment of the same workload; its algorithmic bytes per launch are SURVEY.md §8d's 184 B per
+traced segment (ray 24 + hit write 28 + hit read 28 + path read 48 + write 48 + compaction 8)
+x the segments that launch traces.  The fused kernel itself needs only
+44 B in + 44 B per survivor + 24 B per emissive hit, reported as kernel_min_bytes.
 The scan kernel is measured separately at n = 2^28 (8 B/element, 2 GiB, beyond the 256 MiB MALL).
 """
 from __future__ import annotations
@@ -29,7 +31,8 @@ sys.path.insert(0, str(ROOT))
 
 METRIC = "Mray/s (paths×bounces/s) on Cornell scene + scan GB/s vs HBM peak, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-PATH_BYTES = 44                # o(12) d(12) c(12) slot(4) bounces(4)
+SEGMENT_BYTES = 184            # SURVEY.md §8d algorithmic bytes per traced segment
+PATH_BYTES = 44                # fused kernel's path state: o(12) d(12) c(12) slot(4) bounces(4)
 FB_RMW_BYTES = 24              # float3 read + write
 
 
@@ -139,6 +142,7 @@ def main() -> None:
         torch.cuda.synchronize()
 
     import cuda_pathtracer_amd as P
+    from cuda_pathtracer_amd import distributed as D
     P.lib()
 
     scene = P.Scene(args.scene)
@@ -165,13 +169,7 @@ def main() -> None:
     # single RCCL gather of the framebuffer tiles to rank 0
     pt.copy_image_to(tile.data_ptr(), stream)
     if dist is not None:
-        max_rows = (scene.camera().res[1] + world - 1) // world
-        send = torch.zeros((max_rows, pt.width, 3), dtype=torch.float32, device=dev)
-        send[:pt.rows] = tile
-        gather = [torch.empty_like(send) for _ in range(world)] if rank == 0 else None
-        dist.gather(send, gather, dst=0)
-        if rank == 0:
-            rows_all = gather
+        rows_all = D.gather_tiles(torch, dist, tile, scene.camera().res[1])
     barrier()
     elapsed = time.perf_counter() - t0
     s1 = pt.stats()
@@ -196,12 +194,8 @@ def main() -> None:
     t_max = elapsed
     seg_all = seg
     if dist is not None:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t_max = float(tt.item())
-        ss = torch.tensor([seg], dtype=torch.int64, device=dev)
-        dist.all_reduce(ss, op=dist.ReduceOp.SUM)
-        seg_all = int(ss.item())
+        t_max = D.max_over_ranks(torch, dist, elapsed, dev)
+        seg_all = D.sum_over_ranks(torch, dist, seg, dev)
 
     # roofline of the dominant kernel (bounces >= 1), over the profiled segment
     b_ms, b_n = prof["bounce"]
@@ -209,27 +203,25 @@ def main() -> None:
     depth = st_r.traceDepth
     plive = [b - a for a, b in zip(sp0["bounce_live"], sp1["bounce_live"])]
     pemit = [b - a for a, b in zip(sp0["bounce_emit"], sp1["bounce_emit"])]
-    bytes_bounce = 0
+    seg_bounce = sum(plive[1:depth])
+    kernel_min = 0
     for b in range(1, depth):
-        n_in = plive[b]
         n_out = plive[b + 1] if b + 1 < depth else 0
-        bytes_bounce += PATH_BYTES * n_in + PATH_BYTES * n_out + FB_RMW_BYTES * pemit[b]
-    per_launch_bytes = bytes_bounce / max(b_n, 1)
+        kernel_min += PATH_BYTES * plive[b] + PATH_BYTES * n_out + FB_RMW_BYTES * pemit[b]
+    per_launch_bytes = SEGMENT_BYTES * seg_bounce / max(b_n, 1)
     avg_ms = b_ms / max(b_n, 1)
     achieved = per_launch_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": _traffic_from_profiles("k_bounce"),
-                "kernel": "k_bounce<false,true>", "avg_launch_ms": avg_ms, "launches": b_n,
-                "algorithmic_bytes_per_launch": per_launch_bytes}
+                "kernel": "k_bounce<false,true,false>", "avg_launch_ms": avg_ms, "launches": b_n,
+                "segments_per_launch": seg_bounce / max(b_n, 1),
+                "algorithmic_bytes_per_launch": per_launch_bytes,
+                "kernel_min_bytes_per_launch": kernel_min / max(b_n, 1)}
 
     result = None
     if rank == 0:
         if rows_all is not None:
-            H = scene.camera().res[1]
-            full = np.zeros((H, pt.width, 3), np.float32)
-            for r, t in enumerate(rows_all):
-                rows_r = (H - r + world - 1) // world
-                full[r::world] = t[:rows_r].cpu().numpy()
+            full = D.assemble([t.cpu().numpy() for t in rows_all], scene.camera().res[1], world)
             assert np.isfinite(full).all()
         value = seg_all / t_max / 1e6
         result = {

@@ -9,6 +9,7 @@ from ._native import LIB_PATH, NativeLibraryError, PtError, lib  # noqa: F401
 from .pathtrace import (  # noqa: F401
     CUBE, MESH, SPHERE, GuiDataContainer, InitDataContainer, PathTracer, Scene, pathtrace, pathtraceFree,
     pathtraceInit, render, save_image, tonemap)
+from . import distributed  # noqa: F401
 from .stream_compaction import Efficient, compact_device, partition_device, scan_device  # noqa: F401
 
 __all__ = ["Scene", "PathTracer", "GuiDataContainer", "Efficient", "scan_device", "compact_device",

@@ -43,11 +43,11 @@ def assemble(tiles, height: int, world: int) -> np.ndarray:
     return full
 
 
-def gather_image(torch, dist, tile, height: int, group=None):
-    """Gather every rank's (rows_r, W, 3) float32 tile to rank 0; returns the (H, W, 3) numpy
-    image on rank 0 and None elsewhere.  `tile` is a torch tensor on the collective's device
-    (cuda for RCCL, cpu for gloo).  Tiles are padded to ceil(H / world) rows so a single
-    fixed-size gather suffices."""
+def gather_tiles(torch, dist, tile, height: int, group=None):
+    """ONE gather of every rank's (rows_r, W, 3) float32 tile to rank 0.  Returns the list of
+    padded tiles (device tensors, rank order) on rank 0 and None elsewhere.  `tile` lives on the
+    collective's device (cuda for RCCL, cpu for gloo).  Tiles are padded to ceil(H / world) rows
+    so a single fixed-size gather suffices."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     rows = shard_rows(height, rank, world)
@@ -57,6 +57,26 @@ def gather_image(torch, dist, tile, height: int, group=None):
     send[:rows] = tile[:rows]
     recv = [torch.empty_like(send) for _ in range(world)] if rank == 0 else None
     dist.gather(send, recv, dst=0, group=group)
-    if rank != 0:
+    return recv if rank == 0 else None
+
+
+def gather_image(torch, dist, tile, height: int, group=None):
+    """gather_tiles + assemble: the (H, W, 3) numpy image on rank 0, None elsewhere."""
+    tiles = gather_tiles(torch, dist, tile, height, group)
+    if tiles is None:
         return None
-    return assemble([t.cpu().numpy() for t in recv], height, world)
+    return assemble([t.cpu().numpy() for t in tiles], height, len(tiles))
+
+
+def max_over_ranks(torch, dist, seconds: float, device) -> float:
+    """Wall time of the slowest rank (the bench's timed region ends when every rank is done)."""
+    t = torch.tensor([float(seconds)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(torch, dist, count: int, device) -> int:
+    """Units (traced segments) processed by all ranks together."""
+    t = torch.tensor([int(count)], dtype=torch.int64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return int(t.item())

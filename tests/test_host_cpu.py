@@ -1,0 +1,173 @@
+"""Host-side product code on the CPU (no GPU): the C ABI loads and exports every declared symbol,
+the scene loader matches the oracle's independent parse bit for bit, tonemap/PNG output matches
+saveImage, errors are reported as status codes, and the device entry points fail loudly when no
+GPU is present (there is no CPU fallback).
+
+Reference: scene.cpp:33-219 (loader), utilities.cpp:84-92 (transforms), main.cpp:88-136 (camera
+recompute, saveImage), image.cpp:22-42 (PNG), pathtrace.h:6-9 / efficient.h:9-11 (API surface).
+"""
+from __future__ import annotations
+
+import json
+import re
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+import cuda_pathtracer_amd as P
+from cuda_pathtracer_amd import _native as N
+from oracle import binding as O
+
+ROOT = Path(__file__).resolve().parent.parent
+SCENES = ROOT / "tests" / "scenes"
+
+
+def _declared_functions() -> set[str]:
+    names = set()
+    for h in (ROOT / "include").glob("*.h"):
+        text = re.sub(r"/\*.*?\*/", "", h.read_text(), flags=re.S)
+        for m in re.finditer(r"^[A-Za-z_][\w\s\*]*?\b((?:pt|sc)_\w+)\s*\(", text, flags=re.M):
+            names.add(m.group(1))
+    return names
+
+
+def test_abi_exports_every_declared_symbol():
+    declared = _declared_functions()
+    assert len(declared) >= 40
+    L = N.lib()
+    missing = [n for n in sorted(declared) if not hasattr(L, n)]
+    assert not missing, f"declared in include/*.h but not exported: {missing}"
+    assert declared == set(N.SIGNATURES), (declared ^ set(N.SIGNATURES))
+
+
+def test_abi_struct_sizes_match_header():
+    text = (ROOT / "include" / "pt_amd.h").read_text()
+    for struct, size in (("pt_material", 48), ("pt_geom", 272), ("pt_triangle", 124), ("pt_bvh_node", 40)):
+        assert struct in text
+    import ctypes as C
+    assert C.sizeof(N.Material) == 48 and C.sizeof(N.Geom) == 272
+    assert C.sizeof(N.Triangle) == 124 and C.sizeof(N.BvhNode) == 40
+    assert C.sizeof(N.Camera) == 4 * (2 + 3 * 5 + 4)
+
+
+def _f(a):
+    return np.array(list(a), np.float32)
+
+
+@pytest.mark.parametrize("scene", ["cornell.json", "sphere.json"])
+def test_scene_loader_matches_oracle(scene):
+    path = SCENES / scene
+    ps = P.Scene(path)
+    osc = O.OracleScene.from_json(path)
+    ng, nm, ntri, nnode, ntex = ps.counts()
+    assert (ng, nm, ntri, nnode, ntex) == (len(osc.geoms), len(osc.materials), 0, 0, 0)
+    for g, og in zip(ps.geoms(), osc.geoms):
+        assert g.type == og.type and g.material_id == og.materialid
+        for a, b in (("translation", "translation"), ("rotation", "rotation"), ("scale", "scale"),
+                     ("transform", "transform"), ("inverse_transform", "inverse_transform"),
+                     ("inv_transpose", "inv_transpose")):
+            np.testing.assert_array_equal(_f(getattr(g, a)), _f(getattr(og, b)), err_msg=f"{scene} {a}")
+    for m, om in zip(ps.materials(), osc.materials):
+        for k in ("color", "spec_color"):
+            np.testing.assert_array_equal(_f(getattr(m, k)), _f(getattr(om, k)))
+        for k in ("spec_exponent", "has_reflective", "has_refractive", "ior", "emittance"):
+            assert np.float32(getattr(m, k)) == np.float32(getattr(om, k)), k
+    c, oc = ps.camera(), osc.cam
+    assert tuple(c.res) == tuple(oc.res)
+    for k in ("position", "look_at", "view", "up", "right", "fov", "pixel_length"):
+        np.testing.assert_array_equal(_f(getattr(c, k)), _f(getattr(oc, k)), err_msg=k)
+    st = ps.state()
+    assert st.traceDepth == osc.depth and st.iterations == osc.iterations and st.imageName == osc.file
+
+
+def test_materials_are_alphabetical():
+    """nlohmann::json objects iterate in std::map order, so material ids are alphabetical
+    (scene.cpp:40-85); objects refer to them by name."""
+    data = json.loads((SCENES / "cornell.json").read_text())
+    names = sorted(data["Materials"])
+    mats = P.Scene(SCENES / "cornell.json").materials()
+    for i, name in enumerate(names):
+        rgb = data["Materials"][name].get("RGB", [0, 0, 0])
+        np.testing.assert_array_equal(_f(mats[i].color), np.array(rgb, np.float32))
+
+
+def test_programmatic_scene_matches_json(tmp_path):
+    data = json.loads((SCENES / "cornell.json").read_text())
+    js = P.Scene(SCENES / "cornell.json")
+    sc = P.Scene()
+    ids = {}
+    for name in sorted(data["Materials"]):
+        p = data["Materials"][name]
+        rgb = p.get("RGB", [0.0, 0.0, 0.0])
+        ids[name] = sc.add_material(rgb=rgb, specrgb=p.get("SPECRGB", rgb), specex=p.get("SPECEX", 1.0),
+                                    reflective=p.get("REFLECTIVE", 0.0), emittance=p.get("EMITTANCE", 0.0))
+    for o in data["Objects"]:
+        sc.add_geom({"sphere": P.SPHERE, "cube": P.CUBE}[o["TYPE"]], ids[o["MATERIAL"]], o["TRANS"], o["ROTAT"],
+                    o["SCALE"])
+    c = data["Camera"]
+    sc.set_camera(c["RES"], c["FOVY"], c["EYE"], c["LOOKAT"], c["UP"])
+    sc.set_render(c["ITERATIONS"], c["DEPTH"], c["FILE"])
+    sc.finalize()
+    for a, b in zip(sc.geoms(), js.geoms()):
+        np.testing.assert_array_equal(_f(a.inverse_transform), _f(b.inverse_transform))
+    for k in ("position", "view", "right", "pixel_length"):
+        np.testing.assert_array_equal(_f(getattr(sc.camera(), k)), _f(getattr(js.camera(), k)))
+
+
+def test_scene_errors_are_status_codes(tmp_path):
+    with pytest.raises(N.PtError, match="open|read|exist|No such"):
+        P.Scene(tmp_path / "missing.json")
+    bad = tmp_path / "bad.json"
+    bad.write_text("{ not json")
+    with pytest.raises(N.PtError):
+        P.Scene(bad)
+    data = json.loads((SCENES / "cornell.json").read_text())
+    data["Camera"]["DEPTH"] = 65                          # device arrays hold <= 64 bounces
+    deep = tmp_path / "deep.json"
+    deep.write_text(json.dumps(data))
+    with pytest.raises(N.PtError, match="[Dd]epth|DEPTH"):
+        P.Scene(deep)
+    sc = P.Scene()
+    sc.add_geom(P.CUBE, 3, (0, 0, 0), (0, 0, 0), (1, 1, 1))   # materials may be added later ...
+    sc.set_camera((8, 8), 45.0, (0, 0, 5), (0, 0, 0))
+    with pytest.raises(N.PtError, match="material"):
+        sc.finalize()                                          # ... but must exist at finalize
+    with pytest.raises(N.PtError, match="camera"):
+        P.Scene().finalize()
+
+
+def test_tonemap_matches_oracle_and_png_roundtrip(tmp_path):
+    rng = np.random.default_rng(5)
+    img = rng.uniform(0, 3.0, size=(37, 53, 3)).astype(np.float32)
+    img[0, 0] = [np.inf, -1.0, 0.0]
+    out = P.tonemap(img, 2.0)
+    np.testing.assert_array_equal(out[1:], O.tonemap(img, 2.0)[1:])
+    np.testing.assert_array_equal(out[0, :-1], O.tonemap(img, 2.0)[0, :-1])
+    path = tmp_path / "x.png"
+    P.save_image(str(path), img, 2.0)
+    from PIL import Image
+    png = np.asarray(Image.open(path).convert("RGB"))
+    assert png.shape == (37, 53, 3)
+    np.testing.assert_array_equal(png, out)
+
+
+def test_device_entry_points_fail_loudly_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    sc = P.Scene(SCENES / "cornell.json")
+    with pytest.raises(N.PtError):
+        P.PathTracer(sc)
+    a = np.array([1, 5, 0, 1, 2, 0, 3], np.int32)
+    with pytest.raises(N.PtError):
+        P.Efficient.scan(7, np.zeros(7, np.int32), a)
+
+
+def test_product_does_not_import_oracle():
+    """The oracle is test infrastructure: the product package never imports, loads or links it
+    (build.py only compiles it, as build() must)."""
+    pat = re.compile(r"(import\s+oracle|from\s+oracle|liboracle|oracle_[a-z]+\s*\(|pt_oracle|sc_oracle)")
+    for f in (ROOT / "cuda_pathtracer_amd").rglob("*"):
+        if f.suffix in (".py", ".cpp", ".hip", ".h") and f.name != "build.py":
+            assert not pat.search(f.read_text()), f

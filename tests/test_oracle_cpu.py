@@ -1,0 +1,238 @@
+"""Pin the CPU oracle (oracle/) before trusting it as the GPU checker.
+
+* Known-answer vectors from the reference: stream_compaction/INSTRUCTION.md:262-302.
+* Independent restatements: numpy cumsum (scan), boolean masks (compaction, stable partition),
+  a pure-Python minstd_rand + utilhash (pathtrace.cu:57-62, intersections.h:13-22) checked against
+  the C++ standard's minstd_rand value (10000th output from seed 1 == 399268537), numpy sin/cos
+  and a float64 glm-order matrix composition (utilities.cpp:84-92).
+* Committed golden fixtures (tests/golden/*.npz, made by tests/golden/make_golden.py) freeze
+  the pinned behaviour, including small Cornell renders (radiance: parity unpinned against the
+  reference itself).
+"""
+from __future__ import annotations
+
+import math
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from oracle import binding as O
+
+GOLDEN = Path(__file__).resolve().parent / "golden"
+SCENES = Path(__file__).resolve().parent / "scenes"
+
+
+# ---- stream compaction ---------------------------------------------------------------------
+def test_reference_known_answers():
+    a = np.array([1, 5, 0, 1, 2, 0, 3], np.int32)
+    assert O.scan(a).tolist() == [0, 1, 6, 6, 7, 9, 9]
+    assert O.compact_without_scan(a).tolist() == [1, 5, 1, 2, 3]
+    assert O.compact_with_scan(a).tolist() == [1, 5, 1, 2, 3]
+    # map -> scan steps of compactWithScan (INSTRUCTION.md:283-295)
+    assert O.scan((a != 0).astype(np.int32)).tolist() == [0, 1, 2, 2, 3, 4, 4]
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 3, 255, 256, 257, (1 << 16) - 3, 1 << 16])
+def test_scan_matches_numpy(n):
+    rng = np.random.default_rng(n)
+    a = rng.integers(-2**31, 2**31 - 1, size=n, dtype=np.int64).astype(np.int32)
+    ref = np.zeros(n, np.int64)
+    if n:
+        ref[1:] = np.cumsum(a[:-1].astype(np.int64))
+    ref = ((ref + 2**31) % 2**32 - 2**31).astype(np.int32)     # int32 wrap-around
+    np.testing.assert_array_equal(O.scan(a), ref)
+
+
+@pytest.mark.parametrize("n", [0, 1, 7, 1000, 65536 + 5])
+def test_compaction_matches_masks(n):
+    rng = np.random.default_rng(n + 1)
+    a = rng.integers(0, 4, size=n, dtype=np.int32)
+    np.testing.assert_array_equal(O.compact_without_scan(a), a[a != 0])
+    np.testing.assert_array_equal(O.compact_with_scan(a), a[a != 0])
+    perm, live = O.partition_indices(a)
+    idx = np.arange(n, dtype=np.int32)
+    assert live == int((a != 0).sum())
+    # stable partition: kept indices in order, then dropped indices in order
+    np.testing.assert_array_equal(perm, np.concatenate([idx[a != 0], idx[a == 0]]))
+
+
+def test_scan_compact_golden():
+    g = np.load(GOLDEN / "scan_compact.npz")
+    for tag in ("pot", "npot", "small"):
+        np.testing.assert_array_equal(O.scan(g[f"{tag}_scan_in"]), g[f"{tag}_scan_out"])
+        np.testing.assert_array_equal(O.compact_without_scan(g[f"{tag}_compact_in"]), g[f"{tag}_compact_out"])
+        perm, live = O.partition_indices(g[f"{tag}_compact_in"])
+        np.testing.assert_array_equal(perm, g[f"{tag}_partition_perm"])
+        assert live == int(g[f"{tag}_partition_live"][0])
+        a = g[f"{tag}_scan_in"]
+        assert a[-1] == 0 and a.max() < 50           # main.cpp shape
+        assert len(a) in (1 << 12, (1 << 12) - 3, 7)
+
+
+# ---- RNG -----------------------------------------------------------------------------------
+M31 = 2147483647
+
+
+def utilhash(a: int) -> int:
+    m = 0xFFFFFFFF
+    a = ((a + 0x7ed55d16) + (a << 12)) & m
+    a = ((a ^ 0xc761c23c) ^ (a >> 19)) & m
+    a = ((a + 0x165667b1) + (a << 5)) & m
+    a = ((a + 0xd3a2646c) ^ (a << 9)) & m
+    a = ((a + 0xfd7046c5) + (a << 3)) & m
+    a = ((a ^ 0xb55a4f09) ^ (a >> 16)) & m
+    return a
+
+
+def py_u01(it: int, index: int, depth: int, count: int) -> np.ndarray:
+    h = utilhash((1 << 31) | (depth << 22) | it) ^ utilhash(index)
+    x = h % M31 or 1
+    out = []
+    for _ in range(count):
+        x = (48271 * x) % M31
+        out.append(np.float32(x - 1) * np.float32(2.0 ** -31))
+    return np.array(out, np.float32)
+
+
+def test_minstd_standard_check_value():
+    x = 1
+    for _ in range(10000):
+        x = (48271 * x) % M31
+    assert x == 399268537
+
+
+def test_rng_matches_python_restatement_and_golden():
+    g = np.load(GOLDEN / "rng.npz")
+    for (it, index, depth), ref in zip(g["keys"].tolist(), g["u01"]):
+        got = O.u01_sequence(it, index, depth, 16)
+        np.testing.assert_array_equal(got, py_u01(it, index, depth, 16))
+        np.testing.assert_array_equal(got, ref)
+        assert (got >= 0).all() and (got < 1).all()
+
+
+# ---- math ------------------------------------------------------------------------------------
+def test_sincos_accuracy_and_golden():
+    g = np.load(GOLDEN / "sincos.npz")
+    for x, s_ref, c_ref in zip(g["x"], g["sin"], g["cos"]):
+        s, c = O.sincos(float(x))
+        assert np.float32(s) == s_ref and np.float32(c) == c_ref
+        assert abs(s - math.sin(float(x))) <= 4e-7 * max(1.0, abs(float(x)) / 100)
+        assert abs(c - math.cos(float(x))) <= 4e-7 * max(1.0, abs(float(x)) / 100)
+    xs = np.linspace(-20, 20, 2001, dtype=np.float32)
+    err = max(max(abs(O.sincos(float(x))[0] - math.sin(float(x))), abs(O.sincos(float(x))[1] - math.cos(float(x))))
+              for x in xs)
+    assert err < 1e-6
+
+
+def _glm_trs(t, r, s) -> np.ndarray:
+    """float64 T * Rx * Ry * Rz * S (utilities.cpp:84-92), row-major."""
+    def rot(axis, deg):
+        c, sn = math.cos(math.radians(deg)), math.sin(math.radians(deg))
+        m = np.eye(4)
+        i, j = [(1, 2), (0, 2), (0, 1)][axis]
+        m[i, i], m[j, j] = c, c
+        if axis == 1:
+            m[i, j], m[j, i] = sn, -sn
+        else:
+            m[i, j], m[j, i] = -sn, sn
+        return m
+    T = np.eye(4); T[:3, 3] = t
+    S = np.diag([s[0], s[1], s[2], 1.0])
+    return T @ rot(0, r[0]) @ rot(1, r[1]) @ rot(2, r[2]) @ S
+
+
+def test_transforms_match_float64_and_golden():
+    g = np.load(GOLDEN / "transforms.npz")
+    for (t, r, s), T_ref, I_ref, IT_ref in zip(g["trs"], g["transform"], g["inverse"], g["inv_transpose"]):
+        T, Inv, InvT = O.build_transform(t, r, s)
+        np.testing.assert_array_equal(T, T_ref)
+        np.testing.assert_array_equal(Inv, I_ref)
+        np.testing.assert_array_equal(InvT, IT_ref)
+        M = _glm_trs(t.astype(np.float64), r.astype(np.float64), s.astype(np.float64))
+        # glm stores column-major: flat[c*4 + r] == M[r, c]
+        np.testing.assert_allclose(T.reshape(4, 4).T, M, rtol=1e-5, atol=1e-5)
+        np.testing.assert_allclose(Inv.reshape(4, 4).T, np.linalg.inv(M), rtol=1e-4, atol=1e-5)
+        np.testing.assert_allclose(InvT.reshape(4, 4).T, np.linalg.inv(M).T, rtol=1e-4, atol=1e-5)
+
+
+def test_camera_orbit_recompute():
+    """main.cpp:117-136 recomputes the camera from phi/theta on frame 1: for cornell.json the eye
+    y becomes 4.9999995 (float cos/sin round trip), view stays -z, right +x."""
+    cam = O.camera((800, 800), 45.0, (0.0, 5.0, 10.5), (0.0, 5.0, 0.0), (0.0, 1.0, 0.0))
+    assert tuple(cam.res) == (800, 800)
+    assert abs(cam.position[1] - 5.0) < 1e-6 and abs(cam.position[2] - 10.5) < 1e-5
+    assert abs(cam.view[2] + 1.0) < 1e-6 and abs(cam.right[0] - 1.0) < 1e-6
+    # FOV: the x fov derives from tan(fovy) (scene.cpp:197-201 quirk), pixel length from fov
+    fovy = math.radians(45.0)
+    yscaled = math.tan(fovy)
+    assert abs(cam.fov[1] - 45.0) < 1e-5
+    assert abs(cam.pixel_length[1] - 2 * yscaled / 800) < 1e-6
+
+
+# ---- renderer ---------------------------------------------------------------------------------
+def _small_scene():
+    sc = O.OracleScene.from_json(SCENES / "cornell.json")
+    sc.cam = O.camera((32, 32), 45.0, (0.0, 5.0, 10.5), (0.0, 5.0, 0.0), (0.0, 1.0, 0.0))
+    return sc
+
+
+CASES = {
+    "default": dict(),
+    "nossaa_nodof_sort": dict(ssaa=False, dof=False, sort_by_material=True),
+    "no_rr": dict(russian_roulette=False),
+}
+
+
+@pytest.mark.parametrize("name", list(CASES))
+def test_render_golden(name):
+    g = np.load(GOLDEN / "render_cornell32.npz")
+    sc = _small_scene()
+    fl = O.flags(**CASES[name])
+    img, live = O.render_pass(sc, fl, iter_first=1)
+    np.testing.assert_array_equal(img, g[f"{name}_image_1"])
+    assert live == g[f"{name}_live_1"].tolist()
+    img2, live2 = O.render_pass(sc, fl, iter_first=2, image=img.copy())
+    np.testing.assert_array_equal(img2, g[f"{name}_image_2"])
+    assert live2 == g[f"{name}_live_2"].tolist()
+    np.testing.assert_array_equal(O.tonemap(img2, 2.0), g[f"{name}_tonemap_2"])
+
+
+def test_render_invariants():
+    """Size-independent properties: non-negative finite radiance; the live-path count per bounce
+    never grows; bounce 0 traces every pixel; sorting by material changes the shading RNG key
+    (compacted index) but not the set of camera rays."""
+    sc = _small_scene()
+    img, live = O.render_pass(sc, O.flags(), iter_first=1)
+    assert np.isfinite(img).all() and (img >= 0).all()
+    assert live[0] == 32 * 32
+    assert all(b <= a for a, b in zip(live, live[1:]))
+    img_s, live_s = O.render_pass(sc, O.flags(sort_by_material=True), iter_first=1)
+    assert live_s[0] == live[0]
+    assert img.sum() > 0 and img_s.sum() > 0
+
+
+def test_render_shards_tile_the_image():
+    """Rank r of W owns rows y % W == r; shards are disjoint and cover the image,
+    and the camera ray of a pixel does not depend on the sharding (raygen key = global pixel)."""
+    sc = _small_scene()
+    fl = O.flags(russian_roulette=False)
+    # depth 1: only camera rays + first hit, which is shard-invariant
+    full, _ = O.render_pass(sc, fl, iter_first=3, depth=1)
+    world = 3
+    parts = [O.render_pass(sc, fl, iter_first=3, rank=r, world=world, depth=1)[0] for r in range(world)]
+    assert sum(p.shape[0] for p in parts) == 32
+    from cuda_pathtracer_amd.distributed import assemble
+    np.testing.assert_array_equal(assemble(parts, 32, world), full)
+
+
+def test_tonemap_rules():
+    """saveImage (main.cpp:88-112) + Image::savePNG (image.cpp:22-42): divide by samples, clamp to
+    [0,1], x255 truncate, mirror in x."""
+    img = np.zeros((2, 3, 3), np.float32)
+    img[0, 0] = [0.5, 1.0, 3.0]
+    img[1, 2] = [0.25, 0.0, 0.999]
+    out = O.tonemap(img, 1.0)
+    # pixel (x=0,y=0) lands at x = W-1 - 0
+    assert out[0, 2].tolist() == [127, 255, 255]
+    assert out[1, 0].tolist() == [63, 0, 254]
