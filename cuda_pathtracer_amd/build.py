@@ -16,6 +16,8 @@ ROOT = PKG.parent
 CSRC = PKG / "csrc"
 LIB = PKG / "libpt_amd.so"
 CLI = PKG / "pathtracer_amd"
+HOST = PKG / "host"
+HOST_LIB = PKG / "build" / "libpt_amd_host.a"
 ORACLE_DIR = ROOT / "oracle"
 ORACLE_LIB = ORACLE_DIR / "build" / "liboracle.so"
 
@@ -61,10 +63,24 @@ def build_native(verbose: bool = False, force: bool = False) -> Path:
         list(ex.map(lambda c: _run(c, verbose), jobs))
     if force or jobs or _stale(LIB, objs):
         _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(LIB), *map(str, objs), "-lz"], verbose)
-    cli_src = CSRC / "pt_cli.cpp"
-    if cli_src.exists() and (force or _stale(CLI, [cli_src, LIB] + headers)):
-        _run([HIPCC, *COMMON, "-I", str(ROOT / "include"), str(cli_src), "-o", str(CLI), "-L", str(PKG),
-              "-lpt_amd", f"-Wl,-rpath,$ORIGIN"], verbose)
+    # C++ host mirror of the reference interface (host/) and the headless CLI over it
+    host_srcs = [HOST / "pathtrace.cpp", HOST / "stream_compaction.cpp"]
+    host_hdrs = list(HOST.glob("*.h"))
+    host_objs = []
+    for s in host_srcs:
+        o = objdir / ("host_" + s.name + ".o")
+        host_objs.append(o)
+        if force or _stale(o, [s] + host_hdrs + headers):
+            _run([HIPCC, f"--offload-arch={ARCH}", *COMMON, "-I", str(ROOT / "include"), "-I", str(HOST), "-c", str(s),
+                  "-o", str(o)], verbose)
+    if force or _stale(HOST_LIB, host_objs):
+        if HOST_LIB.exists():
+            HOST_LIB.unlink()
+        _run(["ar", "rcs", str(HOST_LIB), *map(str, host_objs)], verbose)
+    cli_src = HOST / "main.cpp"
+    if force or _stale(CLI, [cli_src, LIB, HOST_LIB] + host_hdrs + headers):
+        _run([HIPCC, f"--offload-arch={ARCH}", *COMMON, "-I", str(ROOT / "include"), "-I", str(HOST), str(cli_src),
+              "-x", "none", str(HOST_LIB), "-o", str(CLI), "-L", str(PKG), "-lpt_amd", "-Wl,-rpath,$ORIGIN"], verbose)
     return LIB
 
 
@@ -78,9 +94,26 @@ def build_oracle(verbose: bool = False, force: bool = False) -> Path:
     return ORACLE_LIB
 
 
+def build_cpp_tests(verbose: bool = False, force: bool = False) -> list[Path]:
+    """C++ test programs (test infrastructure): the reference-shaped self-tests over the C++ host
+    mirror, checked against the oracle.  Run by tests/test_cpp_gpu.py on the GPU box."""
+    tdir = ROOT / "tests" / "cpp"
+    outs = []
+    for src in sorted(tdir.glob("test_*.cpp")):
+        exe = tdir / "build" / src.stem
+        exe.parent.mkdir(exist_ok=True)
+        outs.append(exe)
+        if force or _stale(exe, [src, LIB, HOST_LIB, ORACLE_LIB] + list(HOST.glob("*.h"))):
+            _run([HIPCC, f"--offload-arch={ARCH}", *COMMON, "-I", str(ROOT / "include"), "-I", str(HOST), str(src),
+                  "-x", "none", str(HOST_LIB), "-o", str(exe), "-L", str(PKG), "-lpt_amd", "-L", str(ORACLE_LIB.parent),
+                  "-loracle", "-Wl,-rpath,$ORIGIN/../../../cuda_pathtracer_amd:$ORIGIN/../../../oracle/build"], verbose)
+    return outs
+
+
 def build_all(verbose: bool = False, force: bool = False) -> None:
     build_native(verbose, force)
     build_oracle(verbose, force)
+    build_cpp_tests(verbose, force)
 
 
 if __name__ == "__main__":

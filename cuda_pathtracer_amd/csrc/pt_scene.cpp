@@ -474,7 +474,7 @@ int pt_scene_get_render(const pt_scene* s, int32_t* iterations, int32_t* depth, 
 }
 
 #define PT_COPY_OUT(field)                                                             \
-    if (!s || (!out && cap > 0)) return fail(PT_ERR_ARG, "null argument");             \
+    if (!s || (!out && cap > 0)) return -fail(PT_ERR_ARG, "null argument");            \
     const auto& S = *reinterpret_cast<const pt::Scene*>(s);                            \
     const int n = (int)S.field.size() < cap ? (int)S.field.size() : cap;               \
     for (int i = 0; i < n; ++i) out[i] = S.field[(size_t)i];                           \

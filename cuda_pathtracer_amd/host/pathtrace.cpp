@@ -1,0 +1,105 @@
+// pathtrace.h mirror over the pt_* C ABI (see pathtrace.h for the reference citations).
+#include "pathtrace.h"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+
+namespace {
+
+GuiDataContainer* g_gui = nullptr;
+Scene* g_scene = nullptr;
+pt_ctx* g_ctx = nullptr;
+
+// checkCUDAError (utilities / common.cu:3-15 pattern): print and exit.
+void check(int rc, const char* what) {
+    if (rc == PT_OK) return;
+    std::fprintf(stderr, "pathtracer error: %s: %s\n", what, pt_last_error());
+    std::exit(EXIT_FAILURE);
+}
+
+pt_flags flags_of(const GuiDataContainer* g) {
+    pt_flags f;
+    pt_flags_default(&f);
+    if (g) {
+        f.russian_roulette = g->russianRoulette;
+        f.use_bvh = g->useBVHtree;
+        f.use_bbox = g->useBBox;
+        f.sort_by_material = g->sortbyMaterial;
+        f.use_thrust_partition = g->useThrustPartition;
+        f.ssaa = g->SSAA;
+        f.dof = g->DoF;
+        f.aperture = g->aperture;
+        f.focal_dist = g->focal_len;
+    }
+    return f;
+}
+
+}  // namespace
+
+Scene::Scene(std::string filename) {
+    std::printf("Reading scene from %s ...\n", filename.c_str());
+    check(pt_scene_load_json(filename.c_str(), &h_), "loadFromJSON");
+    int32_t ng = 0, nm = 0, nt = 0, nn = 0, ntex = 0;
+    check(pt_scene_counts(h_, &ng, &nm, &nt, &nn, &ntex), "counts");
+    if (ntex > 0) {
+        // The reference decodes textures with stb_image; this C++ host has no image decoder, so
+        // textured scenes go through the Python host (PIL) or pt_scene_set_texture_pixels.
+        std::fprintf(stderr, "pathtracer error: %s uses %d texture file(s); decode them and call "
+                             "pt_scene_set_texture_pixels before pathtraceInit\n", filename.c_str(), ntex);
+    }
+    geoms.resize(ng);
+    materials.resize(nm);
+    triangles.resize(nt);
+    if (pt_scene_get_geoms(h_, geoms.data(), ng) != ng) check(PT_ERR_ARG, "geoms");
+    if (pt_scene_get_materials(h_, materials.data(), nm) != nm) check(PT_ERR_ARG, "materials");
+    if (pt_scene_get_triangles(h_, triangles.data(), nt) != nt) check(PT_ERR_ARG, "triangles");
+    check(pt_scene_get_camera(h_, &state.camera), "camera");
+    int32_t it = 0, depth = 0;
+    char name[1024];
+    check(pt_scene_get_render(h_, &it, &depth, name, sizeof name), "render state");
+    state.iterations = (unsigned)it;
+    state.traceDepth = depth;
+    state.imageName = name;
+    state.image.assign((size_t)state.camera.res[0] * state.camera.res[1], vec3f{0.f, 0.f, 0.f});
+}
+
+Scene::~Scene() {
+    if (g_scene == this) pathtraceFree();
+    pt_scene_free(h_);
+}
+
+void InitDataContainer(GuiDataContainer* guiData) {
+    g_gui = guiData;
+    if (g_ctx) {
+        const pt_flags f = flags_of(g_gui);
+        check(pt_set_flags(g_ctx, &f), "InitDataContainer");
+    }
+}
+
+void pathtraceInit(Scene* scene) {
+    pathtraceFree();
+    g_scene = scene;
+    const pt_flags f = flags_of(g_gui);
+    check(pt_create(scene->handle(), &f, nullptr, &g_ctx), "pathtraceInit");
+    std::fill(scene->state.image.begin(), scene->state.image.end(), vec3f{0.f, 0.f, 0.f});
+}
+
+void pathtraceFree() {
+    if (g_ctx) check(pt_destroy(g_ctx), "pathtraceFree");
+    g_ctx = nullptr;
+}
+
+void pathtrace(uchar4* pbo, int frame, int iteration) {
+    (void)frame;
+    if (!g_ctx || !g_scene) {
+        std::fprintf(stderr, "pathtracer error: pathtrace() before pathtraceInit()\n");
+        std::exit(EXIT_FAILURE);
+    }
+    const pt_flags f = flags_of(g_gui);   // the reference re-reads the GUI flags every call
+    check(pt_set_flags(g_ctx, &f), "flags");
+    check(pt_render_pass(g_ctx, iteration, nullptr), "pathtrace");
+    if (pbo) check(pt_preview_rgba(g_ctx, iteration, reinterpret_cast<uint8_t*>(pbo), nullptr), "sendImageToPBO");
+    if (g_gui) g_gui->TracedDepth = g_scene->state.traceDepth;
+    check(pt_get_image(g_ctx, reinterpret_cast<float*>(g_scene->state.image.data())), "image copy");
+}

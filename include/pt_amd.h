@@ -162,6 +162,7 @@ int pt_scene_counts(const pt_scene* s, int32_t* ngeoms, int32_t* nmats, int32_t*
                     int32_t* nnodes, int32_t* ntex);
 int pt_scene_get_camera(const pt_scene* s, pt_camera* out);
 int pt_scene_get_render(const pt_scene* s, int32_t* iterations, int32_t* depth, char* file, int32_t cap);
+/* Getters copy min(count, cap) records and return that number (>= 0), or -PT_ERR_ARG. */
 int pt_scene_get_geoms(const pt_scene* s, pt_geom* out, int32_t cap);
 int pt_scene_get_materials(const pt_scene* s, pt_material* out, int32_t cap);
 int pt_scene_get_triangles(const pt_scene* s, pt_triangle* out, int32_t cap);
@@ -186,9 +187,9 @@ int pt_stats(pt_ctx* c, pt_stats_t* out);                   /* synchronises the 
 /* Per-kernel device timing with hipEvents recorded on the launch stream (for the roofline).  When
  * enabled, pt_render_pass brackets every launch with pooled events; pt_profile_read synchronises
  * and returns, per kernel kind, the summed milliseconds and launch counts since the last read. */
-#define PT_KIND_FIRST_BOUNCE 0   /* k_trace<FIRST>: raygen + intersect + shade (bounce 0)      */
-#define PT_KIND_BOUNCE 1         /* k_trace: intersect + shade (bounces >= 1)                  */
-#define PT_KIND_COMPACT 2        /* k_compact_paths: stable compaction of the survivors        */
+#define PT_KIND_FIRST_BOUNCE 0   /* bounce 0: k_bounce<FIRST> (fused) or k_trace<FIRST> (split)  */
+#define PT_KIND_BOUNCE 1         /* bounces >= 1: k_bounce (fused) or k_trace (split)          */
+#define PT_KIND_COMPACT 2        /* split pipeline only: k_compact_paths                        */
 #define PT_KIND_SORT 3           /* material-sorted mode: raygen/isect/scan/scatter/shade      */
 int pt_profile_enable(pt_ctx* c, int32_t on);
 int pt_profile_read(pt_ctx* c, double ms[4], uint64_t launches[4]);

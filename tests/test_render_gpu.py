@@ -152,3 +152,50 @@ def test_cornell_full_resolution(cornell_path):
     assert (np.abs(tg - tr) <= 2).mean() >= 0.99
     lum = lambda x: (x * np.array([0.2126, 0.7152, 0.0722], np.float32)).sum()  # noqa: E731
     assert abs(lum(g) - lum(r)) <= 0.005 * lum(r)
+
+
+def test_cornell_256spp_tolerance(cornell_path):
+    """§8a's stated radiance tolerance at >= 256 spp (16 passes of 16 batched samples, 128x128):
+    per-pixel |d| <= 2/255 on the tone-mapped image for >= 99% of pixels and mean relative
+    luminance within 0.5% — here the result is also bit-exact."""
+    s, o = _pair(cornell_path, (128, 128))
+    g, r, st, live = _run(s, o, _gui(), iters=256, spp=16)
+    _assert_bitexact(g, r, "cornell 128x128 256spp")
+    tg, tr = _tonemap_pair(g, r, 256)
+    assert (np.abs(tg - tr) <= 2).mean() >= 0.99
+    assert abs(_lum(g) - _lum(r)) <= 0.005 * _lum(r)
+
+
+def _tonemap_pair(g, r, samples):
+    from cuda_pathtracer_amd import tonemap
+    return tonemap(g, samples).astype(int), O.tonemap(r, samples).astype(int)
+
+
+def _lum(x):
+    return float((np.asarray(x, np.float64) * np.array([0.2126, 0.7152, 0.0722])).sum())
+
+
+@pytest.mark.slow
+def test_statistical_match_with_reference_course_render(cornell_path):
+    """Loose check against the reference's only image, path_tracer/img/REFERENCE_cornell.5000samp.png
+    (a course render from an unknown build, so parity stays UNPINNED; this only
+    catches gross model errors).  5000 samples of cornell.json 800x800, tone-mapped, compared as
+    16x16 block means with the committed fixture."""
+    from cuda_pathtracer_amd import PathTracer, Scene, tonemap
+    from pathlib import Path
+    ref = np.load(Path(__file__).parent / "golden" / "reference_cornell_5000samp_16x16means.npz")["block_means"]
+    s = Scene(cornell_path)
+    pt = PathTracer(s, _gui(), spp=50)
+    for it in range(1, 5001, 50):
+        pt.render_pass(it)
+    img = pt.image()
+    pt.free()
+    # the reference writes the PNG through the same x-mirror as tonemap()
+    t = tonemap(img, 5000).astype(np.float32)
+    ours = t.reshape(50, 16, 50, 16, 3).mean(axis=(1, 3))
+    mean_ref, mean_ours = ref.mean(axis=(0, 1)), ours.mean(axis=(0, 1))
+    rel = np.abs(mean_ours - mean_ref) / mean_ref
+    block_mad = float(np.abs(ours - ref).mean())
+    print(f"channel means ours={mean_ours} ref={mean_ref} rel={rel} block MAD={block_mad:.2f}/255")
+    assert (rel < 0.10).all(), (mean_ours, mean_ref)
+    assert block_mad < 12.0
