@@ -68,6 +68,7 @@ struct CamDev {
 struct FlagsDev {
     int32_t rr, bvh, bbox, ssaa, dof;
     float aperture, focal;
+    int32_t single_albedo;
 };
 struct TileDev {
     int32_t W, rank, world, npix, spp, P, depth, iter_first;
@@ -416,7 +417,7 @@ __device__ __forceinline__ bool shade(const SceneDev& S, const FlagsDev& fl, int
     } else {
         p.d = hemisphere(n, rng);
     }
-    p.c = hadamard(p.c, mcol);
+    if (!fl.single_albedo) p.c = hadamard(p.c, mcol);   // interactions.cu:83 (second albedo)
     p.bounces += 1;
     remaining -= 1;
     if (remaining == 0) { p.c = F3(0, 0, 0); return false; }
@@ -936,6 +937,7 @@ void set_flags_dev(pt_ctx* c, const pt_flags& f) {
     c->args.fl.dof = f.dof;
     c->args.fl.aperture = f.aperture;
     c->args.fl.focal = f.focal_dist;
+    c->args.fl.single_albedo = f.single_albedo;
 }
 
 Affine to_affine(const float* m) {   // glm column-major 4x4 -> 3x4 + the exact w=0 terms

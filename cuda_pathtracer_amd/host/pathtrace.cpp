@@ -31,6 +31,7 @@ pt_flags flags_of(const GuiDataContainer* g) {
         f.dof = g->DoF;
         f.aperture = g->aperture;
         f.focal_dist = g->focal_len;
+        f.single_albedo = g->singleAlbedo;
     }
     return f;
 }

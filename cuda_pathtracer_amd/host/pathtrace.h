@@ -30,6 +30,7 @@ public:
     bool DoF{true};
     float aperture{0.1f};
     float focal_len{10.0f};
+    bool singleAlbedo{false};   // extension (include/pt_amd.h pt_flags.single_albedo)
 };
 
 struct vec3f {

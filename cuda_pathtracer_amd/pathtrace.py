@@ -39,6 +39,8 @@ class GuiDataContainer:
         self.DoF = True
         self.aperture = 0.1
         self.focal_len = 10.0
+        # extension, off = the reference: albedo applied once instead of twice (include/pt_amd.h)
+        self.singleAlbedo = False
 
     def to_c(self) -> N.Flags:
         f = N.Flags()
@@ -51,6 +53,7 @@ class GuiDataContainer:
         f.dof = int(bool(self.DoF))
         f.aperture = float(self.aperture)
         f.focal_dist = float(self.focal_len)
+        f.single_albedo = int(bool(self.singleAlbedo))
         return f
 
 

@@ -55,6 +55,10 @@ typedef struct pt_flags {
     int32_t dof;                  /* default 1 */
     float aperture;               /* default 0.1 */
     float focal_dist;             /* default 10 */
+    /* Extension (default 0 = the reference): apply the surface albedo once.  The reference
+     * multiplies the path colour by the albedo at interactions.cu:60 AND :83; its own course
+     * image (img/REFERENCE_cornell.5000samp.png) matches the single-albedo model. */
+    int32_t single_albedo;
 } pt_flags;
 
 /* Material (sceneStructs.h:43-57), 48 bytes. */

@@ -59,6 +59,7 @@ struct OCamera {               // sceneStructs.h:59-69
 struct OFlags {                // utilities.h:17-34 (GuiDataContainer) / pathtrace.cu:31-42 (Settings)
     int32_t russian_roulette, use_bvh, use_bbox, sort_by_material, use_thrust_partition, ssaa, dof;
     float aperture, focal_dist;
+    int32_t single_albedo;     // extension (pt_amd.h); 0 = the reference
 };
 struct OTriangle {             // sceneStructs.h:103-161 (124 bytes)
     int32_t id;
@@ -543,7 +544,7 @@ inline V3 refract3(V3 I, V3 N, float eta) {
 }
 
 // scatterRay (interactions.cu:43-85)
-void scatter(const Scene& sc, Path& p, V3 hit_point, Isect& is, const OMaterial& m, Rng& rng) {
+void scatter(const Scene& sc, Path& p, V3 hit_point, Isect& is, const OMaterial& m, Rng& rng, bool fl_single_albedo) {
     V3 nrm = is.n;
     p.o = add(hit_point, smul(0.0001f, nrm));
     V3 alb = m.texture_id != -1 ? tex_color(sc.texs[m.texture_id], is.uv) : ld3(m.color);
@@ -568,7 +569,7 @@ void scatter(const Scene& sc, Path& p, V3 hit_point, Isect& is, const OMaterial&
     } else {
         p.d = hemisphere(nrm, rng);
     }
-    p.c = mulv(p.c, ld3(m.color));
+    if (!fl_single_albedo) p.c = mulv(p.c, ld3(m.color));   // interactions.cu:83
 }
 
 // shadeMaterials (pathtrace.cu:300-344) for the path at array position idx.
@@ -581,7 +582,7 @@ void shade(const Scene& sc, const OFlags& fl, Path& p, Isect& is, int idx) {
         p.remaining = 0;
         return;
     }
-    scatter(sc, p, point_on_ray(p.o, p.d, is.t), is, m, rng);
+    scatter(sc, p, point_on_ray(p.o, p.d, is.t), is, m, rng, fl.single_albedo != 0);
     p.bounces += 1;
     if (--p.remaining == 0) { p.c = mk(0, 0, 0); return; }
     if (fl.russian_roulette && p.bounces > 3) {

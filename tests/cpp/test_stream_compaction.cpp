@@ -6,6 +6,10 @@
 // mismatch.  Inputs are seeded (the reference uses time()).
 //
 //   test_stream_compaction [SIZE_LOG2=20]
+#include <execinfo.h>
+#include <unistd.h>
+
+#include <csignal>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -54,7 +58,18 @@ void printElapsedTime(float ms, const char* note) { std::printf("   elapsed time
 
 }  // namespace
 
+void on_fault(int sig) {   // print where a crash happened (stdout is unbuffered below)
+    void* frames[64];
+    const int n = backtrace(frames, 64);
+    std::fprintf(stderr, "signal %d, backtrace:\n", sig);
+    backtrace_symbols_fd(frames, n, 2);
+    _exit(128 + sig);
+}
+
 int main(int argc, char** argv) {
+    std::setvbuf(stdout, nullptr, _IONBF, 0);
+    std::signal(SIGSEGV, on_fault);
+    std::signal(SIGABRT, on_fault);
     const int lg = argc > 1 ? std::atoi(argv[1]) : 20;
     const int SIZE = 1 << lg;
     const int NPOT = SIZE - 3;
@@ -84,6 +99,7 @@ int main(int argc, char** argv) {
 
     // small sizes the reference's padded scan could not do
     for (int n : {1, 2, 3, 7, 64, 65, 8191, 8193}) {
+        if (n > SIZE) continue;
         oracle_scan(n, b, a);
         zeroArray(n, c);
         Efficient::scan(n, c, a);

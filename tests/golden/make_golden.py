@@ -117,9 +117,6 @@ def main() -> None:
 if __name__ == "__main__":
     main()
 
-# reference_cornell_5000samp_16x16means.npz was made once, in the survey container, from the
-# reference's course render path_tracer/img/REFERENCE_cornell.5000samp.png (a data file, 800x800
-# RGB8): float32 means over 16x16 pixel blocks -> (50, 50, 3).  /root/reference is absent on the
-# GPU box, so the statistical comparison in tests/test_render_gpu.py reads this fixture:
-#   a = np.asarray(PIL.Image.open(png).convert("RGB")).astype(np.float32)
-#   block_means = a.reshape(50, 16, 50, 16, 3).mean(axis=(1, 3))
+# REFERENCE_cornell.5000samp.png is the reference's course render (path_tracer/img/), copied
+# verbatim as expected-output DATA for tests/test_render_gpu.py (the GPU box has no
+# /root/reference); it is not generated here.

@@ -33,7 +33,7 @@ def _gui(**kw):
 
 def _oflags(g):
     return O.flags(g.russianRoulette, g.useBVHtree, g.useBBox, g.sortbyMaterial, g.useThrustPartition, g.SSAA,
-                   g.DoF, g.aperture, g.focal_len)
+                   g.DoF, g.aperture, g.focal_len, g.singleAlbedo)
 
 
 def _assert_bitexact(gpu, ref, what):
@@ -81,6 +81,8 @@ def test_cornell_bitexact_default_flags(cornell_path):
     dict(sortbyMaterial=True, russianRoulette=False),
     dict(useThrustPartition=True),
     dict(aperture=0.5, focal_len=7.0),
+    dict(singleAlbedo=True),
+    dict(singleAlbedo=True, sortbyMaterial=True),
 ])
 def test_cornell_bitexact_flags(cornell_path, kw):
     s, o = _pair(cornell_path, (48, 40))
@@ -175,27 +177,46 @@ def _lum(x):
     return float((np.asarray(x, np.float64) * np.array([0.2126, 0.7152, 0.0722])).sum())
 
 
-@pytest.mark.slow
-def test_statistical_match_with_reference_course_render(cornell_path):
-    """Loose check against the reference's only image, path_tracer/img/REFERENCE_cornell.5000samp.png
-    (a course render from an unknown build, so parity stays UNPINNED; this only
-    catches gross model errors).  5000 samples of cornell.json 800x800, tone-mapped, compared as
-    16x16 block means with the committed fixture."""
+def _course_render(cornell_path, single_albedo: bool):
     from cuda_pathtracer_amd import PathTracer, Scene, tonemap
-    from pathlib import Path
-    ref = np.load(Path(__file__).parent / "golden" / "reference_cornell_5000samp_16x16means.npz")["block_means"]
     s = Scene(cornell_path)
-    pt = PathTracer(s, _gui(), spp=50)
+    pt = PathTracer(s, _gui(singleAlbedo=single_albedo), spp=50)
     for it in range(1, 5001, 50):
         pt.render_pass(it)
     img = pt.image()
     pt.free()
-    # the reference writes the PNG through the same x-mirror as tonemap()
-    t = tonemap(img, 5000).astype(np.float32)
-    ours = t.reshape(50, 16, 50, 16, 3).mean(axis=(1, 3))
-    mean_ref, mean_ours = ref.mean(axis=(0, 1)), ours.mean(axis=(0, 1))
-    rel = np.abs(mean_ours - mean_ref) / mean_ref
-    block_mad = float(np.abs(ours - ref).mean())
-    print(f"channel means ours={mean_ours} ref={mean_ref} rel={rel} block MAD={block_mad:.2f}/255")
-    assert (rel < 0.10).all(), (mean_ours, mean_ref)
-    assert block_mad < 12.0
+    return tonemap(img, 5000).astype(np.int32)          # same x-mirror as the reference's PNG
+
+
+@pytest.mark.slow
+def test_statistical_match_with_reference_course_render(cornell_path):
+    """The reference's only radiance artefact, path_tracer/img/REFERENCE_cornell.5000samp.png
+    (800x800, 5000 samples; committed as a fixture under tests/golden/), against our render of
+    cornell.json at 5000 samples.
+
+    The reference CODE multiplies the path colour by the albedo twice (interactions.cu:60 and :83);
+    its IMAGE matches the single-albedo model, which therefore pins camera, geometry, sampling,
+    Russian roulette and tone mapping against the reference's own output.  The sample streams
+    differ (the image came from an unknown build), so the match is statistical, not per pixel:
+    §8a's mean relative luminance error <= 0.5%, every channel mean within 0.5%, 16x16 block means
+    within 1/255 on average, per-pixel mean |d| < 3.5/255 (Monte Carlo noise at 5000 spp).  The
+    reference-exact (double-albedo) model is ~25% darker, as that quirk predicts."""
+    from pathlib import Path
+    from PIL import Image
+    ref = np.asarray(Image.open(Path(__file__).parent / "golden" / "REFERENCE_cornell.5000samp.png").convert("RGB"))
+    ref = ref.astype(np.int32)
+    ours1 = _course_render(cornell_path, True)
+    d = np.abs(ours1 - ref)
+    lum = lambda x: float((x * np.array([0.2126, 0.7152, 0.0722])).sum())  # noqa: E731
+    rel_lum = abs(lum(ours1) - lum(ref)) / lum(ref)
+    rel_ch = np.abs(ours1.mean(axis=(0, 1)) - ref.mean(axis=(0, 1))) / ref.mean(axis=(0, 1))
+    blocks = lambda x: x.reshape(50, 16, 50, 16, 3).mean(axis=(1, 3))  # noqa: E731
+    block_mad = float(np.abs(blocks(ours1) - blocks(ref)).mean())
+    ours2 = _course_render(cornell_path, False)
+    ratio2 = ours2.mean(axis=(0, 1)) / ref.mean(axis=(0, 1))
+    print(f"course image: single-albedo rel_lum={rel_lum:.5f} rel_ch={rel_ch} block MAD={block_mad:.3f} "
+          f"pixel mean|d|={float(d.mean()):.3f} <=2/255={float((d.max(axis=2) <= 2).mean()):.4f}; "
+          f"reference-exact/course channel ratio {ratio2}")
+    assert rel_lum <= 0.005 and (rel_ch <= 0.005).all()
+    assert block_mad <= 1.0 and float(d.mean()) < 3.5
+    assert ((ratio2 < 0.85) & (ratio2 > 0.6)).all()
