@@ -11,7 +11,7 @@ import sys
 from pathlib import Path
 
 _PKG = Path(__file__).resolve().parent
-LIB_PATH = _PKG / "libpt_amd.so"
+LIB_PATH = Path(os.environ["PT_AMD_LIB"]) if os.environ.get("PT_AMD_LIB") else _PKG / "libpt_amd.so"
 
 
 class NativeLibraryError(RuntimeError):

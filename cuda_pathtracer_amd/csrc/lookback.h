@@ -51,20 +51,34 @@ __device__ __forceinline__ uint64_t poll(const uint64_t* st, int j) {
     return j >= 0 ? __hip_atomic_load(st + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kFlagPre;
 }
 
+// First-round polls of a look-back, issued early so their latency overlaps other work.
+template <int WINDOWS>
+__device__ __forceinline__ void prepoll(const uint64_t* st, int tile, int lane, uint64_t (&w)[WINDOWS]) {
+#pragma unroll
+    for (int k = 0; k < WINDOWS; ++k) w[k] = poll(st, tile - 1 - 64 * k - lane);
+}
+
 // Called by one full wave (all 64 lanes).  Returns the exclusive prefix of `tile` (> 0).
 // Window w of a round covers predecessors base - 64w - lane; windows are consumed in order.
-__device__ __forceinline__ uint32_t lookback(uint64_t* st, int tile, int lane, uint32_t* err) {
+// WINDOWS x 64 predecessors are polled per round trip; `w` holds the first round's polls
+// (from prepoll, or issued here when PREPOLLED is false).
+template <int WINDOWS, bool PREPOLLED>
+__device__ __forceinline__ uint32_t lookback_impl(uint64_t* st, int tile, int lane, uint32_t* err,
+                                                  uint64_t (&w)[WINDOWS]) {
     uint32_t excl = 0;
     int base = tile - 1;
     uint32_t spins = 0;
+    bool polled = PREPOLLED;
     for (;;) {
-        uint64_t w[kWindows];
+        if (!polled) {
 #pragma unroll
-        for (int k = 0; k < kWindows; ++k) w[k] = poll(st, base - 64 * k - lane);
+            for (int k = 0; k < WINDOWS; ++k) w[k] = poll(st, base - 64 * k - lane);
+        }
+        polled = false;
         int consumed = 0;   // windows fully summed this round
         bool stalled = false;
 #pragma unroll
-        for (int k = 0; k < kWindows; ++k) {
+        for (int k = 0; k < WINDOWS; ++k) {
             if (stalled) break;
             const uint64_t nr = __ballot((w[k] >> 62) == 0);
             const uint64_t pre = __ballot((w[k] >> 62) == 2);
@@ -87,6 +101,12 @@ __device__ __forceinline__ uint32_t lookback(uint64_t* st, int tile, int lane, u
             __builtin_amdgcn_s_sleep(1);
         }
     }
+}
+
+template <int WINDOWS = kWindows>
+__device__ __forceinline__ uint32_t lookback(uint64_t* st, int tile, int lane, uint32_t* err) {
+    uint64_t w[WINDOWS];
+    return lookback_impl<WINDOWS, false>(st, tile, lane, err, w);
 }
 
 }  // namespace lb

@@ -9,13 +9,19 @@
 //   of the per-thread sums, 16 wave totals through LDS, then a decoupled look-back across tiles
 //   (lookback.h).  Algorithmic traffic: 8 B/element for scan (4 read + 4 write), 4 B/element +
 //   4 B/kept for compaction.
+//
+// Kernels: k_scan_lag (16-byte aligned pointers; the look-back of each tile is resolved one
+// iteration late, see below) and k_scan_tiles (unaligned pointers and the partial tail tile;
+// look-back resolved immediately).  Design history with measurements: DESIGN.md §4,
+// profiles/r01_scan_ab.txt.
 #include <hip/hip_runtime.h>
+
 #include <algorithm>
+#include <cstdlib>
+#include <cstring>
 #include <mutex>
 #include <string>
 #include <vector>
-#include <cstdlib>
-#include <cstring>
 
 #include "lookback.h"
 #include "../../include/sc_amd.h"
@@ -25,8 +31,8 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kChunks = 8;                       // int4 chunks per thread
 constexpr int kTile = kThreads * kChunks * 4;    // 8192 elements (32 KiB)
-constexpr size_t kCtlBytes = 256;
-constexpr int64_t kMallMinElems = (int64_t)1 << 26;   // >= 256 MiB of int32 input                // [0] unused, [1] device error word (padded)
+constexpr size_t kCtlBytes = 256;                // [0] unused, [1] device error word (padded)
+constexpr int kLagWindows = 4;                   // look-back predecessors per round trip: 4 x 64
 
 thread_local std::string g_err;
 thread_local float g_timer_ms = 0.f;
@@ -67,32 +73,31 @@ __device__ __forceinline__ void load_guarded(const int32_t* __restrict__ in, int
     }
 }
 
-// Everything after the loads: local + wave scans, block offsets, decoupled look-back, outputs.
-template <int MODE, bool VEC_STORE>
-__device__ __forceinline__ void process_tile(const v4i (&cur)[kChunks], int tile, int num_tiles, int64_t n,
-                                             int32_t* __restrict__ out, uint64_t* __restrict__ status,
-                                             uint32_t* __restrict__ ctl, int64_t* __restrict__ d_count,
-                                             int32_t* __restrict__ dead, uint32_t (&s_wsum)[kChunks][4],
-                                             uint32_t* s_excl) {
+template <int MODE>
+__device__ __forceinline__ uint32_t chunk_count(const v4i& v) {
+    if (MODE == kScan) return ((uint32_t)v[0] + (uint32_t)v[1]) + ((uint32_t)v[2] + (uint32_t)v[3]);
+    return (uint32_t)(v[0] != 0) + (uint32_t)(v[1] != 0) + (uint32_t)(v[2] != 0) + (uint32_t)(v[3] != 0);
+}
+
+// Block-local part shared by both kernels: per-chunk sums, wave scans, the 4 wave totals of every
+// chunk through LDS.  On return pre[k] = this thread's exclusive local offset for chunk k and the
+// tile aggregate is returned.  Starts with a barrier (the previous readers of s_wsum are done).
+template <int MODE>
+__device__ __forceinline__ uint32_t tile_offsets(const v4i (&cur)[kChunks], uint32_t (&s_wsum)[kChunks][4],
+                                                 uint32_t (&pre)[kChunks]) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int64_t base = (int64_t)tile * kTile;
-    uint32_t s[kChunks], incl[kChunks];
+    uint32_t sv[kChunks], incl[kChunks];
 #pragma unroll
     for (int k = 0; k < kChunks; ++k) {
-        if (MODE == kScan)
-            s[k] = ((uint32_t)cur[k][0] + (uint32_t)cur[k][1]) + ((uint32_t)cur[k][2] + (uint32_t)cur[k][3]);
-        else
-            s[k] = (uint32_t)(cur[k][0] != 0) + (uint32_t)(cur[k][1] != 0) + (uint32_t)(cur[k][2] != 0) +
-                   (uint32_t)(cur[k][3] != 0);
-        incl[k] = lb::wave_inclusive_scan(s[k]);
+        sv[k] = chunk_count<MODE>(cur[k]);
+        incl[k] = lb::wave_inclusive_scan(sv[k]);
     }
-    lds_barrier();   // previous tile's readers of s_wsum / s_excl are done
+    lds_barrier();
     if (lane == 63) {
 #pragma unroll
         for (int k = 0; k < kChunks; ++k) s_wsum[k][wave] = incl[k];
     }
     lds_barrier();
-    uint32_t off[kChunks];
     uint32_t run = 0;
 #pragma unroll
     for (int k = 0; k < kChunks; ++k) {
@@ -102,11 +107,55 @@ __device__ __forceinline__ void process_tile(const v4i (&cur)[kChunks], int tile
             const uint32_t x = s_wsum[k][w];
             before += (w < wave) ? x : 0u;
         }
-        off[k] = run + before;
+        pre[k] = run + before + (incl[k] - sv[k]);
 #pragma unroll
         for (int w = 0; w < 4; ++w) run += s_wsum[k][w];
     }
-    const uint32_t total = run;
+    return run;
+}
+
+// Outputs of chunk k of a tile whose prefix is known: scan values, kept values, or partition
+// indices (live in order; dead ones to `dead` in order, appended by k_append_dead).
+template <int MODE, bool FULL>
+__device__ __forceinline__ void write_chunk(const v4i& v, int64_t e0, uint32_t run, int64_t n,
+                                            int32_t* __restrict__ out, int32_t* __restrict__ dead) {
+    if (MODE == kScan) {
+        v4i o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { o[e] = (int32_t)run; run += (uint32_t)v[e]; }
+        if (FULL) {
+            __builtin_nontemporal_store(o, reinterpret_cast<v4i*>(out + e0));
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if (e0 + e < n) out[e0 + e] = o[e];
+        }
+    } else if (MODE == kCompact) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            if (v[e] != 0) out[run++] = v[e];
+    } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int64_t idx = e0 + e;
+            if (FULL || idx < n) {
+                if (v[e] != 0) out[run++] = (int32_t)idx;
+                else dead[idx - (int64_t)run] = (int32_t)idx;
+            }
+        }
+    }
+}
+
+// One tile with the look-back resolved immediately (unaligned inputs, the partial tail tile).
+template <int MODE>
+__device__ __forceinline__ void process_tile(const v4i (&cur)[kChunks], int tile, int num_tiles, int64_t n,
+                                             int32_t* __restrict__ out, uint64_t* __restrict__ status,
+                                             uint32_t* __restrict__ ctl, int64_t* __restrict__ d_count,
+                                             int32_t* __restrict__ dead, uint32_t (&s_wsum)[kChunks][4],
+                                             uint32_t* s_excl) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    uint32_t pre[kChunks];
+    const uint32_t total = tile_offsets<MODE>(cur, s_wsum, pre);
     if (wave == 0) {
         uint32_t excl = 0;
         if (tile == 0) {
@@ -120,243 +169,156 @@ __device__ __forceinline__ void process_tile(const v4i (&cur)[kChunks], int tile
     }
     lds_barrier();
     const uint32_t excl = *s_excl;
+    const int64_t base = (int64_t)tile * kTile;
 #pragma unroll
-    for (int k = 0; k < kChunks; ++k) {
-        const int64_t e0 = base + (int64_t)k * (kThreads * 4) + 4 * tid;
-        uint32_t run_k = excl + off[k] + (incl[k] - s[k]);
-        if (MODE == kScan) {
-            v4i o;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) { o[e] = (int32_t)run_k; run_k += (uint32_t)cur[k][e]; }
-            if (VEC_STORE) {
-                __builtin_nontemporal_store(o, reinterpret_cast<v4i*>(out + e0));
-            } else {
-#pragma unroll
-                for (int e = 0; e < 4; ++e)
-                    if (e0 + e < n) out[e0 + e] = o[e];
-            }
-        } else if (MODE == kCompact) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-                if (cur[k][e] != 0) out[run_k++] = cur[k][e];
-        } else {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int64_t idx = e0 + e;
-                if (idx < n) {
-                    if (cur[k][e] != 0) out[run_k++] = (int32_t)idx;
-                    else dead[idx - (int64_t)run_k] = (int32_t)idx;
-                }
-            }
-        }
-    }
+    for (int k = 0; k < kChunks; ++k)
+        write_chunk<MODE, false>(cur[k], base + (int64_t)k * (kThreads * 4) + 4 * tid, excl + pre[k], n, out, dead);
     if (MODE != kScan && tid == 0 && tile == num_tiles - 1) *d_count = (int64_t)(excl + total);
 }
 
-// Persistent, statically assigned tiles (lookback.h), software-pipelined: the next full tile's
-// loads are issued before this tile's look-back so HBM stays busy while the prefix propagates.
-// The (single) partial tail tile is processed after the loop with guarded scalar loads.
-template <int MODE, bool ALIGNED>
-__global__ __launch_bounds__(kThreads) void k_scan_tiles(const int32_t* __restrict__ in,
-                                                         int32_t* __restrict__ out, int64_t n,
-                                                         uint64_t* __restrict__ status,
-                                                         uint32_t* __restrict__ ctl,
-                                                         int64_t* __restrict__ d_count,
+// Unaligned pointers: persistent static tiles with guarded scalar loads.
+template <int MODE>
+__global__ __launch_bounds__(kThreads) void k_scan_tiles(const int32_t* __restrict__ in, int32_t* __restrict__ out,
+                                                         int64_t n, uint64_t* __restrict__ status,
+                                                         uint32_t* __restrict__ ctl, int64_t* __restrict__ d_count,
                                                          int32_t* __restrict__ dead) {
     __shared__ uint32_t s_wsum[kChunks][4];
     __shared__ uint32_t s_excl;
-    const int tid = threadIdx.x;
     const int num_tiles = (int)((n + kTile - 1) / kTile);
-    const int num_full = ALIGNED ? (int)(n / kTile) : 0;
-    int tile = blockIdx.x;
-    const int G = (int)gridDim.x;
-    if (tile < num_full) {
-        // Unrolled by two with named buffers (no loop-carried register copy, so the compiler's
-        // wait counts keep the prefetched tile in flight across process_tile).
-        v4i bufA[kChunks], bufB[kChunks];
-        load_full(in, (int64_t)tile * kTile, tid, bufA);
-        for (;;) {
-            // unconditional (clamped) prefetch: a branch here would make the wait-count pass merge
-            // "issued"/"skipped" states and drain the prefetch at the first use of bufA
-            const int t1 = tile + G;
-            load_full(in, (int64_t)(t1 < num_full ? t1 : tile) * kTile, tid, bufB);
-            process_tile<MODE, true>(bufA, tile, num_tiles, n, out, status, ctl, d_count, dead, s_wsum, &s_excl);
-            tile = t1;
-            if (tile >= num_full) break;
-            const int t2 = tile + G;
-            load_full(in, (int64_t)(t2 < num_full ? t2 : tile) * kTile, tid, bufA);
-            process_tile<MODE, true>(bufB, tile, num_tiles, n, out, status, ctl, d_count, dead, s_wsum, &s_excl);
-            tile = t2;
-            if (tile >= num_full) break;
-        }
-    }
-    for (; tile < num_tiles; tile += gridDim.x) {   // tail (and everything when unaligned)
+    for (int tile = blockIdx.x; tile < num_tiles; tile += gridDim.x) {
         v4i cur[kChunks];
-        load_guarded(in, n, (int64_t)tile * kTile, tid, cur);
-        process_tile<MODE, false>(cur, tile, num_tiles, n, out, status, ctl, d_count, dead, s_wsum, &s_excl);
+        load_guarded(in, n, (int64_t)tile * kTile, threadIdx.x, cur);
+        process_tile<MODE>(cur, tile, num_tiles, n, out, status, ctl, d_count, dead, s_wsum, &s_excl);
     }
 }
 
-// ---- large inputs: super-rounds that re-read from the Infinity Cache -------------------------
-// For n beyond the MALL, each super-round covers G blocks x S elements (S = mt tiles,
-// ~64 MiB per round).  Block b: pass 1 streams its sub-chunk from HBM and reduces it; ONE
-// look-back per block per round (status index r*G + b); pass 2 re-reads the same sub-chunk —
-// still resident in the 256 MiB MALL, since only ~64 MiB of other traffic happened since — and
-// writes the scanned output.  HBM moves 8 B/element; the look-back chain is per sub-chunk, not
-// per 32 KiB tile.
-constexpr int64_t kMallRoundBytes = (int64_t)64 << 20;   // per super-round, well below the MALL
+// ---- lagged look-back -----------------------------------------------------------------------
+// Measured on MI355X (profiles/r01_scan_ab.txt): resolving each tile's prefix right after
+// reducing it put the look-back round trip on every iteration's critical path (0.69 ms for 2^28
+// ints, 0.39 ms with the look-back removed).  Here a workgroup publishes tile t's aggregate as
+// soon as t is reduced, and resolves t's prefix in the NEXT iteration, after issuing the loads
+// of t+2G and reducing t+G: by then every predecessor's aggregate is out, so the look-back
+// rarely spins, and its round trip overlaps the loads in flight.  The deferred tile's raw values
+// wait in LDS (2 x 32 KiB ping-pong); each thread keeps only its 8 per-chunk local offsets.
+struct LagTile {
+    uint32_t pre[kChunks];   // this thread's exclusive local offset of each of its chunks
+    uint32_t total;          // tile aggregate
+    int tile;
+};
 
+// Reduce tile `cur` into LDS parity `par` and publish its aggregate.
 template <int MODE>
-__device__ __forceinline__ uint32_t tile_reduce(const v4i (&v)[kChunks]) {
-    uint32_t acc = 0;
+__device__ __forceinline__ void lag_reduce(const v4i (&cur)[kChunks], int tile, int par, int32_t (*s_data)[kTile],
+                                           uint32_t (*s_wsum)[kChunks][4], uint64_t* __restrict__ status,
+                                           LagTile& L) {
+    const int tid = threadIdx.x;
+    // tile_offsets' leading barrier also orders these writes after the previous readers of
+    // s_data[par] (the store phase of the step before last)
+    L.total = tile_offsets<MODE>(cur, s_wsum[par], L.pre);
+#pragma unroll
+    for (int k = 0; k < kChunks; ++k)
+        *reinterpret_cast<v4i*>(&s_data[par][k * (kThreads * 4) + 4 * tid]) = cur[k];
+    L.tile = tile;
+    if (tid == 0) lb::publish(status, tile, tile == 0 ? lb::kFlagPre : lb::kFlagAgg, L.total);
+}
+
+// Wave 0: resolve the deferred tile's prefix, publish it, share it through LDS.
+__device__ __forceinline__ void lag_resolve(const LagTile& L, uint32_t* s_excl, uint64_t* __restrict__ status,
+                                            uint32_t* __restrict__ ctl) {
+    const int lane = threadIdx.x & 63;
+    uint32_t excl = 0;
+    if (L.tile != 0) {
+        excl = lb::lookback<kLagWindows>(status, L.tile, lane, &ctl[1]);
+        if (lane == 0) lb::publish(status, L.tile, lb::kFlagPre, excl + L.total);
+    }
+    if (lane == 0) *s_excl = excl;
+}
+
+// Outputs of a resolved tile, values from LDS parity `par`.
+template <int MODE>
+__device__ __forceinline__ void lag_store(const LagTile& L, int par, const int32_t (*s_data)[kTile],
+                                          const uint32_t* s_excl, int num_tiles, int32_t* __restrict__ out,
+                                          int64_t* __restrict__ d_count, int32_t* __restrict__ dead) {
+    const int tid = threadIdx.x;
+    const uint32_t excl = *s_excl;
+    const int64_t base = (int64_t)L.tile * kTile;
 #pragma unroll
     for (int k = 0; k < kChunks; ++k) {
-        if (MODE == kScan)
-            acc += ((uint32_t)v[k][0] + (uint32_t)v[k][1]) + ((uint32_t)v[k][2] + (uint32_t)v[k][3]);
-        else
-            acc += (uint32_t)(v[k][0] != 0) + (uint32_t)(v[k][1] != 0) + (uint32_t)(v[k][2] != 0) +
-                   (uint32_t)(v[k][3] != 0);
+        const v4i v = *reinterpret_cast<const v4i*>(&s_data[par][k * (kThreads * 4) + 4 * tid]);
+        write_chunk<MODE, true>(v, base + (int64_t)k * (kThreads * 4) + 4 * tid, excl + L.pre[k], 0, out, dead);
     }
-    return acc;
+    if (MODE != kScan && tid == 0 && L.tile == num_tiles - 1) *d_count = (int64_t)(excl + L.total);
 }
 
+// One step: prefetch tile+G into `pf`, reduce `cur` (= tile), resolve + write the deferred tile.
 template <int MODE>
-__global__ __launch_bounds__(kThreads) void k_scan_mall(const int32_t* __restrict__ in, int32_t* __restrict__ out,
-                                                        int64_t n, uint64_t* __restrict__ status,
-                                                        uint32_t* __restrict__ ctl, int64_t* __restrict__ d_count,
-                                                        int32_t* __restrict__ dead, int mt, int xp) {
-    __shared__ uint32_t s_wsum[kChunks][4];
-    __shared__ uint32_t s_red[4];
-    __shared__ uint32_t s_excl;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int G = (int)gridDim.x, b = (int)blockIdx.x;
-    const int64_t S = (int64_t)mt * kTile;   // mt even
-    const int64_t round_elems = S * G;
-    const int rounds = (int)((n + round_elems - 1) / round_elems);
-    const int num_units = rounds * G;           // look-back index space
-    uint32_t sink = 0;                          // timing ablations only (xp != 0)
-    for (int r = 0; r < rounds; ++r) {
-        const int64_t lo = (int64_t)r * round_elems + (int64_t)b * S;
-        const int unit = r * G + b;
-        // pass 1: aggregate of the sub-chunk (HBM), two tiles in flight
-        uint32_t acc = 0;
-        if (xp & 4) {
-        } else if (lo + S <= n) {
-            v4i x[kChunks], y[kChunks];
-            load_full(in, lo, tid, x);
-#pragma unroll
-            for (int t = 0; t < mt; t += 2) {
-                load_full(in, lo + (int64_t)(t + 1) * kTile, tid, y);
-                acc += tile_reduce<MODE>(x);
-                if (t + 2 < mt) load_full(in, lo + (int64_t)(t + 2) * kTile, tid, x);
-                acc += tile_reduce<MODE>(y);
-            }
-        } else {
-            for (int t = 0; t < mt; ++t) {
-                const int64_t tb = lo + (int64_t)t * kTile;
-                if (tb >= n) break;
-                v4i x[kChunks];
-                load_guarded(in, n, tb, tid, x);
-                acc += tile_reduce<MODE>(x);
-            }
-        }
-        // block reduce -> publish aggregate -> look-back
-        uint32_t wacc = lb::wave_sum(acc);
+__device__ __forceinline__ void lag_step(const int32_t* __restrict__ in, const v4i (&cur)[kChunks],
+                                         v4i (&pf)[kChunks], int tile, int G, int num_full, int num_tiles, int par,
+                                         LagTile& prev, bool& have_prev, int32_t (*s_data)[kTile],
+                                         uint32_t (*s_wsum)[kChunks][4], uint32_t* s_excl,
+                                         int32_t* __restrict__ out, uint64_t* __restrict__ status,
+                                         uint32_t* __restrict__ ctl, int64_t* __restrict__ d_count,
+                                         int32_t* __restrict__ dead) {
+    const int t1 = tile + G;
+    // unconditional (clamped) prefetch: a branch here would make the wait-count pass merge
+    // "issued"/"skipped" states and drain the prefetch at the first use of the other buffer
+    load_full(in, (int64_t)(t1 < num_full ? t1 : tile) * kTile, (int)threadIdx.x, pf);
+    LagTile L;
+    lag_reduce<MODE>(cur, tile, par, s_data, s_wsum, status, L);
+    if (have_prev) {
+        if ((threadIdx.x >> 6) == 0) lag_resolve(prev, s_excl, status, ctl);
         lds_barrier();
-        if (lane == 0) s_red[wave] = wacc;
-        lds_barrier();
-        const uint32_t agg = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
-        if (wave == 0) {
-            uint32_t excl = 0;
-            if (unit == 0 || (xp & 1)) {
-                if (lane == 0) lb::publish(status, unit, lb::kFlagPre, agg);
-            } else {
-                if (lane == 0) lb::publish(status, unit, lb::kFlagAgg, agg);
-                excl = lb::lookback(status, unit, lane, &ctl[1]);
-                if (lane == 0) lb::publish(status, unit, lb::kFlagPre, excl + agg);
-            }
-            if (lane == 0) s_excl = excl;
-        }
-        lds_barrier();
-        uint32_t running = s_excl;
-        // pass 2: re-read (MALL), scan, write
-        for (int t = 0; t < mt; ++t) {
-            const int64_t tb = lo + (int64_t)t * kTile;
-            if (tb >= n) break;
-            const bool full = tb + kTile <= n;
-            v4i cur[kChunks];
-            if (xp & 2) {
-#pragma unroll
-                for (int k = 0; k < kChunks; ++k) cur[k] = v4i{tid, k, r, t};
-            } else if (full) load_full(in, tb, tid, cur);
-            else load_guarded(in, n, tb, tid, cur);
-            uint32_t sv[kChunks], incl[kChunks];
-#pragma unroll
-            for (int k = 0; k < kChunks; ++k) {
-                if (MODE == kScan)
-                    sv[k] = ((uint32_t)cur[k][0] + (uint32_t)cur[k][1]) + ((uint32_t)cur[k][2] + (uint32_t)cur[k][3]);
-                else
-                    sv[k] = (uint32_t)(cur[k][0] != 0) + (uint32_t)(cur[k][1] != 0) + (uint32_t)(cur[k][2] != 0) +
-                            (uint32_t)(cur[k][3] != 0);
-                incl[k] = lb::wave_inclusive_scan(sv[k]);
-            }
-            lds_barrier();
-            if (lane == 63) {
-#pragma unroll
-                for (int k = 0; k < kChunks; ++k) s_wsum[k][wave] = incl[k];
-            }
-            lds_barrier();
-            uint32_t run = 0;
-            uint32_t off[kChunks];
-#pragma unroll
-            for (int k = 0; k < kChunks; ++k) {
-                uint32_t before = 0;
-#pragma unroll
-                for (int w = 0; w < 4; ++w) {
-                    const uint32_t xw = s_wsum[k][w];
-                    before += (w < wave) ? xw : 0u;
-                }
-                off[k] = run + before;
-#pragma unroll
-                for (int w = 0; w < 4; ++w) run += s_wsum[k][w];
-            }
-#pragma unroll
-            for (int k = 0; k < kChunks; ++k) {
-                const int64_t e0 = tb + (int64_t)k * (kThreads * 4) + 4 * tid;
-                uint32_t run_k = running + off[k] + (incl[k] - sv[k]);
-                if (MODE == kScan) {
-                    v4i o;
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) { o[e] = (int32_t)run_k; run_k += (uint32_t)cur[k][e]; }
-                    if (xp & 8) {
-                        sink += (uint32_t)(o[0] ^ o[1] ^ o[2] ^ o[3]);
-                    } else if (full) {
-                        __builtin_nontemporal_store(o, reinterpret_cast<v4i*>(out + e0));
-                    } else {
-#pragma unroll
-                        for (int e = 0; e < 4; ++e)
-                            if (e0 + e < n) out[e0 + e] = o[e];
-                    }
-                } else if (MODE == kCompact) {
-#pragma unroll
-                    for (int e = 0; e < 4; ++e)
-                        if (cur[k][e] != 0) out[run_k++] = cur[k][e];
-                } else {
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        const int64_t idx = e0 + e;
-                        if (idx < n) {
-                            if (cur[k][e] != 0) out[run_k++] = (int32_t)idx;
-                            else dead[idx - (int64_t)run_k] = (int32_t)idx;
-                        }
-                    }
-                }
-            }
-            running += run;
-        }
-        if (MODE != kScan && tid == 0 && unit == num_units - 1) *d_count = (int64_t)running;
+        lag_store<MODE>(prev, par ^ 1, s_data, s_excl, num_tiles, out, d_count, dead);
     }
-    if (xp & 8) dead[(int64_t)b * kThreads + tid] = (int32_t)sink;   // keeps the ablated work live
+    prev = L;
+    have_prev = true;
+}
+
+// 16-byte aligned pointers: persistent co-resident grid, static tiles b, b+G, b+2G, ...
+template <int MODE>
+__global__ __launch_bounds__(kThreads) void k_scan_lag(const int32_t* __restrict__ in, int32_t* __restrict__ out,
+                                                       int64_t n, uint64_t* __restrict__ status,
+                                                       uint32_t* __restrict__ ctl, int64_t* __restrict__ d_count,
+                                                       int32_t* __restrict__ dead) {
+    __shared__ __attribute__((aligned(16))) int32_t s_data[2][kTile];
+    __shared__ uint32_t s_wsum[2][kChunks][4];
+    __shared__ uint32_t s_excl;
+    const int tid = threadIdx.x;
+    const int G = (int)gridDim.x;
+    const int num_tiles = (int)((n + kTile - 1) / kTile);
+    const int num_full = (int)(n / kTile);
+    int tile = blockIdx.x;
+    if (tile < num_full) {
+        // two named register buffers, loop unrolled by two: no load destination is ever copied,
+        // so the wait-count pass keeps each prefetch in flight across the other buffer's step
+        v4i bA[kChunks], bB[kChunks];
+        LagTile prev;
+        bool have_prev = false;
+        int par = 0;
+        load_full(in, (int64_t)tile * kTile, tid, bA);
+        for (;;) {
+            lag_step<MODE>(in, bA, bB, tile, G, num_full, num_tiles, par, prev, have_prev, s_data, s_wsum, &s_excl,
+                           out, status, ctl, d_count, dead);
+            tile += G;
+            par ^= 1;
+            if (tile >= num_full) break;
+            lag_step<MODE>(in, bB, bA, tile, G, num_full, num_tiles, par, prev, have_prev, s_data, s_wsum, &s_excl,
+                           out, status, ctl, d_count, dead);
+            tile += G;
+            par ^= 1;
+            if (tile >= num_full) break;
+        }
+        // drain: the last reduced tile
+        if ((tid >> 6) == 0) lag_resolve(prev, &s_excl, status, ctl);
+        lds_barrier();
+        lag_store<MODE>(prev, par ^ 1, s_data, &s_excl, num_tiles, out, d_count, dead);
+    }
+    // the (single) partial tail tile, resolved immediately
+    for (; tile < num_tiles; tile += G) {
+        v4i cur[kChunks];
+        load_guarded(in, n, (int64_t)tile * kTile, tid, cur);
+        process_tile<MODE>(cur, tile, num_tiles, n, out, status, ctl, d_count, dead, s_wsum[0], &s_excl);
+    }
 }
 
 __global__ void k_append_dead(const int32_t* __restrict__ dead, int32_t* __restrict__ perm,
@@ -368,10 +330,12 @@ __global__ void k_append_dead(const int32_t* __restrict__ dead, int32_t* __restr
         perm[live + j] = dead[j];
 }
 
-// Co-resident persistent grid for a 256-thread kernel: CUs x blocks/CU, one block/CU below the
-// occupancy API's answer (it can over-report by one for SGPR-heavy kernels, MI355X_MICROARCH.md
-// "Residency and cooperative launch"), at most 8.
+// ---- host ---------------------------------------------------------------------------------
 int resident_grid(const void* kernel) {
+    // Persistent look-back kernels need every workgroup co-resident.  The occupancy API can
+    // over-report by one when a resource is filled exactly (scripts/probes/residency.hip: five
+    // 32 KiB-LDS workgroups per CU are NOT all resident), so a per-CU count is accepted only
+    // while LDS and VGPRs keep headroom.
     static std::mutex mu;
     static std::vector<std::pair<const void*, int>> cache;
     std::lock_guard<std::mutex> lk(mu);
@@ -382,28 +346,23 @@ int resident_grid(const void* kernel) {
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kThreads, 0) != hipSuccess || per_cu <= 0)
         per_cu = 2;
-    per_cu = std::max(1, std::min(per_cu, 8) - 1);
+    per_cu = std::min(per_cu, 8);
+    hipFuncAttributes fa{};
+    if (hipFuncGetAttributes(&fa, kernel) == hipSuccess) {
+        const int vgpr = ((fa.numRegs + 7) / 8) * 8;
+        const size_t lds = fa.sharedSizeBytes;
+        while (per_cu > 1 && ((size_t)per_cu * lds > (size_t)(152 * 1024) || per_cu * vgpr > 504)) --per_cu;
+    } else {
+        per_cu = std::max(1, per_cu - 1);
+    }
     const int g = cus * per_cu;
     cache.push_back({kernel, g});
     return g;
 }
 
-int env_int(const char* name, int dflt) {
-    const char* v = getenv(name);
-    return v && *v ? atoi(v) : dflt;
-}
-int cu_count() {
-    int dev = 0, cus = 256;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    return cus;
-}
-
 size_t status_bytes(int64_t n) {
-    // per-tile words for k_scan_tiles; k_scan_mall uses rounds x G <= n / (2 kTile) + G
-    // words, which is below this bound for n >= kMallMinElems; the +2048 covers G anyway.
-    const int64_t tiles = (n + kTile - 1) / kTile + 2048;
-    return (size_t)tiles * sizeof(uint64_t);
+    const int64_t tiles = (n + kTile - 1) / kTile;
+    return (size_t)(tiles > 0 ? tiles : 1) * sizeof(uint64_t);
 }
 
 struct Workspace {
@@ -458,31 +417,17 @@ int launch(const int32_t* d_in, int32_t* d_out, int64_t n, int64_t* d_count, voi
     if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(workspace)");
     const int64_t tiles = (n + kTile - 1) / kTile;
     const bool aligned = ((reinterpret_cast<uintptr_t>(d_in) | reinterpret_cast<uintptr_t>(d_out)) & 15) == 0;
-    // Infinity-Cache two-pass scheme for inputs well beyond the 256 MiB MALL (and out of place:
-    // pass 2 re-reads the input after other blocks have written outputs).
-    static const bool use_mall = env_int("SC_MALL", 1) != 0;
-    if (use_mall && aligned && d_in != d_out && n >= kMallMinElems) {
-        // SC_EXPERIMENT / SC_PER_CU / SC_ROUND_MB: timing ablations for tuning (results are not
-        // valid when SC_EXPERIMENT is set); unset in production.
-        static const int xp = env_int("SC_EXPERIMENT", 0);
-        static const int per_cu_env = env_int("SC_PER_CU", 0);
-        static const int64_t round_bytes = (int64_t)env_int("SC_ROUND_MB", (int)(kMallRoundBytes >> 20)) << 20;
-        int g = resident_grid((const void*)k_scan_mall<MODE>);
-        if (per_cu_env > 0) g = cu_count() * per_cu_env;
-        const int mt = std::max<int>(2, (int)(round_bytes / ((int64_t)g * kTile * 4)) & ~1);
-        hipLaunchKernelGGL((k_scan_mall<MODE>), dim3(g), dim3(kThreads), 0, stream, d_in, d_out, n, status, ctl,
-                           d_count, dead, mt, xp);
-    } else if (aligned) {
-        const int g = (int)std::min<int64_t>(tiles, resident_grid((const void*)k_scan_tiles<MODE, true>));
-        hipLaunchKernelGGL((k_scan_tiles<MODE, true>), dim3(g), dim3(kThreads), 0, stream,
-                           d_in, d_out, n, status, ctl, d_count, dead);
+    if (aligned) {
+        const int g = (int)std::min<int64_t>(tiles, resident_grid((const void*)k_scan_lag<MODE>));
+        hipLaunchKernelGGL((k_scan_lag<MODE>), dim3(g), dim3(kThreads), 0, stream, d_in, d_out, n, status, ctl,
+                           d_count, dead);
     } else {
-        const int g = (int)std::min<int64_t>(tiles, resident_grid((const void*)k_scan_tiles<MODE, false>));
-        hipLaunchKernelGGL((k_scan_tiles<MODE, false>), dim3(g), dim3(kThreads), 0, stream,
-                           d_in, d_out, n, status, ctl, d_count, dead);
+        const int g = (int)std::min<int64_t>(tiles, resident_grid((const void*)k_scan_tiles<MODE>));
+        hipLaunchKernelGGL((k_scan_tiles<MODE>), dim3(g), dim3(kThreads), 0, stream, d_in, d_out, n, status, ctl,
+                           d_count, dead);
     }
     e = hipGetLastError();
-    if (e != hipSuccess) return hip_fail(e, "k_scan_tiles launch");
+    if (e != hipSuccess) return hip_fail(e, "scan kernel launch");
     if (MODE == kPartition) {
         const int64_t blocks = std::min<int64_t>((n + 255) / 256, 4096);
         hipLaunchKernelGGL(k_append_dead, dim3((unsigned)blocks), dim3(256), 0, stream, dead, d_out, n,

@@ -24,4 +24,8 @@ e1.record(st)
 torch.cuda.synchronize()
 ms = e0.elapsed_time(e1) / reps
 ok = bool(torch.equal(out[1:] - out[:-1], a[:-1])) and int(out[0].item()) == 0
-print(f"{os.environ.get('TAG','')} ms={ms:.4f} GB/s={8*n/ms/1e6:.0f} ok={ok}", flush=True)
+extra = ""
+if int(os.environ.get("SC_EXPERIMENT", "0")) & 16:
+    c = ws[:16].view(torch.int32).cpu().tolist()
+    extra = f" lookbacks={c[2]} extra_rounds={c[3]} ({c[3] / max(c[2], 1):.2f}/lookback, last call)"
+print(f"{os.environ.get('TAG','')} ms={ms:.4f} GB/s={8*n/ms/1e6:.0f} ok={ok}{extra}", flush=True)
