@@ -21,7 +21,7 @@ namespace lb {
 
 constexpr uint64_t kFlagAgg = 1ull << 62;
 constexpr uint64_t kFlagPre = 2ull << 62;
-constexpr uint32_t kSpinLimit = 1u << 21;
+constexpr uint32_t kSpinLimit = 1u << 18;   // ~0.25 s of polling; a live chain resolves in us
 constexpr int kWindows = 4;
 
 __device__ __forceinline__ void publish(uint64_t* st, int tile, uint64_t flag, uint32_t v) {
@@ -94,9 +94,13 @@ __device__ __forceinline__ uint32_t lookback_impl(uint64_t* st, int tile, int la
         }
         base -= 64 * consumed;
         if (stalled) {
-            if (++spins > kSpinLimit) {
+            // Give up when this wave has spun too long or any other wave already gave up (so one
+            // stuck chain costs ~0.25 s, not one timeout per tile): results are then wrong and
+            // flagged, but the grid always drains.
+            if (++spins > kSpinLimit ||
+                ((spins & 63) == 0 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)) {
                 if (lane == 0) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                return excl;   // give up (flagged): results are wrong but the grid drains
+                return excl;
             }
             __builtin_amdgcn_s_sleep(1);
         }

@@ -896,7 +896,8 @@ struct pt_ctx {
     pt_flags flags{};
     KArgs args{};
     int max_tiles = 0, max_t64 = 0;
-    int grid_trace = 0, grid_compact = 0, grid_fused = 0;
+    int grid_trace = 0, grid_compact = 0;
+    int grid_bounce[8] = {};   // per k_bounce variant (first, spp1, mesh): its co-resident grid
     bool fused = true;   // pipeline: fused bounce kernel (default) or trace + compact
     uint64_t compact_launches = 0;   // parity of the look-back status / live-count words
     // owned device allocations
@@ -974,6 +975,24 @@ int prof_begin(pt_ctx* c, hipStream_t st, int kind, ProfEv** out) {
 int prof_end(ProfEv* ev, hipStream_t st) {
     if (ev) HIP_TRY(hipEventRecord(ev->b, st));
     return PT_OK;
+}
+
+// Workgroups per CU that are guaranteed co-resident for a persistent look-back kernel: the
+// occupancy API's answer, lowered while LDS or VGPRs would be filled (almost) exactly.  Measured:
+// five 32 KiB-LDS workgroups per CU are not all resident (scripts/probes/residency.hip), and a
+// k_bounce variant at 7 x 72 VGPRs per SIMD stalled its look-back; 2 x 176 VGPRs and 3 x 48 KiB
+// LDS are fine.  Budget: <= 448 of 512 VGPRs per SIMD lane, <= 152 KiB of 160 KiB LDS per CU.
+int resident_per_cu(const void* kernel) {
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, 0) != hipSuccess || per_cu <= 0)
+        return 1;
+    per_cu = std::min(per_cu, 8);
+    hipFuncAttributes fa{};
+    if (hipFuncGetAttributes(&fa, kernel) != hipSuccess) return std::max(1, per_cu - 1);
+    const int vgpr = ((fa.numRegs + 7) / 8) * 8;
+    const size_t lds = fa.sharedSizeBytes;
+    while (per_cu > 1 && ((size_t)per_cu * lds > (size_t)(152 * 1024) || per_cu * vgpr > 448)) --per_cu;
+    return per_cu;
 }
 
 using KernelFn = void (*)(const KArgs);
@@ -1167,18 +1186,14 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
     // k_trace has no inter-workgroup dependency: 8 workgroups per CU, grid-stride beyond that.
     // k_compact_paths is persistent + look-back: co-resident grid (one block/CU below the
     // occupancy API's answer, which can over-report by one for SGPR-heavy kernels).
-    int cus = 256, per_cu = 0;
+    int cus = 256;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
     c->grid_trace = std::max(1, std::min({(int)((P + kBlock - 1) / kBlock), cus * 8, A.emit_stride}));
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_compact_paths, kBlock, 0) != hipSuccess || per_cu <= 0)
-        per_cu = 2;
-    per_cu = std::max(1, std::min(per_cu, 8) - 1);
-    c->grid_compact = std::max(1, std::min(c->max_tiles, cus * per_cu));
-    per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_bounce<false, true, false>, kBlock, 0) != hipSuccess || per_cu <= 0)
-        per_cu = 2;
-    per_cu = std::max(1, std::min(per_cu, 8) - 1);
-    c->grid_fused = std::max(1, std::min({c->max_tiles, cus * per_cu, A.emit_stride}));
+    c->grid_compact = std::max(1, std::min(c->max_tiles, cus * resident_per_cu((const void*)k_compact_paths)));
+    for (int v = 0; v < 8; ++v) {   // each k_bounce variant launches with its own co-resident grid
+        const int per_cu = resident_per_cu((const void*)bounce_kernel(v & 4, v & 2, v & 1));
+        c->grid_bounce[v] = std::max(1, std::min({c->max_tiles, cus * per_cu, A.emit_stride}));
+    }
     if (const char* pl = std::getenv("PT_PIPELINE")) c->fused = std::string(pl) != "split";
     *out = c;
     return PT_OK;
@@ -1217,7 +1232,7 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
         A.out = c->buf[cur ^ 1];
         int rc;
         if (!sorted && c->fused) {
-            rc = launch_k(c, bounce_kernel(b == 0, spp1, mesh), c->grid_fused, st,
+            rc = launch_k(c, bounce_kernel(b == 0, spp1, mesh), c->grid_bounce[(b == 0 ? 4 : 0) + (spp1 ? 2 : 0) + (mesh ? 1 : 0)], st,
                           b == 0 ? PT_KIND_FIRST_BOUNCE : PT_KIND_BOUNCE, A);
             if (rc) return rc;
             ++c->compact_launches;

@@ -333,9 +333,9 @@ __global__ void k_append_dead(const int32_t* __restrict__ dead, int32_t* __restr
 // ---- host ---------------------------------------------------------------------------------
 int resident_grid(const void* kernel) {
     // Persistent look-back kernels need every workgroup co-resident.  The occupancy API can
-    // over-report by one when a resource is filled exactly (scripts/probes/residency.hip: five
-    // 32 KiB-LDS workgroups per CU are NOT all resident), so a per-CU count is accepted only
-    // while LDS and VGPRs keep headroom.
+    // over-report when a resource is filled (almost) exactly (see resident_per_cu in
+    // pt_kernels.hip for the measurements), so a per-CU count is accepted only while LDS
+    // (<= 152 of 160 KiB) and VGPRs (<= 448 of 512 per SIMD lane) keep headroom.
     static std::mutex mu;
     static std::vector<std::pair<const void*, int>> cache;
     std::lock_guard<std::mutex> lk(mu);
@@ -351,7 +351,7 @@ int resident_grid(const void* kernel) {
     if (hipFuncGetAttributes(&fa, kernel) == hipSuccess) {
         const int vgpr = ((fa.numRegs + 7) / 8) * 8;
         const size_t lds = fa.sharedSizeBytes;
-        while (per_cu > 1 && ((size_t)per_cu * lds > (size_t)(152 * 1024) || per_cu * vgpr > 504)) --per_cu;
+        while (per_cu > 1 && ((size_t)per_cu * lds > (size_t)(152 * 1024) || per_cu * vgpr > 448)) --per_cu;
     } else {
         per_cu = std::max(1, per_cu - 1);
     }

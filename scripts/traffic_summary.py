@@ -12,8 +12,8 @@ import sys
 from collections import defaultdict
 from pathlib import Path
 
-KEYS = {"k_bounce<false": "k_bounce", "k_bounce<true": "k_bounce_first", "k_scan_mall<0": "scan",
-        "k_scan_tiles<0": "scan_tiles", "k_trace": "k_trace", "k_compact_paths": "k_compact_paths"}
+KEYS = {"k_bounce<false": "k_bounce", "k_bounce<true": "k_bounce_first", "k_scan_lag<0": "scan",
+        "k_scan_tiles<0": "scan_tiles", "k_scan_mall<0": "scan_mall", "k_trace": "k_trace", "k_compact_paths": "k_compact_paths"}
 
 
 def load(dirpath: Path, counter: str):
