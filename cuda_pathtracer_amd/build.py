@@ -86,7 +86,7 @@ def build_native(verbose: bool = False, force: bool = False) -> Path:
 
 def build_oracle(verbose: bool = False, force: bool = False) -> Path:
     """The CPU checker (test infrastructure only): serial g++ build, no FMA contraction."""
-    srcs = [ORACLE_DIR / "sc_oracle.cpp", ORACLE_DIR / "pt_oracle.cpp"]
+    srcs = [ORACLE_DIR / "sc_oracle.cpp", ORACLE_DIR / "pt_oracle.cpp", ORACLE_DIR / "mesh_oracle.cpp"]
     ORACLE_LIB.parent.mkdir(exist_ok=True)
     if force or _stale(ORACLE_LIB, srcs):
         _run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-fno-fast-math",

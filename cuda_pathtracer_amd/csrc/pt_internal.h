@@ -20,7 +20,8 @@ struct TextureHost {
 struct Scene {
     std::vector<pt_geom> geoms;
     std::vector<pt_material> materials;
-    std::vector<pt_triangle> triangles;     // BVH (DFS) order after finalize
+    std::vector<pt_triangle> tris_load;     // mesh triangles in load order (ids = index here)
+    std::vector<pt_triangle> triangles;     // BVH leaf order, built from tris_load by finalize
     std::vector<pt_bvh_node> bvh;
     std::vector<TextureHost> textures;
     pt_camera camera{};
@@ -39,7 +40,7 @@ int scene_finalize(Scene& S);
 int load_obj_mesh(Scene& S, const std::string& path, int32_t mat, const float* t, const float* r, const float* s);
 int add_mesh(Scene& S, int32_t mat, const float* t, const float* r, const float* s, const float* pos, int32_t npos,
              const float* nrm, int32_t nnrm, const float* uv, int32_t nuv, const int32_t* face_sizes, int32_t nfaces,
-             const int32_t* ip, const int32_t* in, const int32_t* it);
+             const int32_t* ip, const int32_t* in, const int32_t* it, int32_t* id_out);
 int build_bvh(Scene& S);
 
 }  // namespace pt

@@ -41,6 +41,18 @@ class OCamera(C.Structure):
                 ("fov", C.c_float * 2), ("pixel_length", C.c_float * 2)]
 
 
+class OTexture(C.Structure):
+    _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("components", C.c_int32), ("pad", C.c_int32),
+                ("data", C.c_void_p)]
+
+
+TRI_DTYPE = np.dtype([("id", "<i4"), ("v", "<f4", (3, 3)), ("uv", "<f4", (3, 2)), ("n", "<f4", (3, 3)),
+                      ("bmin", "<f4", (3,)), ("bmax", "<f4", (3,))])
+NODE_DTYPE = np.dtype([("bmin", "<f4", (3,)), ("bmax", "<f4", (3,)), ("sub_areas", "<i4"), ("axis", "<i4"),
+                       ("first_area_idx", "<i4"), ("rchild_idx", "<i4")])
+assert TRI_DTYPE.itemsize == 124 and NODE_DTYPE.itemsize == 40
+
+
 class OFlags(C.Structure):
     _fields_ = [("russian_roulette", C.c_int32), ("use_bvh", C.c_int32), ("use_bbox", C.c_int32),
                 ("sort_by_material", C.c_int32), ("use_thrust_partition", C.c_int32), ("ssaa", C.c_int32),
@@ -85,6 +97,10 @@ def lib() -> C.CDLL:
         L.oracle_render.restype = C.c_double
         L.oracle_tonemap.argtypes = [P, C.c_int, C.c_int, C.c_float, P]
         L.oracle_preview.argtypes = [P, C.c_int, C.c_int, C.c_int, P]
+        L.oracle_load_obj.argtypes = [C.c_char_p, P, P, C.c_int, P, C.c_int, P, P]
+        L.oracle_load_obj.restype = C.c_int
+        L.oracle_build_bvh.argtypes = [P, C.c_int, P, C.c_int]
+        L.oracle_build_bvh.restype = C.c_int
         _lib = L
     return _lib
 
@@ -139,6 +155,17 @@ def camera(res, fovy, eye, lookat, up) -> OCamera:
     return cam
 
 
+def load_texture(path):
+    """Decoded texels (the reference decodes with stb_image; both hosts here use PIL, so the
+    oracle and the product shade from the same bytes — JPEG decoding is not on the hot path)."""
+    from PIL import Image
+    im = Image.open(path)
+    if im.mode not in ("RGB", "RGBA", "L"):
+        im = im.convert("RGB")
+    comps = {"RGB": 3, "RGBA": 4, "L": 1}[im.mode]
+    return im.width, im.height, comps, np.frombuffer(im.tobytes(), np.uint8).copy()
+
+
 class OracleScene:
     def __init__(self):
         self.geoms: list[OGeom] = []
@@ -147,6 +174,53 @@ class OracleScene:
         self.depth = 8
         self.iterations = 1
         self.file = "render"
+        self.tris_load = np.zeros(0, TRI_DTYPE)     # mesh triangles, load order
+        self.tris = np.zeros(0, TRI_DTYPE)          # BVH leaf order (after build_bvh)
+        self.nodes = np.zeros(0, NODE_DTYPE)
+        self.textures: list[tuple] = []             # (w, h, comps, uint8 array)
+
+    def add_mesh_obj(self, obj_path, material, t, r, s) -> int:
+        """scene.cpp:94-173: one mesh geom from an OBJ file (oracle/mesh_oracle.cpp)."""
+        gid = self.add_geom(2, material, t, r, s)
+        g = self.geoms[gid]
+        T = np.array(g.transform[:], np.float32)
+        IT = np.array(g.inv_transpose[:], np.float32)
+        bmin, bmax = np.zeros(3, np.float32), np.zeros(3, np.float32)
+        base = len(self.tris_load)
+        n = lib().oracle_load_obj(str(obj_path).encode(), T.ctypes.data, IT.ctypes.data, base, None, 0,
+                                  bmin.ctypes.data, bmax.ctypes.data)
+        if n < 0:
+            raise FileNotFoundError(obj_path)
+        tr = np.zeros(n, TRI_DTYPE)
+        lib().oracle_load_obj(str(obj_path).encode(), T.ctypes.data, IT.ctypes.data, base, tr.ctypes.data, n,
+                              bmin.ctypes.data, bmax.ctypes.data)
+        self.tris_load = np.concatenate([self.tris_load, tr])
+        g.tri_start, g.tri_end, g.bbox_idx = base, base + n, 0
+        g.min_bound[:] = bmin.tolist()
+        g.max_bound[:] = bmax.tolist()
+        return gid
+
+    def build_bvh(self):
+        """build_bvh_tree (BVH_tree.cpp:149-181) over every mesh triangle, load order in."""
+        self.tris = self.tris_load.copy()
+        n = len(self.tris)
+        nodes = np.zeros(max(2 * n, 1), NODE_DTYPE)
+        k = lib().oracle_build_bvh(self.tris.ctypes.data, n, nodes.ctypes.data, len(nodes)) if n else 0
+        self.nodes = nodes[:k].copy()
+
+    def add_texture(self, path) -> int:
+        self.textures.append(load_texture(path))
+        return len(self.textures) - 1
+
+    def _tables(self):
+        texs = (OTexture * max(len(self.textures), 1))()
+        for i, (w, h, c, data) in enumerate(self.textures):
+            texs[i] = OTexture(w, h, c, 0, data.ctypes.data)
+        tris = self.tris if len(self.tris) else None
+        nodes = self.nodes if len(self.nodes) else None
+        return (tris.ctypes.data if tris is not None else None, len(self.tris),
+                nodes.ctypes.data if nodes is not None else None, len(self.nodes),
+                texs if self.textures else None, len(self.textures))
 
     def add_material(self, rgb=(0, 0, 0), specrgb=None, specex=1.0, reflective=0.0, refractive=0.0, ior=0.0,
                      emittance=0.0, texture_id=-1) -> int:
@@ -176,17 +250,24 @@ class OracleScene:
         data = json.loads(Path(path).read_text())
         sc = cls()
         ids = {}
+        base = Path(path).resolve().parent
         for name in sorted(data["Materials"]):           # nlohmann::json objects are std::map
             p = data["Materials"][name]
             rgb = p.get("RGB", [0.0, 0.0, 0.0])
+            tex = -1
+            if p.get("TEXTURE_FILE"):
+                tex = sc.add_texture(base / "Textures" / p["TEXTURE_FILE"])
             ids[name] = sc.add_material(rgb=rgb, specrgb=p.get("SPECRGB", rgb), specex=p.get("SPECEX", 1.0),
                                         reflective=p.get("REFLECTIVE", 0.0), emittance=p.get("EMITTANCE", 0.0),
-                                        refractive=p.get("REFRACTIVE", 0.0), ior=p.get("IOR", 0.0))
+                                        refractive=p.get("REFRACTIVE", 0.0), ior=p.get("IOR", 0.0), texture_id=tex)
         for o in data["Objects"]:
             typ = {"sphere": 0, "cube": 1, "mesh": 2}[o["TYPE"]]
+            mat = ids.get(o["MATERIAL"], 0)
             if typ == 2:
-                raise NotImplementedError("oracle: mesh objects")
-            sc.add_geom(typ, ids.get(o["MATERIAL"], 0), o["TRANS"], o["ROTAT"], o["SCALE"])
+                sc.add_mesh_obj(base / "Models" / o["OBJ_FILE"], mat, o["TRANS"], o["ROTAT"], o["SCALE"])
+            else:
+                sc.add_geom(typ, mat, o["TRANS"], o["ROTAT"], o["SCALE"])
+        sc.build_bvh()
         c = data["Camera"]
         sc.set_camera(c["RES"], c["FOVY"], c["EYE"], c["LOOKAT"], c["UP"])
         sc.depth, sc.iterations, sc.file = int(c["DEPTH"]), int(c["ITERATIONS"]), c["FILE"]
@@ -211,7 +292,7 @@ def render_pass(sc: OracleScene, fl: OFlags, iter_first: int, spp: int = 1, rank
     live = np.zeros(64, np.uint64)
     G = (OGeom * len(sc.geoms))(*sc.geoms)
     M = (OMaterial * len(sc.materials))(*sc.materials)
-    lib().oracle_render_pass(G, len(sc.geoms), M, len(sc.materials), None, 0, None, 0, None, 0,
+    lib().oracle_render_pass(G, len(sc.geoms), M, len(sc.materials), *sc._tables(),
                              C.byref(sc.cam), d, C.byref(fl), iter_first, spp, rank, world,
                              image.ctypes.data, live.ctypes.data)
     return image, [int(x) for x in live[:d]]
@@ -223,7 +304,7 @@ def render(sc: OracleScene, fl: OFlags, iters: int, iter_first: int = 1):
     live = np.zeros(64, np.uint64)
     G = (OGeom * len(sc.geoms))(*sc.geoms)
     M = (OMaterial * len(sc.materials))(*sc.materials)
-    secs = lib().oracle_render(G, len(sc.geoms), M, len(sc.materials), None, 0, None, 0, None, 0,
+    secs = lib().oracle_render(G, len(sc.geoms), M, len(sc.materials), *sc._tables(),
                                C.byref(sc.cam), sc.depth, C.byref(fl), iter_first, iters, image.ctypes.data,
                                live.ctypes.data)
     return image, [int(x) for x in live[:sc.depth]], secs
