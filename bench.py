@@ -120,6 +120,11 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-scan", action="store_true")
     ap.add_argument("--scene", default=str(ROOT / "tests" / "scenes" / "cornell.json"))
+    ap.add_argument("--config", default="cornell", choices=["cornell", "cornell_hd_sorted", "multi_object_4k",
+                                                           "random_triangles_100k"],
+                    help="BASELINE.json workload: cornell (configs[1], the default line) or configs 3-5 "
+                         "generated by cuda_pathtracer_amd.scenes")
+    ap.add_argument("--bvh-cull", action="store_true", help="pt_flags.bvh_cull extension (mesh scenes)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -145,10 +150,27 @@ def main() -> None:
     from cuda_pathtracer_amd import distributed as D
     P.lib()
 
-    scene = P.Scene(args.scene)
+    from cuda_pathtracer_amd import scenes as SG
+    gui = P.GuiDataContainer()
+    scene_path, workload = args.scene, None
+    if args.config != "cornell":
+        gen_dir = ROOT / "gpurun_out" / "bench_scenes"
+        if rank == 0:
+            scene_path = SG.CONFIGS[args.config](gen_dir)
+        if dist is not None:
+            box = [scene_path]
+            dist.broadcast_object_list(box, src=0)
+            scene_path = box[0]
+        gui.sortbyMaterial = args.config == "cornell_hd_sorted"
+        workload = {"cornell_hd_sorted": "config 3: cornell geometry 1920x1080 DEPTH 16, material-sorted shading",
+                    "multi_object_4k": "config 4: 4K multi-object (spheres+boxes; diffuse, mirror, glass) DEPTH 8",
+                    "random_triangles_100k": "config 5: 100k random triangles via OBJ+BVH, 4K, DEPTH 32",
+                    }[args.config]
+    gui.bvhCull = bool(args.bvh_cull)
+    scene = P.Scene(scene_path)
     st_r = scene.state()
     spp = world
-    pt = P.PathTracer(scene, P.GuiDataContainer(), rank=rank, world=world, spp=spp)
+    pt = P.PathTracer(scene, gui, rank=rank, world=world, spp=spp)
     stream = torch.cuda.current_stream()
     _log(rank, f"[bench] tile rows={pt.rows} npix={pt.npix} paths/pass={pt.npaths} depth={st_r.traceDepth}")
 
@@ -199,11 +221,16 @@ def main() -> None:
 
     # roofline of the dominant kernel (bounces >= 1), over the profiled segment
     b_ms, b_n = prof["bounce"]
+    if b_n == 0:   # material-sorted pipeline: its kernels are all profiled under "sort"
+        b_ms, b_n = prof["sort"][0], max(1, prof_passes * (st_r.traceDepth - 1))
     f_ms, f_n = prof["first_bounce"]
     depth = st_r.traceDepth
     plive = [b - a for a, b in zip(sp0["bounce_live"], sp1["bounce_live"])]
     pemit = [b - a for a, b in zip(sp0["bounce_emit"], sp1["bounce_emit"])]
     seg_bounce = sum(plive[1:depth])
+    mesh = scene.counts()[2] > 0
+    kernel_name = ("material-sorted pipeline (raygen/isect+hist/scan/scatter/shade/compact)" if gui.sortbyMaterial
+                   else f"k_bounce<false,{'true' if spp == 1 else 'false'},{'true' if mesh else 'false'}>")
     kernel_min = 0
     for b in range(1, depth):
         n_out = plive[b + 1] if b + 1 < depth else 0
@@ -213,7 +240,7 @@ def main() -> None:
     achieved = per_launch_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": _traffic_from_profiles("k_bounce"),
-                "kernel": "k_bounce<false,true,false>", "avg_launch_ms": avg_ms, "launches": b_n,
+                "kernel": kernel_name, "avg_launch_ms": avg_ms, "launches": b_n,
                 "segments_per_launch": seg_bounce / max(b_n, 1),
                 "algorithmic_bytes_per_launch": per_launch_bytes,
                 "kernel_min_bytes_per_launch": kernel_min / max(b_n, 1)}
@@ -236,11 +263,13 @@ def main() -> None:
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (bundled cornell.json scene; camera rays generated on device)",
-            "config": {"workload": "cornell.json 800x800 DEPTH 8 default flags; per GPU 640000 camera paths "
-                                   "per step (rows y%N==rank, N spp per pass); fused bounce kernel",
-                       "scene": "cornell.json", "resolution": [800, 800], "depth": depth, "spp_per_step": spp,
-                       "paths_per_gpu_per_step": pt.npaths, "parallelism": f"pixel-tile x{world} + RCCL gather"},
+            "data": "synthetic (bundled cornell.json scene; camera rays generated on device)" if workload is None
+                    else "synthetic (generated scene, cuda_pathtracer_amd/scenes.py; camera rays generated on device)",
+            "config": {"workload": workload or ("cornell.json 800x800 DEPTH 8 default flags; per GPU 640000 camera "
+                                                "paths per step (rows y%N==rank, N spp per pass); fused bounce kernel"),
+                       "scene": Path(scene_path).name, "resolution": list(scene.camera().res), "depth": depth,
+                       "spp_per_step": spp, "paths_per_gpu_per_step": pt.npaths,
+                       "parallelism": f"pixel-tile x{world} + RCCL gather"},
             "roofline": roofline,
             "segments": seg_all,
             "bounce_live_per_pass": [x / args.steps for x in live],

@@ -29,7 +29,7 @@ class Flags(C.Structure):
     _fields_ = [("russian_roulette", C.c_int32), ("use_bvh", C.c_int32), ("use_bbox", C.c_int32),
                 ("sort_by_material", C.c_int32), ("use_thrust_partition", C.c_int32), ("ssaa", C.c_int32),
                 ("dof", C.c_int32), ("aperture", C.c_float), ("focal_dist", C.c_float),
-                ("single_albedo", C.c_int32)]
+                ("single_albedo", C.c_int32), ("bvh_cull", C.c_int32)]
 
 
 class Material(C.Structure):

@@ -86,19 +86,23 @@ struct DTexture {
     const uint8_t* data;
 };
 
-// Triangle hot data: v0 and the two edges (e1 = v1 - v0, e2 = v2 - v0 computed on the host with
-// the same single subtraction glm performs), so the per-test arithmetic is unchanged.
-struct DTri {
-    float v0[3], e1[3], e2[3];
-    int32_t id;
+typedef float v4f __attribute__((ext_vector_type(4)));
+
+// Triangle hot data, 48 bytes = three 16-byte loads: (v0, id bits), (e1, 0), (e2, 0).  The edges
+// e1 = v1 - v0, e2 = v2 - v0 are computed on the host with the same single subtraction glm
+// performs, so the per-test arithmetic is unchanged.
+struct alignas(16) DTri {
+    v4f a, b, c;
 };
 struct DTriAttr {    // read once for the closest hit
     float n[3][3];
     float uv[3][2];
 };
-struct DNode {       // == pt_bvh_node
-    float bmin[3], bmax[3];
-    int32_t sub_areas, axis, first, rchild;
+// BVH node, 32 bytes = two 16-byte loads: lo = (bmin, meta), hi = (bmax, link)
+//   leaf:     meta = sub_areas (> 0),  link = first triangle
+//   interior: meta = -(axis + 1),      link = right child (the left child is this node + 1)
+struct alignas(16) DNode {
+    v4f lo, hi;
 };
 
 // ---- RNG: thrust::default_random_engine (minstd_rand) seeded like makeSeededRandomEngine ----

@@ -60,6 +60,7 @@ struct SceneDev {
     const DNode* __restrict__ nodes;
     const DTexture* __restrict__ texs;
     int32_t ngeoms, nmats, ntris, nnodes;
+    int32_t bvh_depth;     // deepest interior node (root = 0): bounds the traversal stack
 };
 struct CamDev {
     float pos[3], view[3], up[3], right[3], pl[2];
@@ -69,6 +70,7 @@ struct FlagsDev {
     int32_t rr, bvh, bbox, ssaa, dof;
     float aperture, focal;
     int32_t single_albedo;
+    int32_t bvh_cull;
 };
 struct TileDev {
     int32_t W, rank, world, npix, spp, P, depth, iter_first;
@@ -168,9 +170,9 @@ __device__ __forceinline__ f3 sphere_normal(const DGeom& g, f3 obj, bool outside
 
 // glm::intersectRayTriangle (gtx/intersect.inl:37-74) with e1/e2 precomputed on the host.
 __device__ __forceinline__ bool ray_tri(const DTri& tr, f3 o, f3 d, float& bx, float& by, float& bz) {
-    const f3 v0 = F3(tr.v0[0], tr.v0[1], tr.v0[2]);
-    const f3 e1 = F3(tr.e1[0], tr.e1[1], tr.e1[2]);
-    const f3 e2 = F3(tr.e2[0], tr.e2[1], tr.e2[2]);
+    const f3 v0 = F3(tr.a[0], tr.a[1], tr.a[2]);
+    const f3 e1 = F3(tr.b[0], tr.b[1], tr.b[2]);
+    const f3 e2 = F3(tr.c[0], tr.c[1], tr.c[2]);
     const f3 p = cross(d, e2);
     const float a = dot(e1, p);
     if (a < kFLT_EPS) return false;
@@ -185,14 +187,18 @@ __device__ __forceinline__ bool ray_tri(const DTri& tr, f3 o, f3 d, float& bx, f
     return bz >= 0.0f;
 }
 
-// BoundingBox::intersect (boundingbox.h:73-92)
-__device__ __forceinline__ bool aabb_hit(const float* bmin, const float* bmax, f3 o, f3 inv) {
+// BoundingBox::intersect (boundingbox.h:73-92); `lo` = the entry parameter
+__device__ __forceinline__ bool aabb_hit(const float* bmin, const float* bmax, f3 o, f3 inv, float& lo) {
     const float mx = (bmin[0] - o.x) * inv.x, Mx = (bmax[0] - o.x) * inv.x;
     const float my = (bmin[1] - o.y) * inv.y, My = (bmax[1] - o.y) * inv.y;
     const float mz = (bmin[2] - o.z) * inv.z, Mz = (bmax[2] - o.z) * inv.z;
-    const float lo = gmax(gmax(gmin(mx, Mx), gmin(my, My)), gmin(mz, Mz));
+    lo = gmax(gmax(gmin(mx, Mx), gmin(my, My)), gmin(mz, Mz));
     const float hi = gmin(gmin(gmax(mx, Mx), gmax(my, My)), gmax(mz, Mz));
     return !(hi < 0) && !(lo > hi);
+}
+__device__ __forceinline__ bool aabb_hit(const float* bmin, const float* bmax, f3 o, f3 inv) {
+    float lo;
+    return aabb_hit(bmin, bmax, o, inv, lo);
 }
 
 struct MeshHit {
@@ -204,38 +210,72 @@ struct MeshHit {
 
 // BVHIntersectionTest (intersections.cu:169-224): explicit stack of 64, near child first,
 // pops silently on overflow, no t culling; ties keep the first triangle found.
-__device__ MeshHit bvh_traverse(const SceneDev& S, f3 o, f3 d) {
+//   The stack lives in LDS (kLdsStack entries per thread, column layout: slot * kBlock + tid, so a
+// wave's pushes hit 64 distinct banks) when the tree is shallow enough that the reference's 64
+// entries are never reached (pt_create checks the depth: occupancy <= interior depth); deeper trees
+// use a 64-entry private array (scratch), which is the reference's exact overflow behaviour.
+constexpr int kLdsStack = 32;
+
+template <class Stack>
+__device__ __forceinline__ MeshHit bvh_walk(const SceneDev& S, f3 o, f3 d, bool cull, Stack stack) {
     MeshHit r{false, -1, -1, kFLT_MAX, 0.f, 0.f};
-    if (S.nnodes == 0) return r;
-    int stack[64];
     int top = 0, cur = 0;
     const bool neg[3] = {d.x < 0.0f, d.y < 0.0f, d.z < 0.0f};
     const f3 inv = F3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     for (;;) {
-        const DNode nd = S.nodes[cur];
-        if (aabb_hit(nd.bmin, nd.bmax, o, inv)) {
-            if (nd.sub_areas > 0) {
-                for (int k = 0; k < nd.sub_areas; ++k) {
-                    const DTri tr = S.tris[nd.first + k];
+        const v4f nlo = S.nodes[cur].lo, nhi = S.nodes[cur].hi;
+        const float bmin[3] = {nlo[0], nlo[1], nlo[2]}, bmax[3] = {nhi[0], nhi[1], nhi[2]};
+        const int meta = __float_as_int(nlo[3]), link = __float_as_int(nhi[3]);
+        float lo;
+        // extension (pt_flags.bvh_cull): a node entered beyond the best t (+1e-3 relative) is a miss
+        if (aabb_hit(bmin, bmax, o, inv, lo) && !(cull && lo > r.t * 1.001f + 1e-4f)) {
+            if (meta > 0) {   // leaf: `meta` triangles from `link`
+                for (int k = 0; k < meta; ++k) {
+                    const DTri tr = S.tris[link + k];
                     float bx, by, bz;
                     if (ray_tri(tr, o, d, bx, by, bz)) {
                         r.any = true;
-                        if (r.t == -1.0f || bz < r.t) { r.t = bz; r.bx = bx; r.by = by; r.id = tr.id; r.idx = nd.first + k; }
+                        if (r.t == -1.0f || bz < r.t) {
+                            r.t = bz; r.bx = bx; r.by = by; r.id = __float_as_int(tr.a[3]); r.idx = link + k;
+                        }
                     }
                 }
                 if (top == 0) break;
-                cur = stack[--top];
-            } else {
-                if (top == 64) { cur = stack[--top]; continue; }
-                if (neg[nd.axis]) { stack[top++] = cur + 1; cur = nd.rchild; }
-                else { stack[top++] = nd.rchild; cur = cur + 1; }
+                cur = stack.get(--top);
+            } else {          // interior: axis = -meta - 1, right child = link, left child = cur + 1
+                if (top == 64) { cur = stack.get(--top); continue; }
+                const int axis = -meta - 1;
+                const bool ng = axis == 0 ? neg[0] : (axis == 1 ? neg[1] : neg[2]);
+                if (ng) { stack.set(top++, cur + 1); cur = link; }
+                else { stack.set(top++, link); cur = cur + 1; }
             }
         } else {
             if (top == 0) break;
-            cur = stack[--top];
+            cur = stack.get(--top);
         }
     }
     return r;
+}
+
+struct LdsStack {
+    int* col;   // this thread's column of the block's stack
+    __device__ int get(int i) const { return col[i * kBlock]; }
+    __device__ void set(int i, int v) const { col[i * kBlock] = v; }
+};
+struct PrivStack {
+    int* a;
+    __device__ int get(int i) const { return a[i]; }
+    __device__ void set(int i, int v) const { a[i] = v; }
+};
+
+__device__ MeshHit bvh_traverse(const SceneDev& S, f3 o, f3 d, bool cull) {
+    if (S.nnodes == 0) return MeshHit{false, -1, -1, kFLT_MAX, 0.f, 0.f};
+    if (S.bvh_depth < kLdsStack) {
+        __shared__ int s_stack[kLdsStack * kBlock];
+        return bvh_walk(S, o, d, cull, LdsStack{s_stack + threadIdx.x});
+    }
+    int stack[64];
+    return bvh_walk(S, o, d, cull, PrivStack{stack});
 }
 
 // Triangle::intersect's attributes for the closest triangle (sceneStructs.h:151-154).
@@ -298,7 +338,7 @@ __device__ __forceinline__ Hit intersect_scene(const SceneDev& S, const FlagsDev
             t = sphere_test(g, ro, rd, obj, outside);
         } else if (MESH && type == PT_GEOM_MESH) {
             if (fl.bvh) {
-                if (!traversed) { mh = bvh_traverse(S, ro, rd); traversed = true; }
+                if (!traversed) { mh = bvh_traverse(S, ro, rd, fl.bvh_cull != 0); traversed = true; }
                 if (mh.any && mh.id >= g.tri_start && mh.id < g.tri_end) {
                     t = mh.t;
                     tri_attrs(S.attrs[mh.idx], mh.bx, mh.by, tmp_n, tmp_u, tmp_v);
@@ -939,6 +979,13 @@ void set_flags_dev(pt_ctx* c, const pt_flags& f) {
     c->args.fl.aperture = f.aperture;
     c->args.fl.focal = f.focal_dist;
     c->args.fl.single_albedo = f.single_albedo;
+    c->args.fl.bvh_cull = f.bvh_cull;
+}
+
+float bits_to_float(int32_t v) {
+    float f;
+    std::memcpy(&f, &v, 4);
+    return f;
 }
 
 Affine to_affine(const float* m) {   // glm column-major 4x4 -> 3x4 + the exact w=0 terms
@@ -1075,7 +1122,7 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
         (e = hipMemcpy(d_mats, S.materials.data(), S.materials.size() * sizeof(DMaterial), hipMemcpyHostToDevice)) != hipSuccess)
         return bail(pt::fail(PT_ERR_HIP, std::string("scene upload: ") + hipGetErrorString(e)));
     static_assert(sizeof(DMaterial) == sizeof(pt_material), "material layout");
-    static_assert(sizeof(DNode) == sizeof(pt_bvh_node), "bvh node layout");
+    static_assert(sizeof(DNode) == 32 && sizeof(DTri) == 48, "packed device layouts");
     A.S.geoms = d_geoms;
     A.S.mats = d_mats;
     A.S.ngeoms = (int)dg.size();
@@ -1086,11 +1133,13 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
         for (size_t i = 0; i < S.triangles.size(); ++i) {
             const pt_triangle& t = S.triangles[i];
             for (int k = 0; k < 3; ++k) {
-                tr[i].v0[k] = t.v[0][k];
-                tr[i].e1[k] = t.v[1][k] - t.v[0][k];
-                tr[i].e2[k] = t.v[2][k] - t.v[0][k];
+                tr[i].a[k] = t.v[0][k];
+                tr[i].b[k] = t.v[1][k] - t.v[0][k];
+                tr[i].c[k] = t.v[2][k] - t.v[0][k];
             }
-            tr[i].id = t.id;
+            int32_t id = t.id;
+            tr[i].a[3] = bits_to_float(id);
+            tr[i].b[3] = tr[i].c[3] = 0.0f;
             std::memcpy(at[i].n, t.n, sizeof at[i].n);
             std::memcpy(at[i].uv, t.uv, sizeof at[i].uv);
         }
@@ -1106,12 +1155,31 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
         A.S.ntris = (int)tr.size();
     }
     if (!S.bvh.empty()) {
+        std::vector<DNode> nodes(S.bvh.size());
+        for (size_t i = 0; i < S.bvh.size(); ++i) {
+            const pt_bvh_node& b = S.bvh[i];
+            const int32_t meta = b.sub_areas > 0 ? b.sub_areas : -(b.axis + 1);
+            const int32_t link = b.sub_areas > 0 ? b.first_area_idx : b.rchild_idx;
+            for (int k = 0; k < 3; ++k) { nodes[i].lo[k] = b.bmin[k]; nodes[i].hi[k] = b.bmax[k]; }
+            nodes[i].lo[3] = bits_to_float(meta);
+            nodes[i].hi[3] = bits_to_float(link);
+        }
         DNode* d_nodes;
-        if (int rc = c->alloc(&d_nodes, S.bvh.size())) return bail(rc);
-        if ((e = hipMemcpy(d_nodes, S.bvh.data(), S.bvh.size() * sizeof(DNode), hipMemcpyHostToDevice)) != hipSuccess)
+        if (int rc = c->alloc(&d_nodes, nodes.size())) return bail(rc);
+        if ((e = hipMemcpy(d_nodes, nodes.data(), nodes.size() * sizeof(DNode), hipMemcpyHostToDevice)) != hipSuccess)
             return bail(pt::fail(PT_ERR_HIP, std::string("bvh upload: ") + hipGetErrorString(e)));
         A.S.nodes = d_nodes;
         A.S.nnodes = (int)S.bvh.size();
+        std::vector<int32_t> depth(S.bvh.size(), 0);
+        int32_t deepest = 0;
+        for (size_t i = 0; i < S.bvh.size(); ++i)
+            if (S.bvh[i].sub_areas == 0) {
+                deepest = std::max(deepest, depth[i]);
+                if (i + 1 < depth.size()) depth[i + 1] = depth[i] + 1;
+                if (S.bvh[i].rchild_idx > 0 && (size_t)S.bvh[i].rchild_idx < depth.size())
+                    depth[(size_t)S.bvh[i].rchild_idx] = depth[i] + 1;
+            }
+        A.S.bvh_depth = deepest;
     }
     if (!S.textures.empty()) {
         std::vector<DTexture> tx(S.textures.size());

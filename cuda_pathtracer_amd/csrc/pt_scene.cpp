@@ -350,6 +350,7 @@ void pt_flags_default(pt_flags* f) {   // utilities.h:23-33
     f->ssaa = 1;
     f->dof = 1;
     f->single_albedo = 0;
+    f->bvh_cull = 0;
     f->aperture = 0.1f;
     f->focal_dist = 10.0f;
 }

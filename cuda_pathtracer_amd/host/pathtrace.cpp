@@ -32,6 +32,7 @@ pt_flags flags_of(const GuiDataContainer* g) {
         f.aperture = g->aperture;
         f.focal_dist = g->focal_len;
         f.single_albedo = g->singleAlbedo;
+        f.bvh_cull = g->bvhCull;
     }
     return f;
 }

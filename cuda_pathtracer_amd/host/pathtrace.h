@@ -31,6 +31,7 @@ public:
     float aperture{0.1f};
     float focal_len{10.0f};
     bool singleAlbedo{false};   // extension (include/pt_amd.h pt_flags.single_albedo)
+    bool bvhCull{false};        // extension (include/pt_amd.h pt_flags.bvh_cull)
 };
 
 struct vec3f {

@@ -41,6 +41,8 @@ class GuiDataContainer:
         self.focal_len = 10.0
         # extension, off = the reference: albedo applied once instead of twice (include/pt_amd.h)
         self.singleAlbedo = False
+        # extension, off = the reference: cull BVH nodes beyond the closest hit so far
+        self.bvhCull = False
 
     def to_c(self) -> N.Flags:
         f = N.Flags()
@@ -54,6 +56,7 @@ class GuiDataContainer:
         f.aperture = float(self.aperture)
         f.focal_dist = float(self.focal_len)
         f.single_albedo = int(bool(self.singleAlbedo))
+        f.bvh_cull = int(bool(self.bvhCull))
         return f
 
 

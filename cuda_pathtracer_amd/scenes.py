@@ -1,0 +1,128 @@
+"""Synthetic workload scenes in the reference's JSON scene format (BASELINE.json configs 3-5).
+
+Each generator writes a scene file (and, for meshes, an OBJ under Models/) into a directory and
+returns its path; generation is deterministic for a given seed.  The files use only the keys the
+reference loader reads (scene.cpp:33-219), plus the REFRACTIVE / IOR extension for config 4
+(the reference loader ignores those keys — SURVEY.md §2 quirk 1 — so refraction is parity-unpinned
+against the reference itself; the CPU oracle restates the build's refraction).
+
+  cornell_hd        config 3: cornell.json geometry, 1920x1080, DEPTH 16 (run with material sort on)
+  multi_object      config 4: Cornell-style room with a grid of spheres and boxes — diffuse,
+                    mirror and refractive materials — 3840x2160, DEPTH 8
+  random_triangles  config 5: N random triangles (one OBJ mesh through the BVH path) in a lit
+                    box, 3840x2160, DEPTH 32
+"""
+from __future__ import annotations
+
+import json
+from pathlib import Path
+
+import numpy as np
+
+_HERE = Path(__file__).resolve().parent
+
+CORNELL_MATERIALS = {
+    "light": {"TYPE": "Emitting", "RGB": [1.0, 1.0, 1.0], "EMITTANCE": 5.0},
+    "diffuse_white": {"TYPE": "Diffuse", "RGB": [0.98, 0.98, 0.98]},
+    "diffuse_red": {"TYPE": "Diffuse", "RGB": [0.85, 0.35, 0.35]},
+    "diffuse_green": {"TYPE": "Diffuse", "RGB": [0.35, 0.85, 0.35]},
+    "specular_white": {"TYPE": "Specular", "RGB": [0.98, 0.98, 0.98], "SPECRGB": [0.98, 0.98, 0.98],
+                       "REFLECTIVE": 1.0},
+}
+
+
+def _room(light_scale=(3.0, 0.3, 3.0)):
+    """The Cornell box shell of cornell.json: light, floor, ceiling, back, left, right walls."""
+    def cube(mat, t, r, s):
+        return {"TYPE": "cube", "MATERIAL": mat, "TRANS": list(t), "ROTAT": list(r), "SCALE": list(s)}
+    return [
+        cube("light", (0.0, 10.0, 0.0), (0, 0, 0), light_scale),
+        cube("diffuse_white", (0.0, 0.0, 0.0), (0, 0, 0), (10.0, 0.01, 10.0)),
+        cube("diffuse_white", (0.0, 10.0, 0.0), (0, 0, 90), (0.01, 10.0, 10.0)),
+        cube("diffuse_white", (0.0, 5.0, -5.0), (0, 90, 0), (0.01, 10.0, 10.0)),
+        cube("diffuse_red", (-5.0, 5.0, 0.0), (0, 0, 0), (0.01, 10.0, 10.0)),
+        cube("diffuse_green", (5.0, 5.0, 0.0), (0, 0, 0), (0.01, 10.0, 10.0)),
+    ]
+
+
+def _camera(res, depth, iterations, name):
+    return {"RES": list(res), "FOVY": 45.0, "ITERATIONS": iterations, "DEPTH": depth, "FILE": name,
+            "EYE": [0.0, 5.0, 10.5], "LOOKAT": [0.0, 5.0, 0.0], "UP": [0.0, 1.0, 0.0]}
+
+
+def _write(out_dir, name, scene) -> str:
+    out = Path(out_dir)
+    out.mkdir(parents=True, exist_ok=True)
+    path = out / f"{name}.json"
+    path.write_text(json.dumps(scene, indent=1))
+    return str(path)
+
+
+def cornell_hd(out_dir, res=(1920, 1080), depth=16) -> str:
+    """Config 3: the bundled Cornell scene at a different resolution and depth."""
+    scene = json.loads((_HERE.parent / "tests" / "scenes" / "cornell.json").read_text())
+    scene["Camera"]["RES"] = list(res)
+    scene["Camera"]["DEPTH"] = int(depth)
+    scene["Camera"]["FILE"] = "cornell_hd"
+    return _write(out_dir, "cornell_hd", scene)
+
+
+def multi_object(out_dir, res=(3840, 2160), depth=8, grid=(4, 3), seed=4) -> str:
+    """Config 4: spheres and boxes on a grid inside the box; materials cycle through diffuse,
+    mirror and glass (REFRACTIVE/IOR extension)."""
+    rng = np.random.default_rng(seed)
+    mats = dict(CORNELL_MATERIALS)
+    mats["glass"] = {"TYPE": "Refractive", "RGB": [0.98, 0.98, 0.98], "SPECRGB": [0.98, 0.98, 0.98],
+                     "REFRACTIVE": 1.0, "IOR": 1.5}
+    mats["mirror_gold"] = {"TYPE": "Specular", "RGB": [0.95, 0.8, 0.4], "SPECRGB": [0.95, 0.8, 0.4],
+                           "REFLECTIVE": 1.0}
+    mats["diffuse_blue"] = {"TYPE": "Diffuse", "RGB": [0.35, 0.35, 0.85]}
+    cycle = ["diffuse_blue", "glass", "specular_white", "mirror_gold", "diffuse_white", "glass"]
+    objs = _room()
+    nx, nz = grid
+    k = 0
+    for iz in range(nz):
+        for ix in range(nx):
+            x = -3.0 + 6.0 * ix / max(nx - 1, 1)
+            z = -2.5 + 4.0 * iz / max(nz - 1, 1)
+            size = float(rng.uniform(0.9, 1.6))
+            mat = cycle[k % len(cycle)]
+            if k % 2 == 0:
+                objs.append({"TYPE": "sphere", "MATERIAL": mat, "TRANS": [x, size / 2 + 0.01, z],
+                             "ROTAT": [0.0, 0.0, 0.0], "SCALE": [size, size, size]})
+            else:
+                objs.append({"TYPE": "cube", "MATERIAL": mat, "TRANS": [x, size / 2 + 0.01, z],
+                             "ROTAT": [0.0, float(rng.uniform(0, 90)), 0.0], "SCALE": [size, size, size]})
+            k += 1
+    scene = {"Materials": mats, "Camera": _camera(res, depth, 5000, "multi_object"), "Objects": objs}
+    return _write(out_dir, "multi_object", scene)
+
+
+def random_triangles(out_dir, n=100_000, res=(3840, 2160), depth=32, seed=5) -> str:
+    """Config 5: n random small triangles in the box volume as one OBJ mesh (BVH path)."""
+    rng = np.random.default_rng(seed)
+    out = Path(out_dir)
+    (out / "Models").mkdir(parents=True, exist_ok=True)
+    centers = rng.uniform((-4.0, 0.5, -4.0), (4.0, 8.5, 2.0), size=(n, 3))
+    verts = centers[:, None, :] + rng.normal(0.0, 0.12, size=(n, 3, 3))
+    normals = np.cross(verts[:, 1] - verts[:, 0], verts[:, 2] - verts[:, 0])
+    normals /= np.maximum(np.linalg.norm(normals, axis=1, keepdims=True), 1e-12)
+    lines = ["# random triangles (cuda_pathtracer_amd.scenes.random_triangles)"]
+    lines += [f"v {x:.6f} {y:.6f} {z:.6f}" for x, y, z in verts.reshape(-1, 3)]
+    lines += [f"vn {x:.6f} {y:.6f} {z:.6f}" for x, y, z in normals]
+    lines += [f"f {3 * i + 1}//{i + 1} {3 * i + 2}//{i + 1} {3 * i + 3}//{i + 1}" for i in range(n)]
+    name = f"tri{n}"
+    (out / "Models" / f"{name}.obj").write_text("\n".join(lines) + "\n")
+    objs = _room(light_scale=(4.0, 0.3, 4.0))
+    objs.append({"TYPE": "mesh", "MATERIAL": "diffuse_white", "OBJ_FILE": f"{name}.obj",
+                 "TRANS": [0.0, 0.0, 0.0], "ROTAT": [0.0, 0.0, 0.0], "SCALE": [1.0, 1.0, 1.0]})
+    scene = {"Materials": dict(CORNELL_MATERIALS), "Camera": _camera(res, depth, 5000, name), "Objects": objs}
+    return _write(out_dir, name, scene)
+
+
+CONFIGS = {
+    "cornell": None,   # the bundled scene itself (configs[1])
+    "cornell_hd_sorted": cornell_hd,
+    "multi_object_4k": multi_object,
+    "random_triangles_100k": random_triangles,
+}

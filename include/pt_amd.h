@@ -59,6 +59,12 @@ typedef struct pt_flags {
      * multiplies the path colour by the albedo at interactions.cu:60 AND :83; its own course
      * image (img/REFERENCE_cornell.5000samp.png) matches the single-albedo model. */
     int32_t single_albedo;
+    /* Extension (default 0 = the reference): skip BVH nodes whose entry distance exceeds the
+     * closest triangle found so far by a 1e-3 relative margin.  BVHIntersectionTest
+     * (intersections.cu:170-224) visits every node the ray line crosses.  The closest hit is
+     * unchanged unless rounding moves a triangle's computed t by more than the margin
+     * (DESIGN.md §4). */
+    int32_t bvh_cull;
 } pt_flags;
 
 /* Material (sceneStructs.h:43-57), 48 bytes. */

@@ -163,3 +163,12 @@ def test_missing_obj_is_an_error(tmp_path):
     (tmp_path / "m.json").write_text(json.dumps(scene))
     with pytest.raises(N.PtError, match="OBJ"):
         P.Scene(tmp_path / "m.json")
+
+
+def test_random_triangles_100k_bvh_matches_oracle(tmp_path):
+    """Config 5's scene at full size: 100k triangles, product BVH == oracle BVH byte for byte."""
+    from cuda_pathtracer_amd import scenes
+    path = scenes.random_triangles(tmp_path, n=100_000)
+    s, o, pt, pn = _assert_same(path)
+    assert len(pt) == 100_000
+    assert int(pn[pn["sub_areas"] > 0]["sub_areas"].sum()) == 100_000

@@ -244,6 +244,7 @@ def _room_pair(room_path, res=(40, 40)):
     dict(useBVHtree=False, useBBox=False),        # linear mesh loop, no cull
     dict(sortbyMaterial=True),
     dict(singleAlbedo=True, russianRoulette=False),
+    dict(bvhCull=True),                           # extension: same image, fewer node visits
 ])
 def test_room_meshes_textures_bitexact(room_path, kw):
     """room.json: three chairs (OBJ, fan-triangulated quads/octagons) + a textured wall mesh, one
@@ -253,3 +254,31 @@ def test_room_meshes_textures_bitexact(room_path, kw):
     g, r, st, live = _run(s, o, _gui(**kw), iters=2)
     _assert_bitexact(g, r, f"room {kw}")
     assert live[0] == 2 * 40 * 40 and r.sum() > 0
+
+
+@pytest.fixture(scope="module")
+def config_scenes(tmp_path_factory):
+    """BASELINE.json configs 3-5 generated at parity-test sizes (cuda_pathtracer_amd.scenes)."""
+    from cuda_pathtracer_amd import scenes
+    d = tmp_path_factory.mktemp("configs")
+    return {
+        "cornell_hd": scenes.cornell_hd(d, res=(96, 54), depth=16),
+        "multi_object": scenes.multi_object(d, res=(64, 36), depth=8),
+        "random_triangles": scenes.random_triangles(d, n=3000, res=(48, 27), depth=32),
+    }
+
+
+@pytest.mark.parametrize("name,kw", [
+    ("cornell_hd", dict(sortbyMaterial=True)),            # config 3: DEPTH 16, material-sorted shading
+    ("multi_object", dict()),                             # config 4: diffuse + mirror + glass
+    ("multi_object", dict(sortbyMaterial=True, SSAA=False)),
+    ("random_triangles", dict()),                         # config 5: BVH over random triangles, DEPTH 32
+    ("random_triangles", dict(useBVHtree=False)),
+    ("random_triangles", dict(bvhCull=True)),
+])
+def test_config_scenes_bitexact(config_scenes, name, kw):
+    from cuda_pathtracer_amd import Scene
+    path = config_scenes[name]
+    g, r, st, live = _run(Scene(path), O.OracleScene.from_json(path), _gui(**kw), iters=2)
+    _assert_bitexact(g, r, f"{name} {kw}")
+    assert r.sum() > 0
