@@ -2,8 +2,11 @@
 
 Workload (BASELINE.json configs[1]): path_tracer/scenes/cornell.json as-is — 800x800, DEPTH 8,
 default flags.  A step is one render pass.  On N GPUs (one process per GPU, torchrun) rank r owns
-the image rows y % N == r and traces N samples per pixel per pass (spp = N), so every GPU traces
-800*800 camera paths per step (weak scaling; N = 1 is exactly the reference's pathtrace()).
+the image rows y % N == r; a pass traces `--spp` (default 4) iterations of those rows per GPU
+share, i.e. spp*N samples per pixel of the rank's rows, so every GPU traces spp*800*800 camera
+paths per step (weak scaling).  Batching iterations into one pass is bit-identical to tracing
+them one pass at a time (tests/test_render_gpu.py::test_tiles_and_batched_samples); it fills the
+GPU during the short tail bounces.  --spp 1 is exactly the reference's pathtrace() per step.
 After the timed passes the float tiles are gathered to rank 0 with one RCCL gather (inside the
 timed region).  value = all ranks' traced segments / max-over-ranks wall time / 1e6.
 
@@ -125,6 +128,9 @@ def main() -> None:
                     help="BASELINE.json workload: cornell (configs[1], the default line) or configs 3-5 "
                          "generated by cuda_pathtracer_amd.scenes")
     ap.add_argument("--bvh-cull", action="store_true", help="pt_flags.bvh_cull extension (mesh scenes)")
+    ap.add_argument("--spp", type=int, default=4,
+                    help="iterations traced together per pass and GPU (a pass covers spp x N iterations of "
+                         "the rank's rows; results are bit-identical to one iteration per pass)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -169,7 +175,7 @@ def main() -> None:
     gui.bvhCull = bool(args.bvh_cull)
     scene = P.Scene(scene_path)
     st_r = scene.state()
-    spp = world
+    spp = world * max(1, args.spp)
     pt = P.PathTracer(scene, gui, rank=rank, world=world, spp=spp)
     stream = torch.cuda.current_stream()
     _log(rank, f"[bench] tile rows={pt.rows} npix={pt.npix} paths/pass={pt.npaths} depth={st_r.traceDepth}")
@@ -265,8 +271,10 @@ def main() -> None:
             "dtype": "f32",
             "data": "synthetic (bundled cornell.json scene; camera rays generated on device)" if workload is None
                     else "synthetic (generated scene, cuda_pathtracer_amd/scenes.py; camera rays generated on device)",
-            "config": {"workload": workload or ("cornell.json 800x800 DEPTH 8 default flags; per GPU 640000 camera "
-                                                "paths per step (rows y%N==rank, N spp per pass); fused bounce kernel"),
+            "config": {"workload": workload or (f"cornell.json 800x800 DEPTH 8 default flags; a step = one render pass "
+                                                f"of {max(1, args.spp)} iteration(s) per GPU-share (rows y%N==rank, "
+                                                f"{max(1, args.spp)}*N samples per pixel of those rows; bit-identical "
+                                                f"to one iteration per pass); fused bounce kernel"),
                        "scene": Path(scene_path).name, "resolution": list(scene.camera().res), "depth": depth,
                        "spp_per_step": spp, "paths_per_gpu_per_step": pt.npaths,
                        "parallelism": f"pixel-tile x{world} + RCCL gather"},

@@ -575,6 +575,7 @@ __device__ __forceinline__ void count_bounce(const KArgs& A, int N) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         atomicAdd(&A.stats->bounce_live[A.bounce], (unsigned long long)N);
         atomicAdd(&A.stats->segments, (unsigned long long)N);
+        if (A.bounce == 0) atomicAdd(&A.stats->passes, 1ull);   // (no separate ~4 us launch per pass)
     }
 }
 __device__ __forceinline__ void store_survivor(const PathSoA& B, int i, const PathReg& p, bool with_slot) {
@@ -898,7 +899,6 @@ __global__ void k_finalize_spp(float* __restrict__ image, const float* __restric
     }
 }
 
-__global__ void k_stats_pass(DevStats* st) { atomicAdd(&st->passes, 1ull); }
 
 // sendImageToPBO (pathtrace.cu:64-86)
 __global__ void k_preview(const float* __restrict__ image, uint8_t* __restrict__ rgba, int npix, int iter) {
@@ -1348,8 +1348,6 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
                            (const float*)A.colbuf, npix, A.tile.spp);
         HIP_TRY(hipGetLastError());
     }
-    hipLaunchKernelGGL(k_stats_pass, dim3(1), dim3(1), 0, st, c->stats);
-    HIP_TRY(hipGetLastError());
     return PT_OK;
 }
 

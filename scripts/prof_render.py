@@ -1,4 +1,5 @@
-"""Render-only workload for rocprofv3 (no torch kernels, no scan): N passes of cornell 800x800."""
+"""Render-only workload for rocprofv3 (no torch kernels, no scan): N passes of cornell 800x800,
+`spp=K` iterations per pass (default 4, like bench.py)."""
 import sys
 from pathlib import Path
 ROOT = Path(__file__).resolve().parent.parent
@@ -8,13 +9,14 @@ os.environ.setdefault("PT_AMD_NO_TORCH", "1")
 import cuda_pathtracer_amd as P
 
 passes = int(sys.argv[1]) if len(sys.argv) > 1 else 20
-sort = len(sys.argv) > 2 and sys.argv[2] == "sort"
+sort = "sort" in sys.argv[2:]
+spp = next((int(a[4:]) for a in sys.argv[2:] if a.startswith("spp=")), 4)   # bench.py's default batch
 s = P.Scene(str(ROOT / "tests" / "scenes" / "cornell.json"))
 g = P.GuiDataContainer()
 g.sortbyMaterial = sort
-pt = P.PathTracer(s, g)
-for it in range(1, passes + 1):
-    pt.render_pass(it)
+pt = P.PathTracer(s, g, spp=spp)
+for k in range(passes):
+    pt.render_pass(1 + k * spp)
 st = pt.stats()
 print(st["segments"], st["bounce_live"])
 pt.free()
