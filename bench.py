@@ -140,12 +140,21 @@ def main() -> None:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
 
     import torch
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # One process per GPU.  PT_BENCH_REHEARSAL=1 lets several ranks share the visible GPUs
+    # (device = local_rank % count) and uses gloo for the collectives: a functional rehearsal of
+    # the N > 1 path on a 1-GPU box, never a measurement.
+    rehearsal = os.environ.get("PT_BENCH_REHEARSAL", "0") == "1"
+    ndev = torch.cuda.device_count()
+    dev_index = local_rank % ndev if rehearsal else local_rank
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if rehearsal:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     def barrier():
         if dist is not None:

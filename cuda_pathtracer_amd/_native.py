@@ -29,7 +29,7 @@ class Flags(C.Structure):
     _fields_ = [("russian_roulette", C.c_int32), ("use_bvh", C.c_int32), ("use_bbox", C.c_int32),
                 ("sort_by_material", C.c_int32), ("use_thrust_partition", C.c_int32), ("ssaa", C.c_int32),
                 ("dof", C.c_int32), ("aperture", C.c_float), ("focal_dist", C.c_float),
-                ("single_albedo", C.c_int32), ("bvh_cull", C.c_int32)]
+                ("single_albedo", C.c_int32), ("bvh_cull", C.c_int32), ("shared_gpu", C.c_int32)]
 
 
 class Material(C.Structure):
@@ -92,6 +92,7 @@ SIGNATURES = {
     "sc_efficient_scan": (_I, [C.c_int, _P, _P]),
     "sc_efficient_compact": (_I, [C.c_int, _P, _P, _IP]),
     "sc_timer_gpu_ms": (C.c_float, []),
+    "sc_set_tile_schedule": (_I, [_I]),
     # pt_amd.h
     "pt_last_error": (C.c_char_p, []),
     "pt_flags_default": (None, [C.POINTER(Flags)]),

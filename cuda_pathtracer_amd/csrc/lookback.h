@@ -6,16 +6,13 @@
 // tile AGGREGATE, later the INCLUSIVE prefix.  A successor's wave 0 reads 4 x 64 predecessors
 // per round trip with relaxed agent-scope loads and stops at the nearest inclusive prefix.
 //
-// Tile assignment is STATIC and persistent: a grid of G co-resident workgroups, workgroup b
-// owns tiles b, b+G, b+2G, ... and processes them in increasing order.  There is no ticket
-// counter (a single returning atomic saturates at ~88 dequeues/us on MI355X, which made the
-// ticket the bottleneck).  Forward progress: the lowest unpublished tile's predecessors are all
-// published and its workgroup is resident (G <= resident capacity, see grid_for()), so it
-// completes.  Every spin is still bounded; on timeout the tile proceeds and raises *err
-// (results then wrong, but the kernel always drains — a hung wave would take the GPU down).
+// Tile assignment: TileSeq below (static co-resident grid, or tiles claimed from a ticket for
+// shared GPUs).  Every spin is bounded; on timeout the tile proceeds and raises *err (results
+// then wrong and reported, but the kernel always drains — a hung wave would take the GPU down).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <climits>
 
 namespace lb {
 
@@ -111,6 +108,79 @@ template <int WINDOWS = kWindows>
 __device__ __forceinline__ uint32_t lookback(uint64_t* st, int tile, int lane, uint32_t* err) {
     uint64_t w[WINDOWS];
     return lookback_impl<WINDOWS, false>(st, tile, lane, err, w);
+}
+
+// ---- tile schedules ------------------------------------------------------------------------
+// STATIC (default, fastest): a grid of G workgroups that must all be resident at once (sized by
+// the host from the occupancy with headroom); workgroup b owns tiles b, b+G, b+2G, ...  No
+// atomics.  If part of the grid cannot become resident — another kernel or process holding the
+// GPU — the look-back stalls, hits its spin bound and the launch reports an error (it never
+// hangs).
+// CLAIMED (shared GPUs): each tile is claimed from a ticket on its own, so claim order == tile
+// order: every predecessor of a claimed tile was claimed earlier by a running workgroup and the
+// lowest unfinished tile always progresses, whatever else runs on the GPU.  A workgroup claims
+// kAhead steps ahead, so the claim's round trip overlaps its current work and consecutive tiles
+// go to different workgroups (contiguous multi-tile claims would chain each chunk's first
+// look-back to the previous chunk's last tile — measured 100x slower).  The cost is one
+// device-scope atomic per tile on one address, which saturates at ~88/us on MI355X: about 2x
+// slower bounce kernels at 256-path tiles, ~15% slower scans.
+//   Claimed mode plumbing: the claim returned at step k is written to the LDS ring at the END of
+// step k (so the wave does not stall on the atomic) and read at the top of step k + 2, after step
+// k + 1's barriers; the caller's per-step work must contain a workgroup barrier.
+constexpr int kAhead = 3;   // claims in flight: next, next + 1, next + 2
+constexpr int kRing = 4;
+
+struct TileSeq {
+    int tile;      // current tile (INT_MAX: done)
+    int next;      // the tile after it (INT_MAX: none)
+    int k;         // step index (ring position)
+    int limit;
+    bool claimed;
+    uint32_t pending;   // thread 0: claim issued this step, stored at seq_advance
+};
+
+// Block-wide start (contains a barrier in claimed mode).
+__device__ __forceinline__ TileSeq seq_start(bool claimed, uint32_t* ticket, int* s_ring, int limit) {
+    TileSeq q;
+    q.k = 0;
+    q.limit = limit;
+    q.claimed = claimed;
+    q.pending = 0;
+    if (!claimed) {
+        q.tile = (int)blockIdx.x < limit ? (int)blockIdx.x : INT_MAX;
+        const int n = (int)blockIdx.x + (int)gridDim.x;
+        q.next = n < limit ? n : INT_MAX;
+        return q;
+    }
+    if (threadIdx.x == 0)
+        for (int i = 0; i < kAhead; ++i) s_ring[i] = (int)atomicAdd(ticket, 1u);
+    __syncthreads();
+    q.tile = s_ring[0] < limit ? s_ring[0] : INT_MAX;
+    q.next = s_ring[1] < limit ? s_ring[1] : INT_MAX;
+    return q;
+}
+
+// Top of a step: claimed mode, thread 0 claims the tile for step k + kAhead (kept in a register).
+__device__ __forceinline__ void seq_step(TileSeq& q, uint32_t* ticket) {
+    if (q.claimed && q.next != INT_MAX && threadIdx.x == 0) q.pending = atomicAdd(ticket, 1u);
+}
+
+// Bottom of a step: publish the claim, then move on.
+__device__ __forceinline__ void seq_advance(TileSeq& q, int* s_ring) {
+    if (q.tile == INT_MAX) return;
+    if (!q.claimed) {
+        q.tile = q.next;
+        if (q.tile == INT_MAX) return;
+        const int n = q.tile + (int)gridDim.x;
+        q.next = n < q.limit ? n : INT_MAX;
+        return;
+    }
+    if (threadIdx.x == 0) s_ring[(q.k + kAhead) % kRing] = q.next != INT_MAX ? (int)q.pending : INT_MAX;
+    ++q.k;
+    q.tile = q.next;
+    if (q.tile == INT_MAX) return;
+    const int c = s_ring[(q.k + 1) % kRing];   // claimed at step k - 1, published before its barriers
+    q.next = c < q.limit ? c : INT_MAX;
 }
 
 }  // namespace lb

@@ -71,6 +71,7 @@ struct FlagsDev {
     float aperture, focal;
     int32_t single_albedo;
     int32_t bvh_cull;
+    int32_t claimed;   // tile schedule (lookback.h TileSeq)
 };
 struct TileDev {
     int32_t W, rank, world, npix, spp, P, depth, iter_first;
@@ -664,26 +665,34 @@ __device__ __forceinline__ int compact_tile(const KArgs& A, int tile, int num_ti
     return (int)(*s_excl + before + rank);
 }
 
-// [raygen] -> intersect -> shade -> stable compaction, persistent co-resident grid with static
-// tile assignment (lookback.h).  Survivors go straight to their final position in A.out.
+// [raygen] -> intersect -> shade -> stable compaction over claimed tiles (lookback.h TileSeq: no
+// co-residency needed).  Survivors go straight to their final position in A.out.
 template <bool FIRST, bool SPP1, bool MESH>
 __global__ __launch_bounds__(kBlock) void k_bounce(const KArgs A) {
     __shared__ DMaterial s_mats[kLdsMats];
     __shared__ uint32_t s_wc[4];
     __shared__ uint32_t s_excl, s_cnt;
+    __shared__ int s_ring[lb::kRing];
     {   // zero the look-back words the next launch (other parity) will use
         uint64_t* nst = A.status + (size_t)(A.parity ^ 1) * A.max_tiles;
         for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < A.max_tiles; j += gridDim.x * blockDim.x) nst[j] = 0ull;
     }
     const int N = live_count(A);
     const int num_tiles = (N + kBlock - 1) / kBlock;
-    if (num_tiles == 0 && blockIdx.x == 0 && threadIdx.x == 0) A.ctl[A.parity ^ 1].live = 0u;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        A.ctl[A.parity ^ 1].ticket = 0u;   // the next look-back launch claims from zero
+        if (num_tiles == 0) A.ctl[A.parity ^ 1].live = 0u;
+    }
+    // workgroups beyond the tile count would only burn ticket atomics (tail bounces are small)
     if ((int)blockIdx.x >= num_tiles) return;
     stage_materials(A, s_mats);
     const bool lds_mats = A.S.nmats <= kLdsMats;
     count_bounce(A, N);
     uint32_t emit_cnt = 0;
-    for (int tile = blockIdx.x; tile < num_tiles; tile += gridDim.x) {
+    lb::TileSeq q = lb::seq_start(A.fl.claimed != 0, &A.ctl[A.parity].ticket, s_ring, num_tiles);
+    while (q.tile != INT_MAX) {
+        lb::seq_step(q, &A.ctl[A.parity].ticket);
+        const int tile = q.tile;
         const int i = tile * kBlock + (int)threadIdx.x;
         bool alive = false, emitted = false;
         PathReg p;
@@ -702,6 +711,7 @@ __global__ __launch_bounds__(kBlock) void k_bounce(const KArgs A) {
         emit_cnt += (uint32_t)__popcll(__ballot(emitted));
         const int pos = compact_tile(A, tile, num_tiles, alive, s_wc, &s_excl);
         if (alive) store_path(A.out, pos, p);
+        lb::seq_advance(q, s_ring);
     }
     flush_emissive(A, emit_cnt, &s_cnt);
 }
@@ -724,6 +734,7 @@ __device__ __forceinline__ void copy_path(const PathSoA& S, const PathSoA& D, in
 __global__ __launch_bounds__(kBlock) void k_compact_paths(const KArgs A) {
     __shared__ uint32_t s_wc[kCompactPer][4];
     __shared__ uint32_t s_excl;
+    __shared__ int s_ring[lb::kRing];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int q = A.parity, nq = q ^ 1;
     uint64_t* st = A.status + (size_t)q * A.max_tiles;
@@ -733,8 +744,15 @@ __global__ __launch_bounds__(kBlock) void k_compact_paths(const KArgs A) {
     }
     const int N = live_count(A);
     const int num_tiles = (N + kCompactTile - 1) / kCompactTile;
-    if (num_tiles == 0 && blockIdx.x == 0 && tid == 0) A.ctl[nq].live = 0u;
-    for (int tile = blockIdx.x; tile < num_tiles; tile += gridDim.x) {
+    if (blockIdx.x == 0 && tid == 0) {
+        A.ctl[nq].ticket = 0u;   // the next look-back launch claims from zero
+        if (num_tiles == 0) A.ctl[nq].live = 0u;
+    }
+    if ((int)blockIdx.x >= num_tiles) return;
+    lb::TileSeq sq = lb::seq_start(A.fl.claimed != 0, &A.ctl[q].ticket, s_ring, num_tiles);
+    while (sq.tile != INT_MAX) {
+        lb::seq_step(sq, &A.ctl[q].ticket);
+        const int tile = sq.tile;
         bool f[kCompactPer];
         uint32_t rank[kCompactPer];
         uint64_t m[kCompactPer];
@@ -764,9 +782,7 @@ __global__ __launch_bounds__(kBlock) void k_compact_paths(const KArgs A) {
         const uint32_t total = run;
         if (wave == 0) {
             uint32_t excl = 0;
-            if (A.experiment & 1) {
-                excl = (uint32_t)(tile * kCompactTile);   // ablation: positions wrong, timing only
-            } else if (tile == 0) {
+            if (tile == 0) {
                 if (lane == 0) lb::publish(st, 0, lb::kFlagPre, total);
             } else {
                 if (lane == 0) lb::publish(st, tile, lb::kFlagAgg, total);
@@ -783,6 +799,7 @@ __global__ __launch_bounds__(kBlock) void k_compact_paths(const KArgs A) {
 #pragma unroll
         for (int k = 0; k < kCompactPer; ++k)
             if (f[k]) copy_path(A.in, A.out, tile * kCompactTile + k * kBlock + tid, (int)(excl + off[k] + rank[k]));
+        lb::seq_advance(sq, s_ring);
     }
 }
 
@@ -937,7 +954,7 @@ struct pt_ctx {
     KArgs args{};
     int max_tiles = 0, max_t64 = 0;
     int grid_trace = 0, grid_compact = 0;
-    int grid_bounce[8] = {};   // per k_bounce variant (first, spp1, mesh): its co-resident grid
+    int grid_bounce[8] = {};   // per k_bounce variant (first, spp1, mesh): one wave of resident workgroups
     bool fused = true;   // pipeline: fused bounce kernel (default) or trace + compact
     uint64_t compact_launches = 0;   // parity of the look-back status / live-count words
     // owned device allocations
@@ -980,6 +997,7 @@ void set_flags_dev(pt_ctx* c, const pt_flags& f) {
     c->args.fl.focal = f.focal_dist;
     c->args.fl.single_albedo = f.single_albedo;
     c->args.fl.bvh_cull = f.bvh_cull;
+    c->args.fl.claimed = f.shared_gpu;
 }
 
 float bits_to_float(int32_t v) {

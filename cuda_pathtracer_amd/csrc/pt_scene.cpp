@@ -5,6 +5,7 @@
 // renders from exactly the numbers the reference host would have produced.
 #include <cfloat>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <sstream>
@@ -351,6 +352,8 @@ void pt_flags_default(pt_flags* f) {   // utilities.h:23-33
     f->dof = 1;
     f->single_albedo = 0;
     f->bvh_cull = 0;
+    const char* sched = std::getenv("PT_AMD_SCHEDULE");
+    f->shared_gpu = sched && std::strcmp(sched, "claim") == 0;
     f->aperture = 0.1f;
     f->focal_dist = 10.0f;
 }

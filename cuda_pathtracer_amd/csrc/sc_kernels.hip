@@ -17,6 +17,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <climits>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -31,11 +33,18 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kChunks = 8;                       // int4 chunks per thread
 constexpr int kTile = kThreads * kChunks * 4;    // 8192 elements (32 KiB)
-constexpr size_t kCtlBytes = 256;                // [0] unused, [1] device error word (padded)
+constexpr size_t kCtlBytes = 256;                // [1] device error word, [2] tile ticket (padded)
 constexpr int kLagWindows = 4;                   // look-back predecessors per round trip: 4 x 64
+constexpr int kTicket = 2;                       // ctl word of the tile ticket
 
 thread_local std::string g_err;
 thread_local float g_timer_ms = 0.f;
+// Tile schedule (lookback.h TileSeq): static co-resident grid, or claimed tiles for shared GPUs.
+// Default from PT_AMD_SCHEDULE=claim|static; sc_set_tile_schedule() overrides.
+std::atomic<bool> g_schedule_claimed{[] {
+    const char* v = std::getenv("PT_AMD_SCHEDULE");
+    return v && std::strcmp(v, "claim") == 0;
+}()};
 
 int fail(int code, const std::string& msg) { g_err = msg; return code; }
 int hip_fail(hipError_t e, const char* where) {
@@ -176,22 +185,6 @@ __device__ __forceinline__ void process_tile(const v4i (&cur)[kChunks], int tile
     if (MODE != kScan && tid == 0 && tile == num_tiles - 1) *d_count = (int64_t)(excl + total);
 }
 
-// Unaligned pointers: persistent static tiles with guarded scalar loads.
-template <int MODE>
-__global__ __launch_bounds__(kThreads) void k_scan_tiles(const int32_t* __restrict__ in, int32_t* __restrict__ out,
-                                                         int64_t n, uint64_t* __restrict__ status,
-                                                         uint32_t* __restrict__ ctl, int64_t* __restrict__ d_count,
-                                                         int32_t* __restrict__ dead) {
-    __shared__ uint32_t s_wsum[kChunks][4];
-    __shared__ uint32_t s_excl;
-    const int num_tiles = (int)((n + kTile - 1) / kTile);
-    for (int tile = blockIdx.x; tile < num_tiles; tile += gridDim.x) {
-        v4i cur[kChunks];
-        load_guarded(in, n, (int64_t)tile * kTile, threadIdx.x, cur);
-        process_tile<MODE>(cur, tile, num_tiles, n, out, status, ctl, d_count, dead, s_wsum, &s_excl);
-    }
-}
-
 // ---- lagged look-back -----------------------------------------------------------------------
 // Measured on MI355X (profiles/r01_scan_ab.txt): resolving each tile's prefix right after
 // reducing it put the look-back round trip on every iteration's critical path (0.69 ms for 2^28
@@ -250,19 +243,18 @@ __device__ __forceinline__ void lag_store(const LagTile& L, int par, const int32
     if (MODE != kScan && tid == 0 && L.tile == num_tiles - 1) *d_count = (int64_t)(excl + L.total);
 }
 
-// One step: prefetch tile+G into `pf`, reduce `cur` (= tile), resolve + write the deferred tile.
+// One step: prefetch `next` into `pf`, reduce `cur` (= tile), resolve + write the deferred tile.
 template <int MODE>
 __device__ __forceinline__ void lag_step(const int32_t* __restrict__ in, const v4i (&cur)[kChunks],
-                                         v4i (&pf)[kChunks], int tile, int G, int num_full, int num_tiles, int par,
-                                         LagTile& prev, bool& have_prev, int32_t (*s_data)[kTile],
+                                         v4i (&pf)[kChunks], int tile, int next, int num_full, int num_tiles,
+                                         int par, LagTile& prev, bool& have_prev, int32_t (*s_data)[kTile],
                                          uint32_t (*s_wsum)[kChunks][4], uint32_t* s_excl,
                                          int32_t* __restrict__ out, uint64_t* __restrict__ status,
                                          uint32_t* __restrict__ ctl, int64_t* __restrict__ d_count,
                                          int32_t* __restrict__ dead) {
-    const int t1 = tile + G;
     // unconditional (clamped) prefetch: a branch here would make the wait-count pass merge
     // "issued"/"skipped" states and drain the prefetch at the first use of the other buffer
-    load_full(in, (int64_t)(t1 < num_full ? t1 : tile) * kTile, (int)threadIdx.x, pf);
+    load_full(in, (int64_t)(next < num_full ? next : tile) * kTile, (int)threadIdx.x, pf);
     LagTile L;
     lag_reduce<MODE>(cur, tile, par, s_data, s_wsum, status, L);
     if (have_prev) {
@@ -274,50 +266,73 @@ __device__ __forceinline__ void lag_step(const int32_t* __restrict__ in, const v
     have_prev = true;
 }
 
-// 16-byte aligned pointers: persistent co-resident grid, static tiles b, b+G, b+2G, ...
+// Unaligned pointers: claimed tiles (above) with guarded scalar loads, prefix resolved at once.
+template <int MODE>
+__global__ __launch_bounds__(kThreads) void k_scan_tiles(const int32_t* __restrict__ in, int32_t* __restrict__ out,
+                                                         int64_t n, uint64_t* __restrict__ status,
+                                                         uint32_t* __restrict__ ctl, int64_t* __restrict__ d_count,
+                                                         int32_t* __restrict__ dead, int claimed) {
+    __shared__ uint32_t s_wsum[kChunks][4];
+    __shared__ uint32_t s_excl;
+    __shared__ int s_ring[lb::kRing];
+    const int num_tiles = (int)((n + kTile - 1) / kTile);
+    lb::TileSeq q = lb::seq_start(claimed != 0, &ctl[kTicket], s_ring, num_tiles);
+    while (q.tile != INT_MAX) {
+        lb::seq_step(q, &ctl[kTicket]);
+        v4i cur[kChunks];
+        load_guarded(in, n, (int64_t)q.tile * kTile, threadIdx.x, cur);
+        process_tile<MODE>(cur, q.tile, num_tiles, n, out, status, ctl, d_count, dead, s_wsum, &s_excl);
+        lb::seq_advance(q, s_ring);
+    }
+}
+
+// 16-byte aligned pointers: tiles claimed in chunks (above), each tile's prefix resolved by
+// look-back one step late.
 template <int MODE>
 __global__ __launch_bounds__(kThreads) void k_scan_lag(const int32_t* __restrict__ in, int32_t* __restrict__ out,
                                                        int64_t n, uint64_t* __restrict__ status,
                                                        uint32_t* __restrict__ ctl, int64_t* __restrict__ d_count,
-                                                       int32_t* __restrict__ dead) {
+                                                       int32_t* __restrict__ dead, int claimed) {
     __shared__ __attribute__((aligned(16))) int32_t s_data[2][kTile];
     __shared__ uint32_t s_wsum[2][kChunks][4];
     __shared__ uint32_t s_excl;
+    __shared__ int s_ring[lb::kRing];
     const int tid = threadIdx.x;
-    const int G = (int)gridDim.x;
     const int num_tiles = (int)((n + kTile - 1) / kTile);
     const int num_full = (int)(n / kTile);
-    int tile = blockIdx.x;
-    if (tile < num_full) {
+    lb::TileSeq q = lb::seq_start(claimed != 0, &ctl[kTicket], s_ring, num_tiles);
+    if (q.tile < num_full) {
         // two named register buffers, loop unrolled by two: no load destination is ever copied,
         // so the wait-count pass keeps each prefetch in flight across the other buffer's step
         v4i bA[kChunks], bB[kChunks];
         LagTile prev;
         bool have_prev = false;
         int par = 0;
-        load_full(in, (int64_t)tile * kTile, tid, bA);
+        load_full(in, (int64_t)q.tile * kTile, tid, bA);
         for (;;) {
-            lag_step<MODE>(in, bA, bB, tile, G, num_full, num_tiles, par, prev, have_prev, s_data, s_wsum, &s_excl,
-                           out, status, ctl, d_count, dead);
-            tile += G;
+            lb::seq_step(q, &ctl[kTicket]);
+            lag_step<MODE>(in, bA, bB, q.tile, q.next, num_full, num_tiles, par, prev, have_prev, s_data, s_wsum,
+                           &s_excl, out, status, ctl, d_count, dead);
+            lb::seq_advance(q, s_ring);
             par ^= 1;
-            if (tile >= num_full) break;
-            lag_step<MODE>(in, bB, bA, tile, G, num_full, num_tiles, par, prev, have_prev, s_data, s_wsum, &s_excl,
-                           out, status, ctl, d_count, dead);
-            tile += G;
+            if (q.tile >= num_full) break;
+            lb::seq_step(q, &ctl[kTicket]);
+            lag_step<MODE>(in, bB, bA, q.tile, q.next, num_full, num_tiles, par, prev, have_prev, s_data, s_wsum,
+                           &s_excl, out, status, ctl, d_count, dead);
+            lb::seq_advance(q, s_ring);
             par ^= 1;
-            if (tile >= num_full) break;
+            if (q.tile >= num_full) break;
         }
         // drain: the last reduced tile
         if ((tid >> 6) == 0) lag_resolve(prev, &s_excl, status, ctl);
         lds_barrier();
         lag_store<MODE>(prev, par ^ 1, s_data, &s_excl, num_tiles, out, d_count, dead);
     }
-    // the (single) partial tail tile, resolved immediately
-    for (; tile < num_tiles; tile += G) {
+    // the partial tail tile (the last tile, so nothing waits on this workgroup after it)
+    if (q.tile == num_full && num_full < num_tiles) {
         v4i cur[kChunks];
-        load_guarded(in, n, (int64_t)tile * kTile, tid, cur);
-        process_tile<MODE>(cur, tile, num_tiles, n, out, status, ctl, d_count, dead, s_wsum[0], &s_excl);
+        load_guarded(in, n, (int64_t)q.tile * kTile, tid, cur);
+        process_tile<MODE>(cur, q.tile, num_tiles, n, out, status, ctl, d_count, dead, s_wsum[0], &s_excl);
     }
 }
 
@@ -417,14 +432,15 @@ int launch(const int32_t* d_in, int32_t* d_out, int64_t n, int64_t* d_count, voi
     if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(workspace)");
     const int64_t tiles = (n + kTile - 1) / kTile;
     const bool aligned = ((reinterpret_cast<uintptr_t>(d_in) | reinterpret_cast<uintptr_t>(d_out)) & 15) == 0;
+    const bool claimed = g_schedule_claimed.load(std::memory_order_relaxed);
     if (aligned) {
         const int g = (int)std::min<int64_t>(tiles, resident_grid((const void*)k_scan_lag<MODE>));
         hipLaunchKernelGGL((k_scan_lag<MODE>), dim3(g), dim3(kThreads), 0, stream, d_in, d_out, n, status, ctl,
-                           d_count, dead);
+                           d_count, dead, (int)claimed);
     } else {
         const int g = (int)std::min<int64_t>(tiles, resident_grid((const void*)k_scan_tiles<MODE>));
         hipLaunchKernelGGL((k_scan_tiles<MODE>), dim3(g), dim3(kThreads), 0, stream, d_in, d_out, n, status, ctl,
-                           d_count, dead);
+                           d_count, dead, (int)claimed);
     }
     e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "scan kernel launch");
@@ -535,5 +551,10 @@ int sc_efficient_compact(int n, int* odata, const int* idata, int* count_out) {
 }
 
 float sc_timer_gpu_ms(void) { return g_timer_ms; }
+
+int sc_set_tile_schedule(int32_t claimed) {
+    g_schedule_claimed.store(claimed != 0, std::memory_order_relaxed);
+    return SC_OK;
+}
 
 }  // extern "C"

@@ -50,6 +50,8 @@ def gather_tiles(torch, dist, tile, height: int, group=None):
     so a single fixed-size gather suffices."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
+    if dist.get_backend(group) == "gloo" and tile.is_cuda:   # gloo gathers host tensors
+        tile = tile.cpu()
     rows = shard_rows(height, rank, world)
     if tile.dim() != 3 or tile.shape[0] < rows or tile.shape[2] != 3:
         raise ValueError(f"tile shape {tuple(tile.shape)} does not hold {rows} rows of RGB")
@@ -68,15 +70,19 @@ def gather_image(torch, dist, tile, height: int, group=None):
     return assemble([t.cpu().numpy() for t in tiles], height, len(tiles))
 
 
+def _coll_device(torch, dist, device):
+    return torch.device("cpu") if dist.get_backend() == "gloo" else device
+
+
 def max_over_ranks(torch, dist, seconds: float, device) -> float:
     """Wall time of the slowest rank (the bench's timed region ends when every rank is done)."""
-    t = torch.tensor([float(seconds)], dtype=torch.float64, device=device)
+    t = torch.tensor([float(seconds)], dtype=torch.float64, device=_coll_device(torch, dist, device))
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
 
 def sum_over_ranks(torch, dist, count: int, device) -> int:
     """Units (traced segments) processed by all ranks together."""
-    t = torch.tensor([int(count)], dtype=torch.int64, device=device)
+    t = torch.tensor([int(count)], dtype=torch.int64, device=_coll_device(torch, dist, device))
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return int(t.item())

@@ -32,6 +32,7 @@ public:
     float focal_len{10.0f};
     bool singleAlbedo{false};   // extension (include/pt_amd.h pt_flags.single_albedo)
     bool bvhCull{false};        // extension (include/pt_amd.h pt_flags.bvh_cull)
+    bool sharedGPU{false};      // extension (include/pt_amd.h pt_flags.shared_gpu); see flags_of()
 };
 
 struct vec3f {

@@ -43,6 +43,9 @@ class GuiDataContainer:
         self.singleAlbedo = False
         # extension, off = the reference: cull BVH nodes beyond the closest hit so far
         self.bvhCull = False
+        # tile schedule of the look-back kernels: False = static grid (fastest), True = claimed
+        # tiles (other kernels / processes share the GPU); default from PT_AMD_SCHEDULE=claim
+        self.sharedGPU = os.environ.get("PT_AMD_SCHEDULE", "") == "claim"
 
     def to_c(self) -> N.Flags:
         f = N.Flags()
@@ -57,6 +60,7 @@ class GuiDataContainer:
         f.focal_dist = float(self.focal_len)
         f.single_albedo = int(bool(self.singleAlbedo))
         f.bvh_cull = int(bool(self.bvhCull))
+        f.shared_gpu = int(bool(self.sharedGPU))
         return f
 
 

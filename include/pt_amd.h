@@ -65,6 +65,11 @@ typedef struct pt_flags {
      * unchanged unless rounding moves a triangle's computed t by more than the margin
      * (DESIGN.md §4). */
     int32_t bvh_cull;
+    /* Tile schedule of the look-back kernels (lookback.h): 0 = static co-resident grid (fastest;
+     * a launch that cannot get the whole GPU reports PT_ERR_DEVICE), 1 = tiles claimed in order
+     * from a ticket (correct when other kernels or processes share the GPU; ~2x slower bounce
+     * kernels).  pt_flags_default: 1 if PT_AMD_SCHEDULE=claim is set, else 0. */
+    int32_t shared_gpu;
 } pt_flags;
 
 /* Material (sceneStructs.h:43-57), 48 bytes. */

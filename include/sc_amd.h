@@ -66,6 +66,13 @@ int sc_partition_i32(const int32_t* d_flags, int32_t* d_perm, int64_t n, int64_t
 int sc_efficient_scan(int n, int* odata, const int* idata);
 int sc_efficient_compact(int n, int* odata, const int* idata, int* count_out);
 
+/* Tile schedule of the look-back kernels (process-wide).  0 (default, fastest): a static
+ * assignment over a grid that must be fully resident — if another kernel or process holds part of
+ * the GPU the call fails with SC_ERR_HIP-level "look-back spin bound" instead of hanging.
+ * 1: tiles claimed in order from a ticket — correct whatever else runs on the GPU, ~15% slower.
+ * The environment variable PT_AMD_SCHEDULE=claim selects 1 at load time. */
+int sc_set_tile_schedule(int32_t claimed);
+
 /* Elapsed device time (ms) of the previous host-pointer operation
  * (PerformanceTimer::getGpuElapsedTimeForPreviousOperation, common.h:98-101). */
 float sc_timer_gpu_ms(void);

@@ -170,3 +170,60 @@ def test_reference_size_2e28_properties(gpu_device):
         assert bool(torch.equal(out[:nz], f[f != 0]))
         del a, f, out
         torch.cuda.empty_cache()
+
+
+def test_concurrent_streams_make_progress(gpu_device):
+    """Two large scans and two compactions in flight at once on separate streams: each kernel is
+    sized to fill the GPU, so neither can have its whole grid resident.  In the claimed tile
+    schedule (lookback.h TileSeq) tiles are claimed in order from a ticket, so the look-back still
+    completes (the static schedule assumes a fully resident grid)."""
+    import torch
+    from cuda_pathtracer_amd._native import check_sc, lib
+    n = (1 << 24) + 777
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    a = torch.randint(0, 50, (n,), dtype=torch.int32, device=gpu_device)
+    b = torch.randint(0, 4, (n,), dtype=torch.int32, device=gpu_device)
+    oa, ob = torch.empty_like(a), torch.empty_like(b)
+    cnt = torch.zeros(1, dtype=torch.int64, device=gpu_device)
+    wa = torch.empty(int(lib().sc_workspace_bytes(n)), dtype=torch.uint8, device=gpu_device)
+    wb = torch.empty_like(wa)
+    torch.cuda.synchronize()
+    check_sc(lib().sc_set_tile_schedule(1))      # claimed tiles: safe when kernels share the GPU
+    try:
+        for _ in range(4):
+            check_sc(lib().sc_scan_exclusive_i32(a.data_ptr(), oa.data_ptr(), n, wa.data_ptr(), s1.cuda_stream))
+            check_sc(lib().sc_compact_i32(b.data_ptr(), ob.data_ptr(), n, cnt.data_ptr(), wb.data_ptr(),
+                                          s2.cuda_stream))
+        torch.cuda.synchronize()
+    finally:
+        check_sc(lib().sc_set_tile_schedule(0))
+    ha, hb = a.cpu().numpy(), b.cpu().numpy()
+    np.testing.assert_array_equal(oa.cpu().numpy(), O.scan(ha))
+    ref = O.compact_without_scan(hb)
+    assert int(cnt.item()) == len(ref)
+    np.testing.assert_array_equal(ob[:len(ref)].cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("n", [1, 8191, 8193, 100003, (1 << 20) + 5, (1 << 24) + 3])
+def test_claimed_schedule_matches_oracle(gpu_device, n):
+    """The claimed tile schedule gives the same bits as the static one (scan, compact, partition)."""
+    import torch
+    from cuda_pathtracer_amd import compact_device, partition_device, scan_device
+    from cuda_pathtracer_amd._native import check_sc, lib
+    a = _gen(n, 50, n + 11)
+    f = (a % 4).astype(np.int32)
+    check_sc(lib().sc_set_tile_schedule(1))
+    try:
+        s = scan_device(torch.from_numpy(a).to(gpu_device)).cpu().numpy()
+        out, cnt = compact_device(torch.from_numpy(f).to(gpu_device))
+        perm, live = partition_device(torch.from_numpy(f).to(gpu_device))
+        torch.cuda.synchronize()
+    finally:
+        check_sc(lib().sc_set_tile_schedule(0))
+    np.testing.assert_array_equal(s, O.scan(a))
+    ref = O.compact_without_scan(f)
+    assert int(cnt.item()) == len(ref)
+    np.testing.assert_array_equal(out[:len(ref)].cpu().numpy(), ref)
+    ref_perm, ref_live = O.partition_indices(f)
+    assert int(live.item()) == ref_live
+    np.testing.assert_array_equal(perm.cpu().numpy(), ref_perm)
