@@ -96,7 +96,6 @@ struct KArgs {
     DevStats* stats;
     unsigned long long* emit_slots;   // [64 bounces][emit_stride]: per-workgroup emissive counts
     int32_t emit_stride;
-    int32_t experiment;    // timing ablations only (PT_EXPERIMENT): bit0 no look-back, bit1 no shade, bit2 no isect
 };
 
 // ------------------------------------------------------------------------------------------
@@ -606,26 +605,19 @@ __global__ __launch_bounds__(kBlock) void k_trace(const KArgs A) {
         bool emitted = false;
         if (i < N) {
             PathReg p;
-            if (FIRST || (A.experiment & 8)) raygen(A.cam, A.fl, A.tile, i, p);
+            if (FIRST) raygen(A.cam, A.fl, A.tile, i, p);
             else load_path(A.in, i, p);
-            if (!FIRST && (A.experiment & 8)) p.bounces = 1;
-            Hit h;
-            if (A.experiment & 4) { h.t = 1.0f + p.d.x; h.n = p.d; h.mat = 1; h.u = h.v = 0.f; }
-            else h = intersect_scene<MESH>(A.S, A.fl, p.o, p.d);
-            if (A.experiment & 16) h.mat = 2;
-            if ((A.experiment & 64) && h.mat == 3) h.mat = 2;
+            const Hit h = intersect_scene<MESH>(A.S, A.fl, p.o, p.d);
             const int iter = A.tile.iter_first + (SPP1 ? 0 : p.slot / A.tile.npix);
-            bool alive;
-            if (A.experiment & 2) { alive = (h.t > 1.0f); p.o = p.o + h.n; }
-            else if (lds_mats) alive = shade(A.S, A.fl, A.tile.depth, iter, i, p, h, s_mats);
-            else alive = shade(A.S, A.fl, A.tile.depth, iter, i, p, h, A.S.mats);
+            const bool alive = lds_mats ? shade(A.S, A.fl, A.tile.depth, iter, i, p, h, s_mats)
+                                        : shade(A.S, A.fl, A.tile.depth, iter, i, p, h, A.S.mats);
             if (alive) {
-                if (!(A.experiment & 128)) store_survivor(A.in, i, p, FIRST);
+                store_survivor(A.in, i, p, FIRST);
             } else {
                 emitted = p.c.x != 0.0f || p.c.y != 0.0f || p.c.z != 0.0f;
-                if (!(A.experiment & 32)) retire<SPP1>(A, p);
+                retire<SPP1>(A, p);
             }
-            if (!(A.experiment & 256)) A.flags[i] = alive ? 1 : 0;
+            A.flags[i] = alive ? 1 : 0;
         }
         emit_cnt += (uint32_t)__popcll(__ballot(emitted));
     }
@@ -1229,7 +1221,6 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
     A.cam.res[0] = W;
     A.cam.res[1] = H;
     A.tile = TileDev{W, sh.rank, sh.world, (int)npix, sh.spp, (int)P, S.depth, 1};
-    if (const char* ex = std::getenv("PT_EXPERIMENT")) A.experiment = std::atoi(ex);
 
     // ---- path state, image, control ----
     for (int b = 0; b < 2; ++b)
