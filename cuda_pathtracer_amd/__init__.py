@@ -10,8 +10,10 @@ from .pathtrace import (  # noqa: F401
     CUBE, MESH, SPHERE, GuiDataContainer, InitDataContainer, PathTracer, Scene, pathtrace, pathtraceFree,
     pathtraceInit, render, save_image, tonemap)
 from . import distributed  # noqa: F401
-from .stream_compaction import Efficient, compact_device, partition_device, scan_device  # noqa: F401
+from .stream_compaction import (Efficient, compact_device, live_indices_device, partition_device,  # noqa: F401
+                                scan_device)
 
 __all__ = ["Scene", "PathTracer", "GuiDataContainer", "Efficient", "scan_device", "compact_device",
-           "partition_device", "render", "save_image", "tonemap", "pathtraceInit", "pathtraceFree", "pathtrace",
+           "partition_device", "live_indices_device", "render", "save_image", "tonemap", "pathtraceInit",
+           "pathtraceFree", "pathtrace",
            "InitDataContainer", "lib", "LIB_PATH", "NativeLibraryError", "PtError"]

@@ -29,7 +29,8 @@ class Flags(C.Structure):
     _fields_ = [("russian_roulette", C.c_int32), ("use_bvh", C.c_int32), ("use_bbox", C.c_int32),
                 ("sort_by_material", C.c_int32), ("use_thrust_partition", C.c_int32), ("ssaa", C.c_int32),
                 ("dof", C.c_int32), ("aperture", C.c_float), ("focal_dist", C.c_float),
-                ("single_albedo", C.c_int32), ("bvh_cull", C.c_int32), ("shared_gpu", C.c_int32)]
+                ("single_albedo", C.c_int32), ("bvh_cull", C.c_int32), ("shared_gpu", C.c_int32),
+                ("rng_key_pixel", C.c_int32)]
 
 
 class Material(C.Structure):
@@ -89,6 +90,7 @@ SIGNATURES = {
     "sc_scan_exclusive_i32": (_I, [_P, _P, C.c_int64, _P, _P]),
     "sc_compact_i32": (_I, [_P, _P, C.c_int64, _P, _P, _P]),
     "sc_partition_i32": (_I, [_P, _P, C.c_int64, _P, _P, _P]),
+    "sc_partition_indices": (_I, [_P, _P, C.c_int64, _P, _P, _P]),
     "sc_efficient_scan": (_I, [C.c_int, _P, _P]),
     "sc_efficient_compact": (_I, [C.c_int, _P, _P, _IP]),
     "sc_timer_gpu_ms": (C.c_float, []),
@@ -122,6 +124,8 @@ SIGNATURES = {
     "pt_preview_rgba": (_I, [_P, _I, _P, _P]),
     "pt_tile_info": (_I, [_P, _IP, _IP, _IP, _IP]),
     "pt_get_image": (_I, [_P, _P]),
+    "pt_get_accum": (_I, [_P, _P]),
+    "pt_render_iteration": (_I, [_P, _I, _P, _P]),
     "pt_copy_image": (_I, [_P, _P, _P]),
     "pt_reset_image": (_I, [_P, _P]),
     "pt_stats": (_I, [_P, C.POINTER(Stats)]),

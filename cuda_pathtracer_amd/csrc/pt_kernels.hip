@@ -72,6 +72,7 @@ struct FlagsDev {
     int32_t single_albedo;
     int32_t bvh_cull;
     int32_t claimed;   // tile schedule (lookback.h TileSeq)
+    int32_t rng_pixel; // shading RNG keyed by global pixel (pt_flags.rng_key_pixel)
 };
 struct TileDev {
     int32_t W, rank, world, npix, spp, P, depth, iter_first;
@@ -423,6 +424,14 @@ __device__ __forceinline__ f3 refract(f3 I, f3 N, float eta) {   // glm 0.9.6.3:
     return (eta * I - (eta * dv + sqrtf(k)) * N) * (float)(k >= 0.0f);
 }
 
+// Global pixel index of tile slot `slot` (the raygen mapping below): the shading RNG key under
+// pt_flags.rng_key_pixel, independent of compaction order and of the shard layout.
+__device__ __forceinline__ int slot_pixel(const CamDev& cam, const TileDev& T, int slot) {
+    const int lp = slot % T.npix;
+    const int row = lp / T.W;
+    return (lp - row * T.W) + (row * T.world + T.rank) * cam.res[0];
+}
+
 // Returns true if the path survives.  `idx` is the path's position in the (compacted, possibly
 // material-sorted) array — the RNG key of the reference (pathtrace.cu:315).
 template <class MT>
@@ -609,8 +618,8 @@ __global__ __launch_bounds__(kBlock) void k_trace(const KArgs A) {
             else load_path(A.in, i, p);
             const Hit h = intersect_scene<MESH>(A.S, A.fl, p.o, p.d);
             const int iter = A.tile.iter_first + (SPP1 ? 0 : p.slot / A.tile.npix);
-            const bool alive = lds_mats ? shade(A.S, A.fl, A.tile.depth, iter, i, p, h, s_mats)
-                                        : shade(A.S, A.fl, A.tile.depth, iter, i, p, h, A.S.mats);
+            const bool alive = lds_mats ? shade(A.S, A.fl, A.tile.depth, iter, A.fl.rng_pixel ? slot_pixel(A.cam, A.tile, p.slot) : i, p, h, s_mats)
+                                        : shade(A.S, A.fl, A.tile.depth, iter, A.fl.rng_pixel ? slot_pixel(A.cam, A.tile, p.slot) : i, p, h, A.S.mats);
             if (alive) {
                 store_survivor(A.in, i, p, FIRST);
             } else {
@@ -693,8 +702,8 @@ __global__ __launch_bounds__(kBlock) void k_bounce(const KArgs A) {
             else load_path(A.in, i, p);
             const Hit h = intersect_scene<MESH>(A.S, A.fl, p.o, p.d);
             const int iter = A.tile.iter_first + (SPP1 ? 0 : p.slot / A.tile.npix);
-            alive = lds_mats ? shade(A.S, A.fl, A.tile.depth, iter, i, p, h, s_mats)
-                             : shade(A.S, A.fl, A.tile.depth, iter, i, p, h, A.S.mats);
+            alive = lds_mats ? shade(A.S, A.fl, A.tile.depth, iter, A.fl.rng_pixel ? slot_pixel(A.cam, A.tile, p.slot) : i, p, h, s_mats)
+                             : shade(A.S, A.fl, A.tile.depth, iter, A.fl.rng_pixel ? slot_pixel(A.cam, A.tile, p.slot) : i, p, h, A.S.mats);
             if (!alive) {
                 emitted = p.c.x != 0.0f || p.c.y != 0.0f || p.c.z != 0.0f;
                 retire<SPP1>(A, p);
@@ -881,8 +890,8 @@ __global__ __launch_bounds__(kBlock) void k_shade_sorted(const KArgs A) {
             h.u = A.hit.u[i];
             h.v = A.hit.v[i];
             const int iter = A.tile.iter_first + (SPP1 ? 0 : p.slot / A.tile.npix);
-            const bool alive = lds_mats ? shade(A.S, A.fl, A.tile.depth, iter, idx, p, h, s_mats)
-                                        : shade(A.S, A.fl, A.tile.depth, iter, idx, p, h, A.S.mats);
+            const bool alive = lds_mats ? shade(A.S, A.fl, A.tile.depth, iter, A.fl.rng_pixel ? slot_pixel(A.cam, A.tile, p.slot) : idx, p, h, s_mats)
+                                        : shade(A.S, A.fl, A.tile.depth, iter, A.fl.rng_pixel ? slot_pixel(A.cam, A.tile, p.slot) : idx, p, h, A.S.mats);
             if (alive) {
                 store_survivor(A.out, idx, p, true);   // sorted order, compacted by k_compact_paths
             } else {
@@ -990,6 +999,7 @@ void set_flags_dev(pt_ctx* c, const pt_flags& f) {
     c->args.fl.single_albedo = f.single_albedo;
     c->args.fl.bvh_cull = f.bvh_cull;
     c->args.fl.claimed = f.shared_gpu;
+    c->args.fl.rng_pixel = f.rng_key_pixel;
 }
 
 float bits_to_float(int32_t v) {
@@ -1369,6 +1379,13 @@ int pt_preview_rgba(pt_ctx* c, int32_t iter, uint8_t* d_rgba, void* stream) {
     return PT_OK;
 }
 
+int pt_render_iteration(pt_ctx* c, int32_t iter, uint8_t* d_rgba, void* stream) {
+    if (!c || iter <= 0) return pt::fail(PT_ERR_ARG, "bad argument");
+    const int rc = pt_render_pass(c, iter, stream);
+    if (rc || !d_rgba) return rc;
+    return pt_preview_rgba(c, iter + c->args.tile.spp - 1, d_rgba, stream);
+}
+
 int pt_tile_info(const pt_ctx* c, int32_t* width, int32_t* rows, int32_t* npix, int32_t* npaths) {
     if (!c) return pt::fail(PT_ERR_ARG, "null context");
     const TileDev& T = c->args.tile;
@@ -1385,6 +1402,8 @@ int pt_get_image(pt_ctx* c, float* host_rgb) {
     HIP_TRY(hipMemcpy(host_rgb, c->args.image, (size_t)c->args.tile.npix * 3 * sizeof(float), hipMemcpyDeviceToHost));
     return PT_OK;
 }
+
+int pt_get_accum(pt_ctx* c, float* host_rgb) { return pt_get_image(c, host_rgb); }
 
 int pt_copy_image(pt_ctx* c, float* d_rgb, void* stream) {
     if (!c || !d_rgb) return pt::fail(PT_ERR_ARG, "null argument");

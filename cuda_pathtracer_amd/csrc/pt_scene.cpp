@@ -351,6 +351,7 @@ void pt_flags_default(pt_flags* f) {   // utilities.h:23-33
     f->ssaa = 1;
     f->dof = 1;
     f->single_albedo = 0;
+    f->rng_key_pixel = 0;
     f->bvh_cull = 0;
     const char* sched = std::getenv("PT_AMD_SCHEDULE");
     f->shared_gpu = sched && std::strcmp(sched, "claim") == 0;

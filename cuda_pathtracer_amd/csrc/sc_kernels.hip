@@ -51,7 +51,7 @@ int hip_fail(hipError_t e, const char* where) {
     return fail(SC_ERR_HIP, std::string(where) + ": " + hipGetErrorString(e));
 }
 
-enum Mode { kScan = 0, kCompact = 1, kPartition = 2 };
+enum Mode { kScan = 0, kCompact = 1, kPartition = 2, kIndices = 3 };
 typedef int v4i __attribute__((ext_vector_type(4)));
 
 // LDS-only workgroup barrier: waits for this wave's LDS traffic, not for its outstanding global
@@ -123,8 +123,9 @@ __device__ __forceinline__ uint32_t tile_offsets(const v4i (&cur)[kChunks], uint
     return run;
 }
 
-// Outputs of chunk k of a tile whose prefix is known: scan values, kept values, or partition
-// indices (live in order; dead ones to `dead` in order, appended by k_append_dead).
+// Outputs of chunk k of a tile whose prefix is known: scan values, kept values, live indices, or
+// partition indices (live in order; dead ones to `dead` in order, appended by k_append_dead).
+// Padding lanes of a partial tile load as 0, so they are never counted or kept.
 template <int MODE, bool FULL>
 __device__ __forceinline__ void write_chunk(const v4i& v, int64_t e0, uint32_t run, int64_t n,
                                             int32_t* __restrict__ out, int32_t* __restrict__ dead) {
@@ -143,6 +144,10 @@ __device__ __forceinline__ void write_chunk(const v4i& v, int64_t e0, uint32_t r
 #pragma unroll
         for (int e = 0; e < 4; ++e)
             if (v[e] != 0) out[run++] = v[e];
+    } else if (MODE == kIndices) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            if (v[e] != 0) out[run++] = (int32_t)(e0 + e);
     } else {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -153,6 +158,14 @@ __device__ __forceinline__ void write_chunk(const v4i& v, int64_t e0, uint32_t r
             }
         }
     }
+}
+
+// The kept count, written once by the last tile: int64 for compact / partition, int32 for the
+// index list (sc_partition_indices' contract).
+template <int MODE>
+__device__ __forceinline__ void store_count(int64_t* __restrict__ d_count, uint32_t v) {
+    if (MODE == kIndices) *reinterpret_cast<int32_t*>(d_count) = (int32_t)v;
+    else *d_count = (int64_t)v;
 }
 
 // One tile with the look-back resolved immediately (unaligned inputs, the partial tail tile).
@@ -182,7 +195,7 @@ __device__ __forceinline__ void process_tile(const v4i (&cur)[kChunks], int tile
 #pragma unroll
     for (int k = 0; k < kChunks; ++k)
         write_chunk<MODE, false>(cur[k], base + (int64_t)k * (kThreads * 4) + 4 * tid, excl + pre[k], n, out, dead);
-    if (MODE != kScan && tid == 0 && tile == num_tiles - 1) *d_count = (int64_t)(excl + total);
+    if (MODE != kScan && tid == 0 && tile == num_tiles - 1) store_count<MODE>(d_count, excl + total);
 }
 
 // ---- lagged look-back -----------------------------------------------------------------------
@@ -240,7 +253,7 @@ __device__ __forceinline__ void lag_store(const LagTile& L, int par, const int32
         const v4i v = *reinterpret_cast<const v4i*>(&s_data[par][k * (kThreads * 4) + 4 * tid]);
         write_chunk<MODE, true>(v, base + (int64_t)k * (kThreads * 4) + 4 * tid, excl + L.pre[k], 0, out, dead);
     }
-    if (MODE != kScan && tid == 0 && L.tile == num_tiles - 1) *d_count = (int64_t)(excl + L.total);
+    if (MODE != kScan && tid == 0 && L.tile == num_tiles - 1) store_count<MODE>(d_count, excl + L.total);
 }
 
 // One step: prefetch `next` into `pf`, reduce `cur` (= tile), resolve + write the deferred tile.
@@ -423,7 +436,7 @@ int launch(const int32_t* d_in, int32_t* d_out, int64_t n, int64_t* d_count, voi
     int32_t* dead = reinterpret_cast<int32_t*>(ws + kCtlBytes + status_bytes(n));
     if (n == 0) {
         if (MODE != kScan) {
-            hipError_t e = hipMemsetAsync(d_count, 0, sizeof(int64_t), stream);
+            hipError_t e = hipMemsetAsync(d_count, 0, MODE == kIndices ? sizeof(int32_t) : sizeof(int64_t), stream);
             if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync");
         }
         return SC_OK;
@@ -542,6 +555,11 @@ int sc_compact_i32(const int32_t* d_in, int32_t* d_out, int64_t n, int64_t* d_co
 int sc_partition_i32(const int32_t* d_flags, int32_t* d_perm, int64_t n, int64_t* d_live, void* workspace,
                      void* stream) {
     return launch<kPartition>(d_flags, d_perm, n, d_live, workspace, (hipStream_t)stream);
+}
+
+int sc_partition_indices(const int32_t* d_flags, int32_t* d_idx, int64_t n, int32_t* d_count, void* workspace,
+                         void* stream) {
+    return launch<kIndices>(d_flags, d_idx, n, reinterpret_cast<int64_t*>(d_count), workspace, (hipStream_t)stream);
 }
 
 int sc_efficient_scan(int n, int* odata, const int* idata) { return host_op<kScan>(n, odata, idata, nullptr); }

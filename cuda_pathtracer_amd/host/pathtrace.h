@@ -33,6 +33,7 @@ public:
     bool singleAlbedo{false};   // extension (include/pt_amd.h pt_flags.single_albedo)
     bool bvhCull{false};        // extension (include/pt_amd.h pt_flags.bvh_cull)
     bool sharedGPU{false};      // extension (include/pt_amd.h pt_flags.shared_gpu); see flags_of()
+    bool rngKeyPixel{false};    // extension (include/pt_amd.h pt_flags.rng_key_pixel)
 };
 
 struct vec3f {

@@ -46,6 +46,9 @@ class GuiDataContainer:
         # tile schedule of the look-back kernels: False = static grid (fastest), True = claimed
         # tiles (other kernels / processes share the GPU); default from PT_AMD_SCHEDULE=claim
         self.sharedGPU = os.environ.get("PT_AMD_SCHEDULE", "") == "claim"
+        # extension, off = the reference: shading RNG keyed by the global pixel, so the image does
+        # not depend on the shard layout or the material sort (bitwise equal across GPU counts)
+        self.rngKeyPixel = False
 
     def to_c(self) -> N.Flags:
         f = N.Flags()
@@ -61,6 +64,7 @@ class GuiDataContainer:
         f.single_albedo = int(bool(self.singleAlbedo))
         f.bvh_cull = int(bool(self.bvhCull))
         f.shared_gpu = int(bool(self.sharedGPU))
+        f.rng_key_pixel = int(bool(self.rngKeyPixel))
         return f
 
 

@@ -106,3 +106,17 @@ def partition_device(d_flags, d_perm=None, stream=None):
     check_sc(lib().sc_partition_i32(d_flags.data_ptr(), d_perm.data_ptr(), d_flags.numel(), live.data_ptr(), None,
                                     _stream_ptr(stream)))
     return d_perm, live
+
+
+def live_indices_device(d_flags, d_idx=None, stream=None):
+    """Index list of the non-zero flags, in order (sc_partition_indices): returns (d_idx, count)
+    with the count as a 1-element int32 tensor; d_idx beyond the count is untouched."""
+    import torch
+    _check_dev_i32(d_flags, "d_flags")
+    if d_idx is None:
+        d_idx = torch.empty_like(d_flags)
+    _check_dev_i32(d_idx, "d_idx")
+    cnt = torch.zeros(1, dtype=torch.int32, device=d_flags.device)
+    check_sc(lib().sc_partition_indices(d_flags.data_ptr(), d_idx.data_ptr(), d_flags.numel(), cnt.data_ptr(), None,
+                                        _stream_ptr(stream)))
+    return d_idx, cnt

@@ -70,6 +70,11 @@ typedef struct pt_flags {
      * from a ticket (correct when other kernels or processes share the GPU; ~2x slower bounce
      * kernels).  pt_flags_default: 1 if PT_AMD_SCHEDULE=claim is set, else 0. */
     int32_t shared_gpu;
+    /* Extension (default 0 = the reference): key the shading RNG by the path's global pixel index
+     * instead of its position in the compacted path array (pathtrace.cu:315).  The image then
+     * no longer depends on how pixels are sharded across GPUs or sorted by material: N-GPU output
+     * is bitwise equal to 1-GPU output (SURVEY.md §8e's rng_key=pixel mode). */
+    int32_t rng_key_pixel;
 } pt_flags;
 
 /* Material (sceneStructs.h:43-57), 48 bytes. */
@@ -194,8 +199,13 @@ int pt_set_flags(pt_ctx* c, const pt_flags* flags);         /* InitDataContainer
 int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream);
 /* sendImageToPBO (pathtrace.cu:64-86) for the tile: d_rgba = npix * 4 bytes on the device. */
 int pt_preview_rgba(pt_ctx* c, int32_t iter, uint8_t* d_rgba, void* stream);
+/* pathtrace(pbo, frame, iteration) (pathtrace.h:9, pathtrace.cu:437-525) as one call, under the
+ * name SURVEY.md §8b gives it: pt_render_pass for iterations [iter, iter + spp), then, when d_rgba
+ * is non-NULL, pt_preview_rgba of the accumulated iter + spp - 1 samples (iterations counted from 1). */
+int pt_render_iteration(pt_ctx* c, int32_t iter, uint8_t* d_rgba, void* stream);
 int pt_tile_info(const pt_ctx* c, int32_t* width, int32_t* rows, int32_t* npix, int32_t* npaths);
 int pt_get_image(pt_ctx* c, float* host_rgb);               /* tile accumulator, npix*3 floats (sync) */
+int pt_get_accum(pt_ctx* c, float* host_rgb);               /* §8b name of pt_get_image (pathtrace.cu:524) */
 int pt_copy_image(pt_ctx* c, float* d_rgb, void* stream);   /* device-to-device copy */
 int pt_reset_image(pt_ctx* c, void* stream);
 int pt_stats(pt_ctx* c, pt_stats_t* out);                   /* synchronises the context stream */

@@ -7,6 +7,7 @@
  *   Efficient::timer()   efficient.h:7   / common.h:46-130        -> sc_timer_gpu_ms
  *   Common::kernMapToBoolean / kernScatter  common.cu:25-46       -> fused into sc_compact_i32
  *   mark_valid + scan + keep  path_tracer/src/pathtrace.cu:359-407 -> sc_partition_i32 (stable partition)
+ *                                                                    and sc_partition_indices (live index list)
  * The reference's CPU:: functions (cpu.h:9-13) are the test ORACLE (oracle/sc_oracle.cpp), not part
  * of this product library: there is no CPU fallback here.
  *
@@ -59,6 +60,12 @@ int sc_compact_i32(const int32_t* d_in, int32_t* d_out, int64_t n, int64_t* d_co
  * `keep` placement of pathtrace.cu:366-376.  *d_live (device int64) = number of live elements. */
 int sc_partition_i32(const int32_t* d_flags, int32_t* d_perm, int64_t n, int64_t* d_live,
                      void* workspace, void* stream);
+
+/* Index list of the live elements: d_idx[j] = index of the j-th non-zero flag, in order;
+ * *d_count (device int32) = their number.  The 8 B/path path-compaction primitive of SURVEY.md
+ * §8b (flag read + index write); d_idx beyond the count is left untouched. */
+int sc_partition_indices(const int32_t* d_flags, int32_t* d_idx, int64_t n, int32_t* d_count,
+                         void* workspace, void* stream);
 
 /* Host-pointer helpers with the reference's exact call semantics (Efficient::scan / compact take
  * host arrays and return after the result is on the host).  They allocate device buffers from a

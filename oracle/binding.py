@@ -57,7 +57,7 @@ class OFlags(C.Structure):
     _fields_ = [("russian_roulette", C.c_int32), ("use_bvh", C.c_int32), ("use_bbox", C.c_int32),
                 ("sort_by_material", C.c_int32), ("use_thrust_partition", C.c_int32), ("ssaa", C.c_int32),
                 ("dof", C.c_int32), ("aperture", C.c_float), ("focal_dist", C.c_float),
-                ("single_albedo", C.c_int32)]
+                ("single_albedo", C.c_int32), ("rng_key_pixel", C.c_int32)]
 
 
 _lib = None
@@ -275,10 +275,11 @@ class OracleScene:
 
 
 def flags(russian_roulette=True, use_bvh=True, use_bbox=True, sort_by_material=False, use_thrust_partition=False,
-          ssaa=True, dof=True, aperture=0.1, focal_dist=10.0, single_albedo=False) -> OFlags:
+          ssaa=True, dof=True, aperture=0.1, focal_dist=10.0, single_albedo=False,
+          rng_key_pixel=False) -> OFlags:
     return OFlags(int(russian_roulette), int(use_bvh), int(use_bbox), int(sort_by_material),
                   int(use_thrust_partition), int(ssaa), int(dof), float(aperture), float(focal_dist),
-                  int(single_albedo))
+                  int(single_albedo), int(rng_key_pixel))
 
 
 def render_pass(sc: OracleScene, fl: OFlags, iter_first: int, spp: int = 1, rank: int = 0, world: int = 1,

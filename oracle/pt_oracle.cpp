@@ -60,6 +60,7 @@ struct OFlags {                // utilities.h:17-34 (GuiDataContainer) / pathtra
     int32_t russian_roulette, use_bvh, use_bbox, sort_by_material, use_thrust_partition, ssaa, dof;
     float aperture, focal_dist;
     int32_t single_albedo;     // extension (pt_amd.h); 0 = the reference
+    int32_t rng_key_pixel;     // extension (pt_amd.h): shading RNG keyed by the global pixel
 };
 struct OTriangle {             // sceneStructs.h:103-161 (124 bytes)
     int32_t id;
@@ -730,7 +731,7 @@ int oracle_render_pass(const OGeom* geoms, int ngeoms, const OMaterial* mats, in
             for (int i = 0; i < N; ++i) { tmp[i] = paths[ord[i]]; is2[i] = isect[ord[i]]; }
             for (int i = 0; i < N; ++i) { paths[i] = tmp[i]; isect[i] = is2[i]; }
         }
-        for (int i = 0; i < N; ++i) shade(sc, *fl, paths[i], isect[i], i);
+        for (int i = 0; i < N; ++i) shade(sc, *fl, paths[i], isect[i], fl->rng_key_pixel ? paths[i].pixel : i);
         // relocate_terminated_paths (pathtrace.cu:377-407) == thrust::stable_partition here
         for (int i = 0; i < N; ++i) flags[i] = paths[i].remaining == 0 ? 0 : 1;
         int live = 0;

@@ -226,6 +226,25 @@ def test_render_shards_tile_the_image():
     np.testing.assert_array_equal(assemble(parts, 32, world), full)
 
 
+def test_rng_key_pixel_is_shard_and_sort_invariant():
+    """pt_flags.rng_key_pixel: with the shading RNG keyed by the global pixel the
+    full-depth image no longer depends on the shard layout or on the material sort — assembled
+    shards and the sorted render equal the 1-rank render bit for bit.  With the reference key
+    (compacted index) they do not."""
+    from cuda_pathtracer_amd.distributed import assemble
+    sc = _small_scene()
+    fl = O.flags(rng_key_pixel=True)
+    full, live = O.render_pass(sc, fl, iter_first=5, spp=2)
+    assert live[1] > 0 and full.sum() > 0
+    world = 3
+    parts = [O.render_pass(sc, fl, iter_first=5, spp=2, rank=r, world=world)[0] for r in range(world)]
+    np.testing.assert_array_equal(assemble(parts, 32, world), full)
+    sorted_img, _ = O.render_pass(sc, O.flags(rng_key_pixel=True, sort_by_material=True), iter_first=5, spp=2)
+    np.testing.assert_array_equal(sorted_img, full)
+    ref = [O.render_pass(sc, O.flags(), iter_first=5, spp=2, rank=r, world=world)[0] for r in range(world)]
+    assert not np.array_equal(assemble(ref, 32, world), O.render_pass(sc, O.flags(), iter_first=5, spp=2)[0])
+
+
 def test_tonemap_rules():
     """saveImage (main.cpp:88-112) + Image::savePNG (image.cpp:22-42): divide by samples, clamp to
     [0,1], x255 truncate, mirror in x."""

@@ -33,7 +33,7 @@ def _gui(**kw):
 
 def _oflags(g):
     return O.flags(g.russianRoulette, g.useBVHtree, g.useBBox, g.sortbyMaterial, g.useThrustPartition, g.SSAA,
-                   g.DoF, g.aperture, g.focal_len, g.singleAlbedo)
+                   g.DoF, g.aperture, g.focal_len, g.singleAlbedo, g.rngKeyPixel)
 
 
 def _assert_bitexact(gpu, ref, what):
@@ -85,6 +85,8 @@ def test_cornell_bitexact_default_flags(cornell_path):
     dict(singleAlbedo=True, sortbyMaterial=True),
     dict(sharedGPU=True),                          # claimed tile schedule, fused pipeline
     dict(sharedGPU=True, sortbyMaterial=True),     # claimed schedule in the sorted pipeline's compaction
+    dict(rngKeyPixel=True),                        # shading RNG keyed by the global pixel
+    dict(rngKeyPixel=True, sortbyMaterial=True),
 ])
 def test_cornell_bitexact_flags(cornell_path, kw):
     s, o = _pair(cornell_path, (48, 40))
@@ -126,6 +128,27 @@ def test_tiles_and_batched_samples(cornell_path, rank, world, spp):
     assert st["bounce_live"] == live
 
 
+def test_rng_key_pixel_shards_equal_single_gpu(cornell_path):
+    """§8e's shard-invariant mode on the device: with rngKeyPixel the 3-way row shards, assembled,
+    equal the 1-GPU image bit for bit — and so does the material-sorted pipeline."""
+    from cuda_pathtracer_amd import PathTracer, distributed
+    s, o = _pair(cornell_path, (40, 37))
+
+    def render(rank, world, **kw):
+        pt = PathTracer(s, _gui(rngKeyPixel=True, **kw), rank=rank, world=world, spp=2)
+        for it in (1, 3):
+            pt.render_pass(it)
+        img = pt.image()
+        pt.free()
+        return img
+
+    full = render(0, 1)
+    assert full.sum() > 0
+    parts = [render(r, 3) for r in range(3)]
+    _assert_bitexact(distributed.assemble(parts, 37, 3), full, "assembled shards vs 1 GPU")
+    _assert_bitexact(render(0, 1, sortbyMaterial=True), full, "sorted vs unsorted")
+
+
 def test_preview_rgba_matches_sendImageToPBO(cornell_path, gpu_device):
     import torch
     from cuda_pathtracer_amd import PathTracer
@@ -141,6 +164,30 @@ def test_preview_rgba_matches_sendImageToPBO(cornell_path, gpu_device):
     O.lib().oracle_preview(np.ascontiguousarray(img).ctypes.data, 32, 32, 2, ref.ctypes.data)
     np.testing.assert_array_equal(buf.cpu().numpy(), ref)
     pt.free()
+
+
+def test_render_iteration_and_get_accum(cornell_path, gpu_device):
+    """The §8b entry points: pt_render_iteration (pass + preview of iter + spp - 1 samples) and
+    pt_get_accum give the same bits as pt_render_pass / pt_preview_rgba / pt_get_image."""
+    import ctypes as C
+    import torch
+    from cuda_pathtracer_amd import PathTracer, lib
+    s, o = _pair(cornell_path, (24, 20))
+    pt = PathTracer(s, _gui(), spp=2)
+    buf = torch.zeros(24 * 20 * 4, dtype=torch.uint8, device=gpu_device)
+    for it in (1, 3):
+        assert lib().pt_render_iteration(pt._h, it, C.c_void_p(buf.data_ptr()), None) == 0
+    torch.cuda.synchronize()
+    acc = np.zeros(24 * 20 * 3, np.float32)
+    assert lib().pt_get_accum(pt._h, acc.ctypes.data) == 0
+    pt.free()
+    r = None
+    for it in (1, 3):
+        r, _ = O.render_pass(o, _oflags(_gui()), it, spp=2, image=r)
+    _assert_bitexact(acc.reshape(r.shape), r, "pt_get_accum")
+    ref = np.zeros(24 * 20 * 4, np.uint8)
+    O.lib().oracle_preview(np.ascontiguousarray(r).ctypes.data, 24, 20, 4, ref.ctypes.data)
+    np.testing.assert_array_equal(buf.cpu().numpy(), ref)
 
 
 @pytest.mark.slow

@@ -82,6 +82,21 @@ def test_partition_matches_keep(gpu_device, n):
     np.testing.assert_array_equal(perm.cpu().numpy(), ref)
 
 
+@pytest.mark.parametrize("n", [1, 2, 65, 8192, 8193, 100000, 1 << 20])
+def test_live_indices_match_keep(gpu_device, n):
+    """sc_partition_indices: the live prefix of the stable partition, int32 count."""
+    import torch
+    from cuda_pathtracer_amd import live_indices_device
+    f = _gen(n, 3, n + 7) * (np.arange(n) % 5 != 0)
+    sentinel = torch.full((n,), -7, dtype=torch.int32, device=gpu_device)
+    idx, cnt = live_indices_device(torch.from_numpy(f.astype(np.int32)).to(gpu_device), sentinel)
+    ref, ref_live = O.partition_indices(f.astype(np.int32))
+    assert cnt.dtype == torch.int32 and int(cnt.item()) == ref_live
+    got = idx.cpu().numpy()
+    np.testing.assert_array_equal(got[:ref_live], ref[:ref_live])
+    assert (got[ref_live:] == -7).all()
+
+
 def test_edge_cases(gpu_device):
     import torch
     from cuda_pathtracer_amd import compact_device, scan_device
