@@ -43,9 +43,9 @@ struct HitSoA {
     int32_t* mat;
 };
 struct Ctl {            // per-parity control block (16 B)
-    uint32_t ticket;
-    uint32_t live;
-    uint32_t pad[2];
+    uint32_t ticket;       // claimed tile schedule (look-back kernels)
+    uint32_t live;         // path count after k_compact_paths (split / sorted pipelines)
+    uint32_t chunk, nseg;  // segment layout written by k_bounce (fused pipeline)
 };
 struct DevStats {
     unsigned long long segments, passes, bounce_live[64];
@@ -94,6 +94,7 @@ struct KArgs {
     int32_t bounce;
     int32_t n_fixed;       // >= 0: path count is known on the host (first bounce)
     int32_t* flags;        // [P] survivor flags of the current bounce
+    int32_t* seg;          // [2][kMaxSeg] per-workgroup survivor counts of k_bounce
     DevStats* stats;
     unsigned long long* emit_slots;   // [64 bounces][emit_stride]: per-workgroup emissive counts
     int32_t emit_stride;
@@ -634,89 +635,133 @@ __global__ __launch_bounds__(kBlock) void k_trace(const KArgs A) {
 }
 
 // ---- fused pipeline: one kernel per bounce ---------------------------------------------------
-// Per-tile stable compaction inside the bounce kernel: wave ballot + mbcnt ranks, 4 wave counts
-// in LDS, decoupled look-back by wave 0.  Returns this lane's output position (valid if alive).
-__device__ __forceinline__ int compact_tile(const KArgs& A, int tile, int num_tiles, bool alive,
-                                            uint32_t* s_wc, uint32_t* s_excl) {
+// Segmented stable compaction, no inter-workgroup dependency.  Workgroup b of a launch owns the
+// contiguous LOGICAL path range [b*chunk, (b+1)*chunk) (chunk = whole 256-path tiles) and writes
+// its survivors, in order, to the front of PHYSICAL segment b = out[b*chunk ...]; its survivor
+// count goes to seg[parity^1][b].  The next launch scans the (<= kMaxSeg) counts in LDS at start:
+// logical survivor j lives in the segment s with pre[s] <= j < pre[s+1], at s*chunk + j - pre[s].
+// Concatenating the segments in order is exactly the stable compaction of pathtrace.cu:377-407,
+// so the logical index is the reference's RNG key (pathtrace.cu:315).
+//   Measured before this design (profiles/r01_*): the decoupled look-back per 256-path tile parked
+// every wave of a workgroup behind wave 0's cross-CU poll — 57% of wave cycles waiting vs 25% in
+// the same trace code without compaction.  Here nothing waits on another workgroup, so the grid
+// need not be co-resident and shared GPUs need no claimed schedule.
+constexpr int kMaxSeg = 2048;
+
+// Exclusive scan of the previous launch's segment counts into s_pre[0..nseg] (s_pre[nseg] = N).
+__device__ __forceinline__ int scan_segments(const int32_t* __restrict__ cnt, int nseg, int32_t* s_pre,
+                                             uint32_t* s_wsum) {
+    constexpr int kPer = kMaxSeg / kBlock;   // 8 counts per thread
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint64_t m = __ballot(alive);
-    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-    __syncthreads();   // the previous tile's readers of s_wc / s_excl are done
-    if (lane == 0) s_wc[wave] = (uint32_t)__popcll(m);
-    __syncthreads();
-    const uint32_t w0 = s_wc[0], w1 = s_wc[1], w2 = s_wc[2], w3 = s_wc[3];
-    const uint32_t total = (w0 + w1) + (w2 + w3);
-    const uint32_t before = (wave > 0 ? w0 : 0u) + (wave > 1 ? w1 : 0u) + (wave > 2 ? w2 : 0u);
-    uint64_t* st = A.status + (size_t)A.parity * A.max_tiles;
-    if (wave == 0) {
-        uint32_t excl = 0;
-        if (tile == 0) {
-            if (lane == 0) lb::publish(st, 0, lb::kFlagPre, total);
-        } else {
-            if (lane == 0) lb::publish(st, tile, lb::kFlagAgg, total);
-            excl = lb::lookback(st, tile, lane, &A.stats->err);
-            if (lane == 0) lb::publish(st, tile, lb::kFlagPre, excl + total);
-        }
-        if (lane == 0) {
-            *s_excl = excl;
-            if (tile == num_tiles - 1) A.ctl[A.parity ^ 1].live = excl + total;
-        }
+    int32_t v[kPer];
+    uint32_t sum = 0;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const int s = tid * kPer + k;
+        v[k] = s < nseg ? cnt[s] : 0;
+        sum += (uint32_t)v[k];
     }
+    const uint32_t incl = lb::wave_inclusive_scan(sum);
+    if (lane == 63) s_wsum[wave] = incl;
     __syncthreads();
-    return (int)(*s_excl + before + rank);
+    uint32_t run = incl - sum;
+    for (int w = 0; w < wave; ++w) run += s_wsum[w];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const int s = tid * kPer + k;
+        if (s <= nseg) s_pre[s] = (int32_t)run;
+        run += (uint32_t)v[k];
+    }
+    if (tid == kBlock - 1) s_pre[kMaxSeg] = (int32_t)run;   // nseg == kMaxSeg
+    __syncthreads();
+    return s_pre[nseg];
 }
 
-// [raygen] -> intersect -> shade -> stable compaction over claimed tiles (lookback.h TileSeq: no
-// co-residency needed).  Survivors go straight to their final position in A.out.
+// Segment holding logical index i, searching up from `s` (s_pre[s] <= i).
+__device__ __forceinline__ int seg_walk(const int32_t* s_pre, int nseg, int s, int i) {
+    while (s + 1 < nseg && s_pre[s + 1] <= i) ++s;
+    return s;
+}
+
+// [raygen] -> intersect -> shade -> segmented compaction (above).
 template <bool FIRST, bool SPP1, bool MESH>
 __global__ __launch_bounds__(kBlock) void k_bounce(const KArgs A) {
     __shared__ DMaterial s_mats[kLdsMats];
-    __shared__ uint32_t s_wc[4];
-    __shared__ uint32_t s_excl, s_cnt;
-    __shared__ int s_ring[lb::kRing];
-    {   // zero the look-back words the next launch (other parity) will use
-        uint64_t* nst = A.status + (size_t)(A.parity ^ 1) * A.max_tiles;
-        for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < A.max_tiles; j += gridDim.x * blockDim.x) nst[j] = 0ull;
+    __shared__ int32_t s_pre[FIRST ? 1 : kMaxSeg + 1];
+    __shared__ uint32_t s_wc[2][4];
+    __shared__ uint32_t s_cnt;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int par = A.parity;
+    int N, nseg_in = 0, chunk_in = 0;
+    if (FIRST) {
+        N = A.n_fixed;
+    } else {
+        nseg_in = (int)A.ctl[par].nseg;
+        chunk_in = (int)A.ctl[par].chunk;
+        N = scan_segments(A.seg + (size_t)par * kMaxSeg, nseg_in, s_pre, s_wc[0]);
     }
-    const int N = live_count(A);
-    const int num_tiles = (N + kBlock - 1) / kBlock;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        A.ctl[A.parity ^ 1].ticket = 0u;   // the next look-back launch claims from zero
-        if (num_tiles == 0) A.ctl[A.parity ^ 1].live = 0u;
+    const int tiles = (N + kBlock - 1) / kBlock;
+    const int tpb = (tiles + (int)gridDim.x - 1) / (int)gridDim.x;   // tiles per workgroup
+    const int chunk = tpb * kBlock;
+    const int nseg = tpb ? (tiles + tpb - 1) / tpb : 0;
+    if (blockIdx.x == 0 && tid == 0) {
+        A.ctl[par ^ 1].nseg = (uint32_t)nseg;
+        A.ctl[par ^ 1].chunk = (uint32_t)chunk;
     }
-    // workgroups beyond the tile count would only burn ticket atomics (tail bounces are small)
-    if ((int)blockIdx.x >= num_tiles) return;
+    if ((int)blockIdx.x >= nseg) return;
     stage_materials(A, s_mats);
     const bool lds_mats = A.S.nmats <= kLdsMats;
     count_bounce(A, N);
-    uint32_t emit_cnt = 0;
-    lb::TileSeq q = lb::seq_start(A.fl.claimed != 0, &A.ctl[A.parity].ticket, s_ring, num_tiles);
-    while (q.tile != INT_MAX) {
-        lb::seq_step(q, &A.ctl[A.parity].ticket);
-        const int tile = q.tile;
-        const int i = tile * kBlock + (int)threadIdx.x;
+    const int first = (int)blockIdx.x * chunk;
+    const int last = min(N, first + chunk);
+    int seg = 0;
+    if (!FIRST) {   // segment of this workgroup's first logical path (binary search, uniform)
+        int lo = 0, hi = nseg_in - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (s_pre[mid] <= first) lo = mid; else hi = mid - 1;
+        }
+        seg = lo;
+    }
+    uint32_t kept = 0, emit_cnt = 0;
+    int k = 0;
+    for (int base = first; base < last; base += kBlock, ++k) {
+        const int i = base + tid;
         bool alive = false, emitted = false;
         PathReg p;
-        if (i < N) {
-            if (FIRST) raygen(A.cam, A.fl, A.tile, i, p);
-            else load_path(A.in, i, p);
+        if (i < last) {
+            if (FIRST) {
+                raygen(A.cam, A.fl, A.tile, i, p);
+            } else {
+                const int s = seg_walk(s_pre, nseg_in, seg, i);
+                load_path(A.in, s * chunk_in + (i - s_pre[s]), p);
+            }
             const Hit h = intersect_scene<MESH>(A.S, A.fl, p.o, p.d);
             const int iter = A.tile.iter_first + (SPP1 ? 0 : p.slot / A.tile.npix);
-            alive = lds_mats ? shade(A.S, A.fl, A.tile.depth, iter, A.fl.rng_pixel ? slot_pixel(A.cam, A.tile, p.slot) : i, p, h, s_mats)
-                             : shade(A.S, A.fl, A.tile.depth, iter, A.fl.rng_pixel ? slot_pixel(A.cam, A.tile, p.slot) : i, p, h, A.S.mats);
+            const int key = A.fl.rng_pixel ? slot_pixel(A.cam, A.tile, p.slot) : i;
+            alive = lds_mats ? shade(A.S, A.fl, A.tile.depth, iter, key, p, h, s_mats)
+                             : shade(A.S, A.fl, A.tile.depth, iter, key, p, h, A.S.mats);
             if (!alive) {
                 emitted = p.c.x != 0.0f || p.c.y != 0.0f || p.c.z != 0.0f;
                 retire<SPP1>(A, p);
             }
         }
         emit_cnt += (uint32_t)__popcll(__ballot(emitted));
-        const int pos = compact_tile(A, tile, num_tiles, alive, s_wc, &s_excl);
-        if (alive) store_path(A.out, pos, p);
-        lb::seq_advance(q, s_ring);
+        // in-tile ranks: wave ballot + mbcnt, 4 wave counts through LDS (double-buffered, so
+        // one barrier per tile: buffer k&1 was last read two tiles ago, before the last barrier)
+        const uint64_t m = __ballot(alive);
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        if (lane == 0) s_wc[k & 1][wave] = (uint32_t)__popcll(m);
+        __syncthreads();
+        const uint32_t w0 = s_wc[k & 1][0], w1 = s_wc[k & 1][1], w2 = s_wc[k & 1][2], w3 = s_wc[k & 1][3];
+        const uint32_t before = (wave > 0 ? w0 : 0u) + (wave > 1 ? w1 : 0u) + (wave > 2 ? w2 : 0u);
+        if (alive) store_path(A.out, first + (int)(kept + before + rank), p);
+        kept += (w0 + w1) + (w2 + w3);
+        if (!FIRST) seg = seg_walk(s_pre, nseg_in, seg, min(base + kBlock, last - 1));
     }
+    if (tid == 0) A.seg[(size_t)(par ^ 1) * kMaxSeg + blockIdx.x] = (int32_t)kept;
     flush_emissive(A, emit_cnt, &s_cnt);
 }
-
 // Stable compaction of the flagged survivors: tile = 256 threads x 4 paths (path order
 // k-major: path = tile*1024 + k*256 + t, so every load/store is wave-contiguous), wave ballot +
 // mbcnt ranks, 16 wave counts through LDS, decoupled look-back (lookback.h) over a persistent,
@@ -955,7 +1000,7 @@ struct pt_ctx {
     KArgs args{};
     int max_tiles = 0, max_t64 = 0;
     int grid_trace = 0, grid_compact = 0;
-    int grid_bounce[8] = {};   // per k_bounce variant (first, spp1, mesh): one wave of resident workgroups
+    int grid_bounce[2] = {};   // k_bounce (later, first bounce): one full wave of workgroups
     bool fused = true;   // pipeline: fused bounce kernel (default) or trace + compact
     uint64_t compact_launches = 0;   // parity of the look-back status / live-count words
     // owned device allocations
@@ -1238,9 +1283,10 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
     if (int rc = c->alloc(&A.image, (size_t)npix * 3)) return bail(rc);
     if (sh.spp > 1)
         if (int rc = c->alloc(&A.colbuf, (size_t)P * 3)) return bail(rc);
-    c->max_tiles = (int)((P + kBlock - 1) / kBlock);   // fused: 256-path tiles (split uses fewer)
+    c->max_tiles = (int)((P + kCompactTile - 1) / kCompactTile);   // k_compact_paths tiles
     if (int rc = c->alloc(&A.flags, (size_t)P)) return bail(rc);
     if (int rc = c->alloc(&A.ctl, 2)) return bail(rc);
+    if (int rc = c->alloc(&A.seg, (size_t)2 * kMaxSeg)) return bail(rc);
     if (int rc = c->alloc(&A.status, (size_t)2 * c->max_tiles)) return bail(rc);
     if (int rc = c->alloc(&c->stats, 1)) return bail(rc);
     A.stats = c->stats;
@@ -1251,6 +1297,7 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
     A.max_tiles = c->max_tiles;
     if ((e = hipMemset(A.image, 0, (size_t)npix * 3 * sizeof(float))) != hipSuccess ||
         (e = hipMemset(A.ctl, 0, 2 * sizeof(Ctl))) != hipSuccess ||
+        (e = hipMemset(A.seg, 0, (size_t)2 * kMaxSeg * sizeof(int32_t))) != hipSuccess ||
         (e = hipMemset(A.status, 0, (size_t)2 * c->max_tiles * sizeof(uint64_t))) != hipSuccess ||
         (e = hipMemset(c->stats, 0, sizeof(DevStats))) != hipSuccess)
         return bail(pt::fail(PT_ERR_HIP, std::string("hipMemset: ") + hipGetErrorString(e)));
@@ -1277,9 +1324,12 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
     c->grid_trace = std::max(1, std::min({(int)((P + kBlock - 1) / kBlock), cus * 8, A.emit_stride}));
     c->grid_compact = std::max(1, std::min(c->max_tiles, cus * resident_per_cu((const void*)k_compact_paths)));
-    for (int v = 0; v < 8; ++v) {   // each k_bounce variant launches with its own co-resident grid
-        const int per_cu = resident_per_cu((const void*)bounce_kernel(v & 4, v & 2, v & 1));
-        c->grid_bounce[v] = std::max(1, std::min({c->max_tiles, cus * per_cu, A.emit_stride}));
+    for (int f = 0; f < 2; ++f) {   // k_bounce: any grid is correct; one full wave of equal-work
+        int per_cu = 0;              // workgroups avoids a half-empty second wave
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bounce_kernel(f, sh.spp == 1, A.S.ntris > 0), kBlock,
+                                                         0) != hipSuccess || per_cu <= 0)
+            per_cu = 4;
+        c->grid_bounce[f] = std::max(1, std::min({cus * per_cu, kMaxSeg, A.emit_stride}));
     }
     if (const char* pl = std::getenv("PT_PIPELINE")) c->fused = std::string(pl) != "split";
     *out = c;
@@ -1319,7 +1369,7 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
         A.out = c->buf[cur ^ 1];
         int rc;
         if (!sorted && c->fused) {
-            rc = launch_k(c, bounce_kernel(b == 0, spp1, mesh), c->grid_bounce[(b == 0 ? 4 : 0) + (spp1 ? 2 : 0) + (mesh ? 1 : 0)], st,
+            rc = launch_k(c, bounce_kernel(b == 0, spp1, mesh), c->grid_bounce[b == 0], st,
                           b == 0 ? PT_KIND_FIRST_BOUNCE : PT_KIND_BOUNCE, A);
             if (rc) return rc;
             ++c->compact_launches;
