@@ -70,7 +70,7 @@ class Shard(C.Structure):
 class Stats(C.Structure):
     _fields_ = [("segments", C.c_uint64), ("passes", C.c_uint64), ("bounce_live", C.c_uint64 * 64),
                 ("emissive_hits", C.c_uint64), ("bounce_emit", C.c_uint64 * 64), ("device_error", C.c_uint32),
-                ("reserved", C.c_uint32)]
+                ("bound_mismatch", C.c_uint32)]
 
 
 assert C.sizeof(Geom) == 272 and C.sizeof(Material) == 48 and C.sizeof(Triangle) == 124

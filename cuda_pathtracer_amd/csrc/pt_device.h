@@ -71,6 +71,13 @@ struct DGeom {
     Affine xf;       // transform
     Affine itr;      // invTranspose
     float bmin[3], bmax[3];
+    // Conservative bounds test (pt_kernels.hip bound_geom), filled by pt_create: the unit cube's
+    // slabs widened to [slo, shi] = [-0.5 - mu_a, 0.5 + mu_a], the sphere's radius^2 widened to
+    // r2w = 0.25 + kappa (mu, kappa exceed the rounding of both the exact test and the bounds
+    // test for every ray origin in the scene), and tslack < 1, the relative slack that turns a
+    // lower bound on the hit parameter into one on the reference's world distance.
+    float slo[3], shi[3];
+    float r2w, tslack;
 };
 
 struct DMaterial {   // == pt_material

@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -49,7 +50,7 @@ struct Ctl {            // per-parity control block (16 B)
 };
 struct DevStats {
     unsigned long long segments, passes, bounce_live[64];
-    uint32_t err, pad;
+    uint32_t err, bound_mismatch;
 };
 
 struct SceneDev {
@@ -61,6 +62,7 @@ struct SceneDev {
     const DTexture* __restrict__ texs;
     int32_t ngeoms, nmats, ntris, nnodes;
     int32_t bvh_depth;     // deepest interior node (root = 0): bounds the traversal stack
+    float abs_slack;       // absolute slack of the world-distance lower bounds (bound_geom)
 };
 struct CamDev {
     float pos[3], view[3], up[3], right[3], pl[2];
@@ -73,6 +75,7 @@ struct FlagsDev {
     int32_t bvh_cull;
     int32_t claimed;   // tile schedule (lookback.h TileSeq)
     int32_t rng_pixel; // shading RNG keyed by global pixel (pt_flags.rng_key_pixel)
+    int32_t verify;    // PT_AMD_VERIFY_BOUNDS=1: re-run the plain closest-hit loop, count differences
 };
 struct TileDev {
     int32_t W, rank, world, npix, spp, P, depth, iter_first;
@@ -382,6 +385,155 @@ __device__ __forceinline__ Hit intersect_scene(const SceneDev& S, const FlagsDev
     return h;
 }
 
+// ---- bounded closest hit for analytic scenes (cubes + spheres) ------------------------------
+// computeIntersections evaluates the exact test of EVERY geom for every ray (≈170 VALU per cube:
+// two affine transforms, a correctly rounded normalize, six correctly rounded divisions, the
+// back-transform and a length).  Here a cheap pass over all geoms computes, per geom, a LOWER
+// BOUND on the reference's world distance (or "surely misses"), from the same inverse transform
+// against the unit cube / sphere WIDENED by more than the rounding error of either computation
+// (DGeom.slo/shi/r2w, sized on the host from the scene's extent).  Only the geoms whose bound is
+// not beyond an exactly evaluated hit are then run through the exact test above — per lane, with
+// the geom read from LDS — in increasing-bound order.  A skipped geom either misses exactly or has
+// an exact distance strictly larger than an evaluated hit, so the selected hit (minimum t, lowest
+// index on ties, pathtrace.cu:284-288) is the reference's bit for bit.  Typically one exact test
+// per ray instead of one per geom.  PT_AMD_VERIFY_BOUNDS=1 re-runs the plain loop and counts any
+// difference (pt_stats_t.bound_mismatch).
+constexpr int kLdsGeoms = 32;
+struct alignas(16) LGeom {   // what the exact tests read: 31 words, one 128-byte LDS row
+    Affine inv, xf;
+    int32_t type;
+};
+constexpr float kInf = __builtin_inff();
+
+__device__ __forceinline__ void stage_geoms(const SceneDev& S, LGeom* s_geoms) {
+    if (S.ngeoms > kLdsGeoms) return;
+    for (int j = threadIdx.x; j < S.ngeoms; j += blockDim.x) {
+        const DGeom& g = S.geoms[j];
+        s_geoms[j].inv = g.inv;
+        s_geoms[j].xf = g.xf;
+        s_geoms[j].type = g.type;
+    }
+}
+
+// Lower bound on the exact test's world distance for geom g (before the scene's absolute slack),
+// +inf when the exact test surely misses.  Rounding here is irrelevant: only the widened bounds,
+// the relative slack and the comparisons' direction matter (NaNs fall through to "candidate").
+template <class G>
+__device__ __forceinline__ float bound_geom(const G& g, f3 ro, f3 rd, float rl) {
+    const f3 qo = xform_point(g.inv, ro);
+    const f3 qv = xform_vector(g.inv, rd);   // un-normalized: world parameter = object parameter
+    const float a = dot(qv, qv);
+    float lo;
+    if (g.type == PT_GEOM_CUBE) {
+        float E = -kInf, X = kInf;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const float r = __builtin_amdgcn_rcpf(at(qv, k));
+            const float t1 = (g.slo[k] - at(qo, k)) * r, t2 = (g.shi[k] - at(qo, k)) * r;
+            E = fmaxf(E, fminf(t1, t2));
+            X = fminf(X, fmaxf(t1, t2));
+        }
+        if (E > X || X < 0.0f) return kInf;
+        lo = fmaxf(E, 0.0f);
+    } else if (g.type == PT_GEOM_SPHERE) {
+        const float b = dot(qo, qv);
+        const float disc = b * b - a * (dot(qo, qo) - g.r2w);
+        if (disc < 0.0f) return kInf;
+        const float sq = __builtin_amdgcn_sqrtf(disc), ia = __builtin_amdgcn_rcpf(a);
+        const float eps = (fabsf(b) + sq) * ia * 0x1p-16f;
+        if ((sq - b) * ia < -eps) return kInf;
+        lo = fmaxf((-b - sq) * ia - eps, 0.0f);
+    } else {
+        return kInf;
+    }
+    // pointOnRay pulls the hit back by 1e-4 along the NORMALIZED object direction: 1e-4/|qv| here
+    const float back = 1.0002e-4f * __builtin_amdgcn_rsqf(a);
+    return fmaxf(lo - back, 0.0f) * rl * g.tslack;
+}
+
+// Exact test of one geom (boxIntersectionTest / sphereIntersectionTest) from its LDS row.
+__device__ __forceinline__ float exact_geom(const LGeom& L, f3 ro, f3 rd, int& code, f3& obj, bool& outside) {
+    code = -1;
+    outside = true;
+    if (L.type == PT_GEOM_CUBE) return box_test(L, ro, rd, code);
+    if (L.type == PT_GEOM_SPHERE) return sphere_test(L, ro, rd, obj, outside);
+    return -1.0f;
+}
+
+__device__ __forceinline__ Hit intersect_bounded(const SceneDev& S, const FlagsDev& fl, const LGeom* s_geoms, f3 ro,
+                                                 f3 rd) {
+    const float rl = __builtin_amdgcn_sqrtf(dot(rd, rd));
+    bool plain = !(rl > 0.5f && rl < 2.0f);   // NaN / degenerate direction: the plain loop
+    float t_min = kFLT_MAX;
+    int hit_geom = -1, best_code = -1;
+    f3 best_obj = F3(0, 0, 0);
+    bool best_outside = true;
+    if (!plain) {
+        // pass 1: the three smallest lower bounds (scene data wave-uniform: scalar loads)
+        float lo1 = kInf, lo2 = kInf, lo3 = kInf;
+        int g1 = -1, g2 = -1;
+        const auto* G = as_const(S.geoms);
+        for (int i = 0; i < S.ngeoms; ++i) {
+            const float lo = bound_geom(G[i], ro, rd, rl) - S.abs_slack;
+            if (lo < lo3) {
+                if (lo < lo2) {
+                    lo3 = lo2;
+                    if (lo < lo1) { lo2 = lo1; g2 = g1; lo1 = lo; g1 = i; }
+                    else { lo2 = lo; g2 = i; }
+                } else {
+                    lo3 = lo;
+                }
+            }
+        }
+        // pass 2: exact tests in increasing-bound order while a bound does not exceed the best hit
+        auto take = [&](int gi) {
+            int code;
+            f3 obj = F3(0, 0, 0);
+            bool outside;
+            const float t = exact_geom(s_geoms[gi], ro, rd, code, obj, outside);
+            if (t > 0.0f && (t_min > t || (t == t_min && hit_geom >= 0 && gi < hit_geom))) {
+                t_min = t; hit_geom = gi; best_code = code; best_obj = obj; best_outside = outside;
+            }
+        };
+        if (g1 >= 0) take(g1);
+        if (g2 >= 0 && lo2 <= t_min) take(g2);
+        plain = lo3 <= t_min;   // a third candidate: the plain loop (rare)
+    }
+    if (plain) return intersect_scene<false>(S, fl, ro, rd);
+    Hit h;
+    if (hit_geom < 0) {
+        h.t = -1.0f;
+        h.mat = 0;
+        h.n = F3(0, 0, 0);
+        h.u = h.v = 0.f;
+        return h;
+    }
+    const DGeom& g = S.geoms[hit_geom];
+    h.t = t_min;
+    h.mat = g.material;
+    h.u = h.v = 0.f;
+    h.n = g.type == PT_GEOM_CUBE ? box_normal(g, best_code) : sphere_normal(g, best_obj, best_outside);
+    return h;
+}
+
+// The closest hit of the kernels: bounded for analytic scenes that fit the LDS geom table.
+// CHECK: compiled-in diagnostic re-run (k_trace and the sorted pipeline only, so the fused
+// kernel's code stays small): verify with PT_PIPELINE=split, whose rays are the fused kernel's.
+template <bool MESH, bool CHECK>
+__device__ __forceinline__ Hit closest_hit(const SceneDev& S, const FlagsDev& fl, const LGeom* s_geoms, f3 ro, f3 rd,
+                                           uint32_t* mismatch) {
+    if (MESH || S.ngeoms > kLdsGeoms) return intersect_scene<MESH>(S, fl, ro, rd);
+    const Hit h = intersect_bounded(S, fl, s_geoms, ro, rd);
+    if (CHECK && fl.verify) {
+        const Hit r = intersect_scene<false>(S, fl, ro, rd);
+        if (__float_as_uint(h.t) != __float_as_uint(r.t) || h.mat != r.mat ||
+            __float_as_uint(h.n.x) != __float_as_uint(r.n.x) || __float_as_uint(h.n.y) != __float_as_uint(r.n.y) ||
+            __float_as_uint(h.n.z) != __float_as_uint(r.n.z))
+            atomicAdd(mismatch, 1u);
+    }
+    return h;
+}
+
 // ------------------------------------------------------------------------------------------
 // Shading (shadeMaterials pathtrace.cu:300-344, scatterRay interactions.cu:43-85)
 // ------------------------------------------------------------------------------------------
@@ -603,9 +755,11 @@ __device__ __forceinline__ void store_survivor(const PathSoA& B, int i, const Pa
 template <bool FIRST, bool SPP1, bool MESH>
 __global__ __launch_bounds__(kBlock) void k_trace(const KArgs A) {
     __shared__ DMaterial s_mats[kLdsMats];
+    __shared__ LGeom s_geoms[MESH ? 1 : kLdsGeoms];
     __shared__ uint32_t s_cnt;
     const int N = live_count(A);
     if ((int)blockIdx.x * kBlock >= N) return;
+    if (!MESH) stage_geoms(A.S, s_geoms);
     stage_materials(A, s_mats);
     const bool lds_mats = A.S.nmats <= kLdsMats;
     count_bounce(A, N);
@@ -617,7 +771,7 @@ __global__ __launch_bounds__(kBlock) void k_trace(const KArgs A) {
             PathReg p;
             if (FIRST) raygen(A.cam, A.fl, A.tile, i, p);
             else load_path(A.in, i, p);
-            const Hit h = intersect_scene<MESH>(A.S, A.fl, p.o, p.d);
+            const Hit h = closest_hit<MESH, true>(A.S, A.fl, s_geoms, p.o, p.d, &A.stats->bound_mismatch);
             const int iter = A.tile.iter_first + (SPP1 ? 0 : p.slot / A.tile.npix);
             const bool alive = lds_mats ? shade(A.S, A.fl, A.tile.depth, iter, A.fl.rng_pixel ? slot_pixel(A.cam, A.tile, p.slot) : i, p, h, s_mats)
                                         : shade(A.S, A.fl, A.tile.depth, iter, A.fl.rng_pixel ? slot_pixel(A.cam, A.tile, p.slot) : i, p, h, A.S.mats);
@@ -687,6 +841,7 @@ __device__ __forceinline__ int seg_walk(const int32_t* s_pre, int nseg, int s, i
 template <bool FIRST, bool SPP1, bool MESH>
 __global__ __launch_bounds__(kBlock) void k_bounce(const KArgs A) {
     __shared__ DMaterial s_mats[kLdsMats];
+    __shared__ LGeom s_geoms[MESH ? 1 : kLdsGeoms];
     __shared__ int32_t s_pre[FIRST ? 1 : kMaxSeg + 1];
     __shared__ uint32_t s_wc[2][4];
     __shared__ uint32_t s_cnt;
@@ -709,6 +864,7 @@ __global__ __launch_bounds__(kBlock) void k_bounce(const KArgs A) {
         A.ctl[par ^ 1].chunk = (uint32_t)chunk;
     }
     if ((int)blockIdx.x >= nseg) return;
+    if (!MESH) stage_geoms(A.S, s_geoms);
     stage_materials(A, s_mats);
     const bool lds_mats = A.S.nmats <= kLdsMats;
     count_bounce(A, N);
@@ -736,7 +892,7 @@ __global__ __launch_bounds__(kBlock) void k_bounce(const KArgs A) {
                 const int s = seg_walk(s_pre, nseg_in, seg, i);
                 load_path(A.in, s * chunk_in + (i - s_pre[s]), p);
             }
-            const Hit h = intersect_scene<MESH>(A.S, A.fl, p.o, p.d);
+            const Hit h = closest_hit<MESH, false>(A.S, A.fl, s_geoms, p.o, p.d, &A.stats->bound_mismatch);
             const int iter = A.tile.iter_first + (SPP1 ? 0 : p.slot / A.tile.npix);
             const int key = A.fl.rng_pixel ? slot_pixel(A.cam, A.tile, p.slot) : i;
             alive = lds_mats ? shade(A.S, A.fl, A.tile.depth, iter, key, p, h, s_mats)
@@ -863,16 +1019,20 @@ __global__ __launch_bounds__(kBlock) void k_raygen(const KArgs A) {
 // yields every path's stable sorted position base.
 __global__ __launch_bounds__(kBlock) void k_isect_hist(const KArgs A, int32_t* __restrict__ keys,
                                                         int32_t* __restrict__ hist, int max_t64) {
+    __shared__ LGeom s_geoms[kLdsGeoms];
     const int N = A.n_fixed >= 0 ? A.n_fixed : (int)A.ctl[A.parity].live;
     const int lane = threadIdx.x & 63;
     const int waves = gridDim.x * (blockDim.x >> 6);
+    stage_geoms(A.S, s_geoms);
+    __syncthreads();
     for (int t64 = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); t64 < max_t64; t64 += waves) {
         const int i = t64 * 64 + lane;
         int key = -1;
         if (i < N) {
             const f3 o = F3(A.in.ox[i], A.in.oy[i], A.in.oz[i]);
             const f3 d = F3(A.in.dx[i], A.in.dy[i], A.in.dz[i]);
-            const Hit h = A.S.ntris > 0 ? intersect_scene<true>(A.S, A.fl, o, d) : intersect_scene<false>(A.S, A.fl, o, d);
+            const Hit h = A.S.ntris > 0 ? closest_hit<true, true>(A.S, A.fl, s_geoms, o, d, &A.stats->bound_mismatch)
+                                        : closest_hit<false, true>(A.S, A.fl, s_geoms, o, d, &A.stats->bound_mismatch);
             A.hit.t[i] = h.t;
             A.hit.nx[i] = h.n.x; A.hit.ny[i] = h.n.y; A.hit.nz[i] = h.n.z;
             A.hit.u[i] = h.u; A.hit.v[i] = h.v;
@@ -1013,6 +1173,9 @@ struct pt_ctx {
     bool profiling = false;
     std::vector<ProfEv> events;   // pool; the first `ev_used` are recorded and unread
     size_t ev_used = 0;
+    std::vector<DGeom> hgeoms;    // host copy of the geom table (bounds re-derived by pt_set_flags)
+    DGeom* d_geoms = nullptr;
+    double scene_ext = 0.0;       // max |coordinate| over every surface and the camera position
 
     ~pt_ctx() {
         for (auto& e : events) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
@@ -1045,6 +1208,8 @@ void set_flags_dev(pt_ctx* c, const pt_flags& f) {
     c->args.fl.bvh_cull = f.bvh_cull;
     c->args.fl.claimed = f.shared_gpu;
     c->args.fl.rng_pixel = f.rng_key_pixel;
+    const char* vb = std::getenv("PT_AMD_VERIFY_BOUNDS");
+    c->args.fl.verify = vb && std::strcmp(vb, "1") == 0;
 }
 
 float bits_to_float(int32_t v) {
@@ -1059,6 +1224,39 @@ Affine to_affine(const float* m) {   // glm column-major 4x4 -> 3x4 + the exact 
         for (int r = 0; r < 3; ++r) a.c[col][r] = m[4 * col + r];
     for (int r = 0; r < 3; ++r) a.z3[r] = m[12 + r] * 0.0f;
     return a;
+}
+
+// Widened bounds of the bounded closest-hit pass (bound_geom), sized from R = the largest
+// |coordinate| any ray origin can have: a surface point (+1e-4 offsets) or the camera lens.
+//   qo = inv * ro is computed with <= 4 ulp of S_a = sum_i |inv_ia| R + |inv_3a| absolute error by
+// either side (exact test, bounds test), the exact slab parameters add <= 5 ulp of (S_a + 0.5):
+// mu_a = 2^-18 (S_a + 1) is >= 10x that.  The sphere's b^2 - a c cancels to <= 2^-20 (S + 1)^2:
+// kappa = 2^-16 (S + 1)^2.  tslack covers the back-transform (transform * inverse != I in float)
+// and the rounding of the reference's length(); abs_slack its absolute part.
+void update_bounds(pt_ctx* c, float aperture) {
+    const double R = c->scene_ext + std::fabs((double)aperture) + 1e-2;
+    for (DGeom& d : c->hgeoms) {
+        double smax = 0.0;
+        for (int a = 0; a < 3; ++a) {
+            double S = std::fabs((double)d.inv.c[3][a]);
+            for (int i = 0; i < 3; ++i) S += std::fabs((double)d.inv.c[i][a]) * R;
+            const double mu = std::ldexp(S + 1.0, -18);
+            d.slo[a] = (float)(-0.5 - mu);
+            d.shi[a] = (float)(0.5 + mu);
+            smax = std::max(smax, S);
+        }
+        d.r2w = (float)(0.25 + std::ldexp((smax + 1.0) * (smax + 1.0), -16));
+        double dev = 0.0;   // Frobenius norm of xf_lin * inv_lin - I
+        for (int r = 0; r < 3; ++r)
+            for (int col = 0; col < 3; ++col) {
+                double m = 0.0;
+                for (int k = 0; k < 3; ++k) m += (double)d.xf.c[k][r] * (double)d.inv.c[col][k];
+                m -= r == col ? 1.0 : 0.0;
+                dev += m * m;
+            }
+        d.tslack = (float)(1.0 - 4.0 * std::sqrt(dev) - std::ldexp(1.0, -14));
+    }
+    c->args.S.abs_slack = (float)std::ldexp(R + 1.0, -17);
 }
 
 int alloc_paths(pt_ctx* c, PathSoA& B, size_t P) {
@@ -1179,9 +1377,32 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
         d.itr = to_affine(g.inv_transpose);
         for (int k = 0; k < 3; ++k) { d.bmin[k] = g.min_bound[k]; d.bmax[k] = g.max_bound[k]; }
     }
+    {   // scene extent: every surface point (cube/sphere corners, mesh vertices) and the camera
+        double ext = 0.0;
+        for (int k = 0; k < 3; ++k) ext = std::max(ext, std::fabs((double)S.camera.position[k]));
+        for (const pt_geom& g : S.geoms) {
+            if (g.type != PT_GEOM_CUBE && g.type != PT_GEOM_SPHERE) continue;
+            for (int corner = 0; corner < 8; ++corner) {
+                const double p[3] = {corner & 1 ? 0.5 : -0.5, corner & 2 ? 0.5 : -0.5, corner & 4 ? 0.5 : -0.5};
+                for (int r = 0; r < 3; ++r) {
+                    double v = g.transform[12 + r];
+                    for (int k = 0; k < 3; ++k) v += (double)g.transform[4 * k + r] * p[k];
+                    ext = std::max(ext, std::fabs(v));
+                }
+            }
+        }
+        for (const pt_triangle& t : S.triangles)
+            for (int v = 0; v < 3; ++v)
+                for (int k = 0; k < 3; ++k) ext = std::max(ext, std::fabs((double)t.v[v][k]));
+        c->scene_ext = ext;
+    }
+    c->hgeoms = dg;
+    update_bounds(c, c->flags.aperture);
+    dg = c->hgeoms;
     DGeom* d_geoms;
     DMaterial* d_mats;
     if (int rc = c->alloc(&d_geoms, dg.size())) return bail(rc);
+    c->d_geoms = d_geoms;
     if (int rc = c->alloc(&d_mats, S.materials.size())) return bail(rc);
     if ((e = hipMemcpy(d_geoms, dg.data(), dg.size() * sizeof(DGeom), hipMemcpyHostToDevice)) != hipSuccess ||
         (e = hipMemcpy(d_mats, S.materials.data(), S.materials.size() * sizeof(DMaterial), hipMemcpyHostToDevice)) != hipSuccess)
@@ -1346,7 +1567,13 @@ int pt_destroy(pt_ctx* c) {
 
 int pt_set_flags(pt_ctx* c, const pt_flags* f) {
     if (!c || !f) return pt::fail(PT_ERR_ARG, "null argument");
+    const bool lens = f->aperture != c->flags.aperture;
     set_flags_dev(c, *f);
+    if (lens) {   // the camera lens bounds the ray origins: re-derive the widened bounds
+        update_bounds(c, f->aperture);
+        HIP_TRY(hipDeviceSynchronize());
+        HIP_TRY(hipMemcpy(c->d_geoms, c->hgeoms.data(), c->hgeoms.size() * sizeof(DGeom), hipMemcpyHostToDevice));
+    }
     return PT_OK;
 }
 
@@ -1487,6 +1714,7 @@ int pt_stats(pt_ctx* c, pt_stats_t* out) {
         out->emissive_hits += e;
     }
     out->device_error = s.err;
+    out->bound_mismatch = s.bound_mismatch;
     return s.err ? pt::fail(PT_ERR_DEVICE, "device-side look-back spin bound was hit") : PT_OK;
 }
 

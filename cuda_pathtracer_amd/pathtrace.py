@@ -244,7 +244,7 @@ class PathTracer:
         return {"segments": int(s.segments), "passes": int(s.passes),
                 "bounce_live": [int(s.bounce_live[k]) for k in range(depth)],
                 "bounce_emit": [int(s.bounce_emit[k]) for k in range(depth)],
-                "emissive_hits": int(s.emissive_hits)}
+                "emissive_hits": int(s.emissive_hits), "bound_mismatch": int(s.bound_mismatch)}
 
     def profile(self, on: bool = True) -> None:
         check_pt(lib().pt_profile_enable(self._h, int(on)))

@@ -120,6 +120,28 @@ def random_triangles(out_dir, n=100_000, res=(3840, 2160), depth=32, seed=5) -> 
     return _write(out_dir, name, scene)
 
 
+def random_primitives(out_dir, n=24, res=(640, 480), depth=8, seed=7) -> str:
+    """Stress scene for the bounded closest-hit pass (not a BASELINE workload): the Cornell shell
+    plus n cubes and spheres with random rotations and strongly non-uniform scales (thin slabs,
+    needles), overlapping each other and the walls; diffuse, mirror and glass materials."""
+    rng = np.random.default_rng(seed)
+    mats = dict(CORNELL_MATERIALS)
+    mats["glass"] = {"TYPE": "Refractive", "RGB": [0.98, 0.98, 0.98], "SPECRGB": [0.98, 0.98, 0.98],
+                     "REFRACTIVE": 1.0, "IOR": 1.5}
+    cycle = ["diffuse_white", "specular_white", "glass", "diffuse_red", "diffuse_green"]
+    objs = _room()
+    for k in range(n):
+        scale = np.exp(rng.uniform(np.log(0.02), np.log(4.0), 3))
+        if k % 3 == 0:
+            scale[:] = scale[0]
+        objs.append({"TYPE": "sphere" if k % 2 else "cube", "MATERIAL": cycle[k % len(cycle)],
+                     "TRANS": [float(v) for v in rng.uniform((-4.5, 0.0, -4.5), (4.5, 9.5, 3.0))],
+                     "ROTAT": [float(v) for v in rng.uniform(0.0, 360.0, 3)],
+                     "SCALE": [float(v) for v in scale]})
+    scene = {"Materials": mats, "Camera": _camera(res, depth, 5000, "random_primitives"), "Objects": objs}
+    return _write(out_dir, f"random_primitives_{seed}", scene)
+
+
 CONFIGS = {
     "cornell": None,   # the bundled scene itself (configs[1])
     "cornell_hd_sorted": cornell_hd,

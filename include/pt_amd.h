@@ -143,7 +143,8 @@ typedef struct pt_stats_t {
     uint64_t emissive_hits;       /* paths that terminated with non-zero radiance (framebuffer adds) */
     uint64_t bounce_emit[64];     /* of those, per bounce */
     uint32_t device_error;        /* nonzero: a device-side bound was hit */
-    uint32_t reserved;
+    uint32_t bound_mismatch;      /* PT_AMD_VERIFY_BOUNDS=1 only: closest hits where the bounded
+                                     pass differed from the plain per-geom loop (must stay 0) */
 } pt_stats_t;
 
 const char* pt_last_error(void);
