@@ -76,8 +76,17 @@ struct DGeom {
     // r2w = 0.25 + kappa (mu, kappa exceed the rounding of both the exact test and the bounds
     // test for every ray origin in the scene), and tslack < 1, the relative slack that turns a
     // lower bound on the hit parameter into one on the reference's world distance.
+    //   A sphere ray whose origin is outside the exact sphere by more than
+    // kappa_ray = (|qo|^2 + 1) (kcs |ro|_inf + kc3) and moves away from its centre surely misses
+    // (the ray leaving the sphere it just hit; the widened radius alone cannot tell).
+    //   Axis-aligned cubes (bkind 3: the Cornell walls, incl. 90-degree rotations) are bounded by
+    // their widened WORLD box [wlo, whi] (of the exact inverse of `inv`): a 6-plane slab test on the
+    // world ray, with `back` >= 1e-4 * (largest stretch of the transform) for pointOnRay's pull-back.
     float slo[3], shi[3];
     float r2w, tslack;
+    float kcs, kc3;
+    float wlo[3], whi[3], back;
+    int32_t bkind;   // 0: never hit (mesh), 1: oriented cube, 2: sphere, 3: world-box cube
 };
 
 struct DMaterial {   // == pt_material

@@ -419,12 +419,25 @@ __device__ __forceinline__ void stage_geoms(const SceneDev& S, LGeom* s_geoms) {
 // +inf when the exact test surely misses.  Rounding here is irrelevant: only the widened bounds,
 // the relative slack and the comparisons' direction matter (NaNs fall through to "candidate").
 template <class G>
-__device__ __forceinline__ float bound_geom(const G& g, f3 ro, f3 rd, float rl) {
+__device__ __forceinline__ float bound_geom(const G& g, f3 ro, f3 rd, f3 invd, float rl, float rinf) {
+    const int kind = g.bkind;
+    if (kind == 3) {   // world box: t = (plane - o) / d (subtract first: exact zeros in d stay safe)
+        float E = -kInf, X = kInf;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const float t1 = (g.wlo[k] - at(ro, k)) * at(invd, k), t2 = (g.whi[k] - at(ro, k)) * at(invd, k);
+            E = fmaxf(E, fminf(t1, t2));
+            X = fminf(X, fmaxf(t1, t2));
+        }
+        if (E > X || X < 0.0f) return kInf;
+        return fmaxf(fmaxf(E, 0.0f) * rl - g.back, 0.0f) * g.tslack;
+    }
+    if (kind == 0) return kInf;
     const f3 qo = xform_point(g.inv, ro);
     const f3 qv = xform_vector(g.inv, rd);   // un-normalized: world parameter = object parameter
     const float a = dot(qv, qv);
     float lo;
-    if (g.type == PT_GEOM_CUBE) {
+    if (kind == 1) {
         float E = -kInf, X = kInf;
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
@@ -435,29 +448,65 @@ __device__ __forceinline__ float bound_geom(const G& g, f3 ro, f3 rd, float rl) 
         }
         if (E > X || X < 0.0f) return kInf;
         lo = fmaxf(E, 0.0f);
-    } else if (g.type == PT_GEOM_SPHERE) {
+    } else {
         const float b = dot(qo, qv);
-        const float disc = b * b - a * (dot(qo, qo) - g.r2w);
+        const float q2 = dot(qo, qo);
+        if (b > 0.0f && q2 - 0.25f > (q2 + 1.0f) * (g.kcs * rinf + g.kc3)) return kInf;   // departing
+        const float disc = b * b - a * (q2 - g.r2w);
         if (disc < 0.0f) return kInf;
         const float sq = __builtin_amdgcn_sqrtf(disc), ia = __builtin_amdgcn_rcpf(a);
         const float eps = (fabsf(b) + sq) * ia * 0x1p-16f;
         if ((sq - b) * ia < -eps) return kInf;
         lo = fmaxf((-b - sq) * ia - eps, 0.0f);
-    } else {
-        return kInf;
     }
     // pointOnRay pulls the hit back by 1e-4 along the NORMALIZED object direction: 1e-4/|qv| here
     const float back = 1.0002e-4f * __builtin_amdgcn_rsqf(a);
     return fmaxf(lo - back, 0.0f) * rl * g.tslack;
 }
 
-// Exact test of one geom (boxIntersectionTest / sphereIntersectionTest) from its LDS row.
-__device__ __forceinline__ float exact_geom(const LGeom& L, f3 ro, f3 rd, int& code, f3& obj, bool& outside) {
+// Exact test of one geom from its LDS row: boxIntersectionTest (intersections.cu:3-58) and
+// sphereIntersectionTest (:60-115) with their common prologue (object-space ray) and epilogue
+// (pointOnRay, back-transform, world length) shared, so a wave whose lanes test different geom
+// types runs only the type-specific middle twice.  Same operations, same order: bit-identical.
+__device__ __forceinline__ float exact_geom(const LGeom& L, f3 r_o, f3 r_d, int& code, f3& obj, bool& outside) {
     code = -1;
     outside = true;
-    if (L.type == PT_GEOM_CUBE) return box_test(L, ro, rd, code);
-    if (L.type == PT_GEOM_SPHERE) return sphere_test(L, ro, rd, obj, outside);
-    return -1.0f;
+    const int type = L.type;
+    if (type != PT_GEOM_CUBE && type != PT_GEOM_SPHERE) return -1.0f;
+    const f3 qo = xform_point(L.inv, r_o);
+    const f3 qd = normalize(xform_vector(L.inv, r_d));
+    float t;
+    bool hit;
+    if (type == PT_GEOM_CUBE) {
+        float tmin = -1e38f, tmax = 1e38f;
+        int nmin = -1, nmax = -1;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            const float qa = at(qd, a), oa = at(qo, a);
+            const float t1 = (-0.5f - oa) / qa;
+            const float t2 = (+0.5f - oa) / qa;
+            const float ta = gmin(t1, t2), tb = gmax(t1, t2);
+            const int c = 2 * a + (t2 < t1 ? 0 : 1);
+            if (ta > 0 && ta > tmin) { tmin = ta; nmin = c; }
+            if (tb < tmax) { tmax = tb; nmax = c; }
+        }
+        hit = tmax >= tmin && tmax > 0;
+        if (tmin <= 0) { tmin = tmax; nmin = nmax; }
+        t = tmin;
+        code = nmin;
+    } else {
+        const float vdd = dot(qo, qd);
+        const float radicand = vdd * vdd - (dot(qo, qo) - 0.25f);
+        const float sq = sqrtf(radicand);
+        const float t1 = -vdd + sq, t2 = -vdd - sq;
+        hit = !(radicand < 0) && !(t1 < 0 && t2 < 0);
+        if (t1 > 0 && t2 > 0) { t = gmin(t1, t2); outside = true; }
+        else { t = gmax(t1, t2); outside = false; }
+    }
+    if (!hit) return -1.0f;
+    obj = point_on_ray(qo, qd, t);
+    const f3 ip = xform_point(L.xf, obj);
+    return length(r_o - ip);
 }
 
 __device__ __forceinline__ Hit intersect_bounded(const SceneDev& S, const FlagsDev& fl, const LGeom* s_geoms, f3 ro,
@@ -472,18 +521,19 @@ __device__ __forceinline__ Hit intersect_bounded(const SceneDev& S, const FlagsD
         // pass 1: the three smallest lower bounds (scene data wave-uniform: scalar loads)
         float lo1 = kInf, lo2 = kInf, lo3 = kInf;
         int g1 = -1, g2 = -1;
+        uint32_t cand = 0u;   // every geom with a finite bound
+        const float rinf = fmaxf(fmaxf(fabsf(ro.x), fabsf(ro.y)), fabsf(ro.z));
+        const f3 invd = F3(__builtin_amdgcn_rcpf(rd.x), __builtin_amdgcn_rcpf(rd.y), __builtin_amdgcn_rcpf(rd.z));
         const auto* G = as_const(S.geoms);
         for (int i = 0; i < S.ngeoms; ++i) {
-            const float lo = bound_geom(G[i], ro, rd, rl) - S.abs_slack;
-            if (lo < lo3) {
-                if (lo < lo2) {
-                    lo3 = lo2;
-                    if (lo < lo1) { lo2 = lo1; g2 = g1; lo1 = lo; g1 = i; }
-                    else { lo2 = lo; g2 = i; }
-                } else {
-                    lo3 = lo;
-                }
-            }
+            const float lo = bound_geom(G[i], ro, rd, invd, rl, rinf) - S.abs_slack;
+            cand |= lo < kInf ? (1u << i) : 0u;
+            const bool c1 = lo < lo1, c2 = lo < lo2, c3 = lo < lo3;
+            lo3 = c2 ? lo2 : (c3 ? lo : lo3);
+            lo2 = c1 ? lo1 : (c2 ? lo : lo2);
+            g2 = c1 ? g1 : (c2 ? i : g2);
+            lo1 = c1 ? lo : lo1;
+            g1 = c1 ? i : g1;
         }
         // pass 2: exact tests in increasing-bound order while a bound does not exceed the best hit
         auto take = [&](int gi) {
@@ -497,7 +547,13 @@ __device__ __forceinline__ Hit intersect_bounded(const SceneDev& S, const FlagsD
         };
         if (g1 >= 0) take(g1);
         if (g2 >= 0 && lo2 <= t_min) take(g2);
-        plain = lo3 <= t_min;   // a third candidate: the plain loop (rare)
+        if (lo3 <= t_min) {   // a third candidate (rare): every remaining geom with a finite bound
+            uint32_t m = cand & ~(1u << g1) & ~(1u << g2);
+            while (m) {
+                take(__builtin_ctz(m));
+                m &= m - 1u;
+            }
+        }
     }
     if (plain) return intersect_scene<false>(S, fl, ro, rd);
     Hit h;
@@ -1246,6 +1302,61 @@ void update_bounds(pt_ctx* c, float aperture) {
             smax = std::max(smax, S);
         }
         d.r2w = (float)(0.25 + std::ldexp((smax + 1.0) * (smax + 1.0), -16));
+        // departing-ray test: |qo_exact - qo_bound| <= 2^-21 S_ray (S_ray <= cs |ro|_inf + c3) moves
+        // |qo|^2 by <= 2^-20 |qo| S_ray; the dot products add <= 2^-21 |qo|^2.  kappa_ray is >= 6x that.
+        double cs = 0.0, c3 = 0.0;
+        for (int a = 0; a < 3; ++a) {
+            cs = std::max(cs, std::fabs((double)d.inv.c[0][a]) + std::fabs((double)d.inv.c[1][a]) +
+                                  std::fabs((double)d.inv.c[2][a]));
+            c3 = std::max(c3, std::fabs((double)d.inv.c[3][a]));
+        }
+        d.kcs = (float)std::ldexp(cs, -18);
+        d.kc3 = (float)std::ldexp(c3 + 2.0, -18);
+        d.bkind = d.type == PT_GEOM_CUBE ? 1 : (d.type == PT_GEOM_SPHERE ? 2 : 0);
+        if (d.type == PT_GEOM_CUBE) {   // world box of the widened cube, if the transform is axis-aligned
+            double M[3][3], X[3][3];
+            for (int r = 0; r < 3; ++r)
+                for (int k = 0; k < 3; ++k) M[r][k] = d.inv.c[k][r];   // q = M p + t
+            const double det = M[0][0] * (M[1][1] * M[2][2] - M[1][2] * M[2][1]) -
+                               M[0][1] * (M[1][0] * M[2][2] - M[1][2] * M[2][0]) +
+                               M[0][2] * (M[1][0] * M[2][1] - M[1][1] * M[2][0]);
+            bool aligned = std::fabs(det) > 0.0;
+            if (aligned) {
+                for (int r = 0; r < 3; ++r)
+                    for (int k = 0; k < 3; ++k) {
+                        const int r1 = (k + 1) % 3, r2 = (k + 2) % 3, k1 = (r + 1) % 3, k2 = (r + 2) % 3;
+                        X[r][k] = (M[r1][k1] * M[r2][k2] - M[r1][k2] * M[r2][k1]) / det;   // adjugate / det
+                    }
+                for (int r = 0; r < 3 && aligned; ++r) {
+                    double big = 0.0;
+                    for (int k = 0; k < 3; ++k) big = std::max(big, std::fabs(X[r][k]));
+                    int n = 0;
+                    for (int k = 0; k < 3; ++k) n += std::fabs(X[r][k]) > 1e-6 * big;
+                    aligned = n == 1;
+                }
+            }
+            if (aligned) {
+                double stretch = 0.0, lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
+                for (int corner = 0; corner < 8; ++corner) {
+                    double q[3];
+                    for (int k = 0; k < 3; ++k) q[k] = ((corner >> k) & 1 ? d.shi[k] : d.slo[k]) - d.inv.c[3][k];
+                    for (int r = 0; r < 3; ++r) {
+                        const double v = X[r][0] * q[0] + X[r][1] * q[1] + X[r][2] * q[2];
+                        lo[r] = std::min(lo[r], v);
+                        hi[r] = std::max(hi[r], v);
+                    }
+                }
+                for (int r = 0; r < 3; ++r)
+                    for (int k = 0; k < 3; ++k) stretch = std::max(stretch, std::fabs(X[r][k]));
+                const double pad = std::ldexp(R + 1.0, -18);
+                for (int r = 0; r < 3; ++r) {
+                    d.wlo[r] = (float)(lo[r] - pad - std::ldexp(std::fabs(lo[r]), -18));
+                    d.whi[r] = (float)(hi[r] + pad + std::ldexp(std::fabs(hi[r]), -18));
+                }
+                d.back = (float)(1.0002e-4 * stretch * (1.0 + 1e-5));
+                d.bkind = 3;
+            }
+        }
         double dev = 0.0;   // Frobenius norm of xf_lin * inv_lin - I
         for (int r = 0; r < 3; ++r)
             for (int col = 0; col < 3; ++col) {
