@@ -88,6 +88,8 @@ struct KArgs {
     PathSoA in, out;
     HitSoA hit;
     const int32_t* perm;
+    const int32_t* sort_offs;   // material-sorted mode: scanned (iteration, material, tile) histogram
+    int32_t sort_t64;           // its tile count per key
     float* image;          // npix * 3 (AoS float3, tile-local)
     float* colbuf;         // P * 3 (spp > 1)
     Ctl* ctl;              // [2]
@@ -97,7 +99,8 @@ struct KArgs {
     int32_t bounce;
     int32_t n_fixed;       // >= 0: path count is known on the host (first bounce)
     int32_t* flags;        // [P] survivor flags of the current bounce
-    int32_t* seg;          // [2][kMaxSeg] per-workgroup survivor counts of k_bounce
+    int32_t* seg;          // [2][kMaxSeg] per-workgroup survivor count | batch iteration << 24 (k_bounce)
+    int32_t* ibase;        // [kMaxSpp + 1] split pipeline: first dense index of each iteration
     DevStats* stats;
     unsigned long long* emit_slots;   // [64 bounces][emit_stride]: per-workgroup emissive counts
     int32_t emit_stride;
@@ -398,6 +401,15 @@ __device__ __forceinline__ Hit intersect_scene(const SceneDev& S, const FlagsDev
 // index on ties, pathtrace.cu:284-288) is the reference's bit for bit.  Typically one exact test
 // per ray instead of one per geom.  PT_AMD_VERIFY_BOUNDS=1 re-runs the plain loop and counts any
 // difference (pt_stats_t.bound_mismatch).
+// Diagnostic build only (scripts/stamps.sh: -DPT_STAMPS): per-wave s_memtime phase sums of the
+// non-first bounce kernel, each phase closed by s_waitcnt 0 (so the split perturbs the schedule).
+#ifdef PT_STAMPS
+__device__ unsigned long long g_stamps[16];   // [0..5] phases, [8..] closest-hit counters
+#define STAMP(v) do { __builtin_amdgcn_s_waitcnt(0); v = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define STAMP(v) do { } while (0)
+#endif
+
 constexpr int kLdsGeoms = 32;
 struct alignas(16) LGeom {   // what the exact tests read: 31 words, one 128-byte LDS row
     Affine inv, xf;
@@ -547,6 +559,21 @@ __device__ __forceinline__ Hit intersect_bounded(const SceneDev& S, const FlagsD
         };
         if (g1 >= 0) take(g1);
         if (g2 >= 0 && lo2 <= t_min) take(g2);
+#ifdef PT_STAMPS
+        {
+            const uint64_t m2 = __ballot(g2 >= 0 && lo2 <= t_min), m3 = __ballot(lo3 <= t_min);
+            const uint64_t mg = __ballot(g1 >= 0), ms = __ballot(g1 >= 0 && s_geoms[g1].type == PT_GEOM_SPHERE);
+            if ((threadIdx.x & 63) == 0) {
+                atomicAdd(&g_stamps[8], 1ull);
+                atomicAdd(&g_stamps[9], (unsigned long long)__popcll(m2));
+                atomicAdd(&g_stamps[10], m2 ? 1ull : 0ull);
+                atomicAdd(&g_stamps[11], (unsigned long long)__popcll(m3));
+                atomicAdd(&g_stamps[12], m3 ? 1ull : 0ull);
+                atomicAdd(&g_stamps[13], (ms && ms != mg) ? 1ull : 0ull);
+                atomicAdd(&g_stamps[14], (unsigned long long)__popcll(mg));
+            }
+        }
+#endif
         if (lo3 <= t_min) {   // a third candidate (rare): every remaining geom with a finite bound
             uint32_t m = cand & ~(1u << g1) & ~(1u << g2);
             while (m) {
@@ -828,9 +855,13 @@ __global__ __launch_bounds__(kBlock) void k_trace(const KArgs A) {
             if (FIRST) raygen(A.cam, A.fl, A.tile, i, p);
             else load_path(A.in, i, p);
             const Hit h = closest_hit<MESH, true>(A.S, A.fl, s_geoms, p.o, p.d, &A.stats->bound_mismatch);
-            const int iter = A.tile.iter_first + (SPP1 ? 0 : p.slot / A.tile.npix);
-            const bool alive = lds_mats ? shade(A.S, A.fl, A.tile.depth, iter, A.fl.rng_pixel ? slot_pixel(A.cam, A.tile, p.slot) : i, p, h, s_mats)
-                                        : shade(A.S, A.fl, A.tile.depth, iter, A.fl.rng_pixel ? slot_pixel(A.cam, A.tile, p.slot) : i, p, h, A.S.mats);
+            const int it = SPP1 ? 0 : p.slot / A.tile.npix;
+            const int iter = A.tile.iter_first + it;
+            // key: index within the path's own iteration (k_iter_bases; see k_bounce)
+            const int key = A.fl.rng_pixel ? slot_pixel(A.cam, A.tile, p.slot)
+                                           : i - (SPP1 ? 0 : (FIRST ? it * A.tile.npix : A.ibase[it]));
+            const bool alive = lds_mats ? shade(A.S, A.fl, A.tile.depth, iter, key, p, h, s_mats)
+                                        : shade(A.S, A.fl, A.tile.depth, iter, key, p, h, A.S.mats);
             if (alive) {
                 store_survivor(A.in, i, p, FIRST);
             } else {
@@ -842,6 +873,16 @@ __global__ __launch_bounds__(kBlock) void k_trace(const KArgs A) {
         emit_cnt += (uint32_t)__popcll(__ballot(emitted));
     }
     flush_emissive(A, emit_cnt, &s_cnt);
+}
+
+// Split pipeline, batched passes: the first dense index of every batch iteration present (the
+// compacted array is iteration-major because the compaction is stable and slots are too).
+__global__ __launch_bounds__(kBlock) void k_iter_bases(const KArgs A) {
+    const int N = live_count(A);
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < N; i += gridDim.x * blockDim.x) {
+        const int it = A.in.slot[i] / A.tile.npix;
+        if (i == 0 || A.in.slot[i - 1] / A.tile.npix != it) A.ibase[it] = i;
+    }
 }
 
 // ---- fused pipeline: one kernel per bounce ---------------------------------------------------
@@ -857,34 +898,72 @@ __global__ __launch_bounds__(kBlock) void k_trace(const KArgs A) {
 // the same trace code without compaction.  Here nothing waits on another workgroup, so the grid
 // need not be co-resident and shared GPUs need no claimed schedule.
 constexpr int kMaxSeg = 2048;
+constexpr int kMaxSpp = 64;   // batch iterations per pass (pt_shard.spp)
 
-// Exclusive scan of the previous launch's segment counts into s_pre[0..nseg] (s_pre[nseg] = N).
-__device__ __forceinline__ int scan_segments(const int32_t* __restrict__ cnt, int nseg, int32_t* s_pre,
-                                             uint32_t* s_wsum) {
+// Segment words of k_bounce: survivor count | batch iteration << 24 (pt_create bounds chunk < 2^24).
+constexpr int kSegItShift = 24;
+constexpr uint32_t kSegCountMask = (1u << kSegItShift) - 1u;
+
+// Thread 0: the launch's workgroup layout from the iteration starts s_ib[0..spp] (see k_bounce):
+// s_lay = {tpb, nseg, iteration of this workgroup (-1: idle), its chunk index in that iteration}.
+__device__ __forceinline__ void plan_layout(const int32_t* s_ib, int spp, int grid, int b, int32_t* s_lay) {
+    int tiles = 0;
+    for (int it = 0; it < spp; ++it) tiles += (s_ib[it + 1] - s_ib[it] + kBlock - 1) / kBlock;
+    const int tpb = max(1, (tiles + grid - spp - 1) / (grid - spp));
+    int nseg = 0, my_it = -1, my_c = 0;
+    for (int it = 0; it < spp; ++it) {
+        const int g = ((s_ib[it + 1] - s_ib[it] + kBlock - 1) / kBlock + tpb - 1) / tpb;
+        if (b >= nseg && b < nseg + g) { my_it = it; my_c = b - nseg; }
+        nseg += g;
+    }
+    s_lay[0] = tpb; s_lay[1] = nseg; s_lay[2] = my_it; s_lay[3] = my_c;
+}
+
+// Exclusive scan of the previous launch's segment counts into s_pre[0..nseg] (s_pre[nseg] = N),
+// the logical index where each batch iteration's survivors start into s_ib[0..spp] (s_ib[spp] = N;
+// an iteration with no survivor gets the next one's start), and this launch's layout (s_lay).
+// s_ib must hold -1 on entry (written before the caller's first barrier).
+__device__ __forceinline__ int scan_segments(const uint32_t* __restrict__ words, int nseg, int spp, int32_t* s_pre,
+                                             int32_t* s_ib, int32_t* s_lay, uint32_t* s_wsum) {
     constexpr int kPer = kMaxSeg / kBlock;   // 8 counts per thread
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    int32_t v[kPer];
+    uint32_t w[kPer];
     uint32_t sum = 0;
+    const int s0 = tid * kPer;
+    const uint32_t wprev = (s0 > 0 && s0 - 1 < nseg) ? words[s0 - 1] : 0xffffffffu;
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
-        const int s = tid * kPer + k;
-        v[k] = s < nseg ? cnt[s] : 0;
-        sum += (uint32_t)v[k];
+        w[k] = s0 + k < nseg ? words[s0 + k] : 0u;
+        sum += w[k] & kSegCountMask;
     }
     const uint32_t incl = lb::wave_inclusive_scan(sum);
     if (lane == 63) s_wsum[wave] = incl;
     __syncthreads();
     uint32_t run = incl - sum;
-    for (int w = 0; w < wave; ++w) run += s_wsum[w];
+    for (int q = 0; q < wave; ++q) run += s_wsum[q];
+    int prev_it = wprev == 0xffffffffu ? -1 : (int)(wprev >> kSegItShift);
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
-        const int s = tid * kPer + k;
+        const int s = s0 + k;
         if (s <= nseg) s_pre[s] = (int32_t)run;
-        run += (uint32_t)v[k];
+        if (s < nseg) {   // first segment of its iteration: that iteration's logical start
+            const int it = (int)(w[k] >> kSegItShift);
+            if (it != prev_it) s_ib[it] = (int32_t)run;
+            prev_it = it;
+        }
+        run += w[k] & kSegCountMask;
     }
     if (tid == kBlock - 1) s_pre[kMaxSeg] = (int32_t)run;   // nseg == kMaxSeg
     __syncthreads();
-    return s_pre[nseg];
+    if (tid == 0) {
+        const int N = s_pre[nseg];
+        s_ib[spp] = N;
+        for (int it = spp - 1; it >= 0; --it)
+            if (s_ib[it] < 0) s_ib[it] = s_ib[it + 1];
+        plan_layout(s_ib, spp, (int)gridDim.x, (int)blockIdx.x, s_lay);
+    }
+    __syncthreads();
+    return __builtin_amdgcn_readfirstlane(s_pre[nseg]);
 }
 
 // Segment holding logical index i, searching up from `s` (s_pre[s] <= i).
@@ -899,33 +978,50 @@ __global__ __launch_bounds__(kBlock) void k_bounce(const KArgs A) {
     __shared__ DMaterial s_mats[kLdsMats];
     __shared__ LGeom s_geoms[MESH ? 1 : kLdsGeoms];
     __shared__ int32_t s_pre[FIRST ? 1 : kMaxSeg + 1];
+    __shared__ int32_t s_ib[kMaxSpp + 1];
     __shared__ uint32_t s_wc[2][4];
     __shared__ uint32_t s_cnt;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int par = A.parity;
+    const int spp = A.tile.spp;
+    __shared__ int32_t s_lay[4];
     int N, nseg_in = 0, chunk_in = 0;
     if (FIRST) {
         N = A.n_fixed;
+        if (tid <= spp) s_ib[tid] = tid * A.tile.npix;
+        __syncthreads();
+        if (tid == 0) plan_layout(s_ib, spp, (int)gridDim.x, (int)blockIdx.x, s_lay);
+        __syncthreads();
     } else {
+        if (tid <= spp) s_ib[tid] = -1;
         nseg_in = (int)A.ctl[par].nseg;
         chunk_in = (int)A.ctl[par].chunk;
-        N = scan_segments(A.seg + (size_t)par * kMaxSeg, nseg_in, s_pre, s_wc[0]);
+        N = scan_segments(reinterpret_cast<const uint32_t*>(A.seg) + (size_t)par * kMaxSeg, nseg_in, spp, s_pre, s_ib,
+                          s_lay, s_wc[0]);
     }
-    const int tiles = (N + kBlock - 1) / kBlock;
-    const int tpb = (tiles + (int)gridDim.x - 1) / (int)gridDim.x;   // tiles per workgroup
+    // Workgroups are dealt to the batch iterations in order, none spanning two: iteration s gets
+    // ceil(tiles_s / tpb) workgroups of tpb whole tiles.  tpb = ceil(tiles / (grid - spp)) keeps the
+    // total within the grid.  The survivors of a pass then stay iteration-major, and a path's
+    // shading key is its index within ITS iteration's compacted array — pathtrace.cu:315 of the
+    // iteration traced alone, so a batched pass equals `spp` sequential pathtrace() calls bit for bit.
+    const int tpb = __builtin_amdgcn_readfirstlane(s_lay[0]);
+    const int nseg = __builtin_amdgcn_readfirstlane(s_lay[1]);
+    const int my_it = __builtin_amdgcn_readfirstlane(s_lay[2]);
+    const int my_c = __builtin_amdgcn_readfirstlane(s_lay[3]);
     const int chunk = tpb * kBlock;
-    const int nseg = tpb ? (tiles + tpb - 1) / tpb : 0;
     if (blockIdx.x == 0 && tid == 0) {
         A.ctl[par ^ 1].nseg = (uint32_t)nseg;
         A.ctl[par ^ 1].chunk = (uint32_t)chunk;
     }
-    if ((int)blockIdx.x >= nseg) return;
+    if (my_it < 0) return;
     if (!MESH) stage_geoms(A.S, s_geoms);
     stage_materials(A, s_mats);
     const bool lds_mats = A.S.nmats <= kLdsMats;
     count_bounce(A, N);
-    const int first = (int)blockIdx.x * chunk;
-    const int last = min(N, first + chunk);
+    const int it_base = __builtin_amdgcn_readfirstlane(s_ib[my_it]);
+    const int first = it_base + my_c * chunk;
+    const int last = min(__builtin_amdgcn_readfirstlane(s_ib[my_it + 1]), first + chunk);
+    const int iter = A.tile.iter_first + my_it;
     int seg = 0;
     if (!FIRST) {   // segment of this workgroup's first logical path (binary search, uniform)
         int lo = 0, hi = nseg_in - 1;
@@ -937,10 +1033,14 @@ __global__ __launch_bounds__(kBlock) void k_bounce(const KArgs A) {
     }
     uint32_t kept = 0, emit_cnt = 0;
     int k = 0;
+#ifdef PT_STAMPS
+    unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0}, t0, t1, t2, t3, t4, t5;
+#endif
     for (int base = first; base < last; base += kBlock, ++k) {
         const int i = base + tid;
         bool alive = false, emitted = false;
         PathReg p;
+        STAMP(t0);
         if (i < last) {
             if (FIRST) {
                 raygen(A.cam, A.fl, A.tile, i, p);
@@ -948,9 +1048,10 @@ __global__ __launch_bounds__(kBlock) void k_bounce(const KArgs A) {
                 const int s = seg_walk(s_pre, nseg_in, seg, i);
                 load_path(A.in, s * chunk_in + (i - s_pre[s]), p);
             }
+            STAMP(t1);
             const Hit h = closest_hit<MESH, false>(A.S, A.fl, s_geoms, p.o, p.d, &A.stats->bound_mismatch);
-            const int iter = A.tile.iter_first + (SPP1 ? 0 : p.slot / A.tile.npix);
-            const int key = A.fl.rng_pixel ? slot_pixel(A.cam, A.tile, p.slot) : i;
+            STAMP(t2);
+            const int key = A.fl.rng_pixel ? slot_pixel(A.cam, A.tile, p.slot) : i - it_base;
             alive = lds_mats ? shade(A.S, A.fl, A.tile.depth, iter, key, p, h, s_mats)
                              : shade(A.S, A.fl, A.tile.depth, iter, key, p, h, A.S.mats);
             if (!alive) {
@@ -958,6 +1059,7 @@ __global__ __launch_bounds__(kBlock) void k_bounce(const KArgs A) {
                 retire<SPP1>(A, p);
             }
         }
+        STAMP(t3);
         emit_cnt += (uint32_t)__popcll(__ballot(emitted));
         // in-tile ranks: wave ballot + mbcnt, 4 wave counts through LDS (double-buffered, so
         // one barrier per tile: buffer k&1 was last read two tiles ago, before the last barrier)
@@ -967,11 +1069,21 @@ __global__ __launch_bounds__(kBlock) void k_bounce(const KArgs A) {
         __syncthreads();
         const uint32_t w0 = s_wc[k & 1][0], w1 = s_wc[k & 1][1], w2 = s_wc[k & 1][2], w3 = s_wc[k & 1][3];
         const uint32_t before = (wave > 0 ? w0 : 0u) + (wave > 1 ? w1 : 0u) + (wave > 2 ? w2 : 0u);
-        if (alive) store_path(A.out, first + (int)(kept + before + rank), p);
+        STAMP(t4);
+        if (alive) store_path(A.out, (int)blockIdx.x * chunk + (int)(kept + before + rank), p);
         kept += (w0 + w1) + (w2 + w3);
         if (!FIRST) seg = seg_walk(s_pre, nseg_in, seg, min(base + kBlock, last - 1));
+        STAMP(t5);
+#ifdef PT_STAMPS
+        st_acc[0] += t1 - t0; st_acc[1] += t2 - t1; st_acc[2] += t3 - t2; st_acc[3] += t4 - t3; st_acc[4] += t5 - t4;
+        st_acc[5] += 1;
+#endif
     }
-    if (tid == 0) A.seg[(size_t)(par ^ 1) * kMaxSeg + blockIdx.x] = (int32_t)kept;
+#ifdef PT_STAMPS
+    if (!FIRST && lane == 0)
+        for (int q = 0; q < 6; ++q) atomicAdd(&g_stamps[q], st_acc[q]);
+#endif
+    if (tid == 0) A.seg[(size_t)(par ^ 1) * kMaxSeg + blockIdx.x] = (int32_t)(kept | ((uint32_t)my_it << kSegItShift));
     flush_emissive(A, emit_cnt, &s_cnt);
 }
 // Stable compaction of the flagged survivors: tile = 256 threads x 4 paths (path order
@@ -1094,16 +1206,20 @@ __global__ __launch_bounds__(kBlock) void k_isect_hist(const KArgs A, int32_t* _
             A.hit.u[i] = h.u; A.hit.v[i] = h.v;
             key = h.t == -1.0f ? 0 : h.mat;     // misses keep the memset materialId 0 (pathtrace.cu:466)
             A.hit.mat[i] = key;
+            // batched passes sort by (iteration, material): each iteration is sorted on its own,
+            // as `spp` sequential pathtrace() calls would (the array is iteration-major already)
+            key += (A.in.slot[i] / A.tile.npix) * A.S.nmats;
             keys[i] = key;
         }
-        for (int k0 = 0; k0 < A.S.nmats; k0 += 64) {
+        const int nkeys = A.S.nmats * A.tile.spp;
+        for (int k0 = 0; k0 < nkeys; k0 += 64) {
             const int k = k0 + lane;
             const uint64_t dummy = 0;
             (void)dummy;
             uint32_t cnt = 0;
             // count of lanes whose key == k (k differs per lane): loop over the wave's keys
             for (int src = 0; src < 64; ++src) cnt += (__shfl(key, src, 64) == k) ? 1u : 0u;
-            if (k < A.S.nmats) hist[(size_t)k * max_t64 + t64] = (int32_t)cnt;
+            if (k < nkeys) hist[(size_t)k * max_t64 + t64] = (int32_t)cnt;
         }
     }
 }
@@ -1151,8 +1267,11 @@ __global__ __launch_bounds__(kBlock) void k_shade_sorted(const KArgs A) {
             h.u = A.hit.u[i];
             h.v = A.hit.v[i];
             const int iter = A.tile.iter_first + (SPP1 ? 0 : p.slot / A.tile.npix);
-            const bool alive = lds_mats ? shade(A.S, A.fl, A.tile.depth, iter, A.fl.rng_pixel ? slot_pixel(A.cam, A.tile, p.slot) : idx, p, h, s_mats)
-                                        : shade(A.S, A.fl, A.tile.depth, iter, A.fl.rng_pixel ? slot_pixel(A.cam, A.tile, p.slot) : idx, p, h, A.S.mats);
+            // key: sorted index within the path's own iteration (its keys start at it * nmats)
+            const int key = A.fl.rng_pixel ? slot_pixel(A.cam, A.tile, p.slot)
+                                           : idx - (SPP1 ? 0 : A.sort_offs[(size_t)(p.slot / A.tile.npix) * A.S.nmats * A.sort_t64]);
+            const bool alive = lds_mats ? shade(A.S, A.fl, A.tile.depth, iter, key, p, h, s_mats)
+                                        : shade(A.S, A.fl, A.tile.depth, iter, key, p, h, A.S.mats);
             if (alive) {
                 store_survivor(A.out, idx, p, true);   // sorted order, compacted by k_compact_paths
             } else {
@@ -1229,6 +1348,7 @@ struct pt_ctx {
     bool profiling = false;
     std::vector<ProfEv> events;   // pool; the first `ev_used` are recorded and unread
     size_t ev_used = 0;
+    size_t path_cap = 0;          // entries per path buffer (>= P, see pt_create)
     std::vector<DGeom> hgeoms;    // host copy of the geom table (bounds re-derived by pt_set_flags)
     DGeom* d_geoms = nullptr;
     double scene_ext = 0.0;       // max |coordinate| over every surface and the camera position
@@ -1452,8 +1572,8 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
     if (S.materials.empty() || S.geoms.empty()) return pt::fail(PT_ERR_ARG, "scene has no geometry/materials");
     pt_shard sh{0, 1, 1, 0};
     if (shard) sh = *shard;
-    if (sh.world < 1 || sh.rank < 0 || sh.rank >= sh.world || sh.spp < 1)
-        return pt::fail(PT_ERR_ARG, "bad shard (rank/world/spp)");
+    if (sh.world < 1 || sh.rank < 0 || sh.rank >= sh.world || sh.spp < 1 || sh.spp > kMaxSpp)
+        return pt::fail(PT_ERR_ARG, "bad shard (rank/world, or spp outside 1..64)");
     const int W = S.camera.res[0], H = S.camera.res[1];
     const int rows = (H - sh.rank + sh.world - 1) / sh.world;
     if (rows <= 0) return pt::fail(PT_ERR_ARG, "empty tile");
@@ -1609,9 +1729,35 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
     A.cam.res[1] = H;
     A.tile = TileDev{W, sh.rank, sh.world, (int)npix, sh.spp, (int)P, S.depth, 1};
 
+    A.emit_stride = 256 * 8;   // >= any grid_trace (cus * 8) / grid_bounce
+    // k_trace has no inter-workgroup dependency: 8 workgroups per CU, grid-stride beyond that.
+    // k_compact_paths is persistent + look-back: co-resident grid (one block/CU below the
+    // occupancy API's answer, which can over-report by one for SGPR-heavy kernels).
+    int cus = 256;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
+    c->grid_trace = std::max(1, std::min({(int)((P + kBlock - 1) / kBlock), cus * 8, A.emit_stride}));
+    c->grid_compact = std::max(1, std::min((int)((P + kCompactTile - 1) / kCompactTile), cus * resident_per_cu((const void*)k_compact_paths)));
+    for (int f = 0; f < 2; ++f) {   // k_bounce: any grid is correct; one full wave of equal-work
+        int per_cu = 0;              // workgroups avoids a half-empty second wave
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bounce_kernel(f, sh.spp == 1, A.S.ntris > 0), kBlock,
+                                                         0) != hipSuccess || per_cu <= 0)
+            per_cu = 4;
+        // > 2 spp workgroups: the per-iteration layout of k_bounce needs grid - spp >= spp
+        c->grid_bounce[f] = std::max(2 * sh.spp + 1, std::min({cus * per_cu, kMaxSeg, A.emit_stride}));
+    }
     // ---- path state, image, control ----
+    // k_bounce writes workgroup b's survivors at b * chunk: with the per-iteration layout the last
+    // segment can end past P by < spp chunks (tiles <= P/256 + spp, tpb <= ceil(tiles / (grid - spp))).
+    {
+        const long long g = std::min(c->grid_bounce[0], c->grid_bounce[1]);
+        const long long tiles = (P + kBlock - 1) / kBlock + sh.spp;
+        const long long tpb = (tiles + g - sh.spp - 1) / (g - sh.spp);
+        c->path_cap = (size_t)kBlock * (size_t)(tiles + sh.spp * tpb);
+        if (tpb * kBlock > (long long)kSegCountMask)
+            return bail(pt::fail(PT_ERR_ARG, "pass too large for the bounce kernel's segment words (chunk >= 2^24)"));
+    }
     for (int b = 0; b < 2; ++b)
-        if (int rc = alloc_paths(c, c->buf[b], (size_t)P)) return bail(rc);
+        if (int rc = alloc_paths(c, c->buf[b], c->path_cap)) return bail(rc);
     if (int rc = c->alloc(&A.image, (size_t)npix * 3)) return bail(rc);
     if (sh.spp > 1)
         if (int rc = c->alloc(&A.colbuf, (size_t)P * 3)) return bail(rc);
@@ -1619,10 +1765,10 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
     if (int rc = c->alloc(&A.flags, (size_t)P)) return bail(rc);
     if (int rc = c->alloc(&A.ctl, 2)) return bail(rc);
     if (int rc = c->alloc(&A.seg, (size_t)2 * kMaxSeg)) return bail(rc);
+    if (int rc = c->alloc(&A.ibase, (size_t)kMaxSpp + 1)) return bail(rc);
     if (int rc = c->alloc(&A.status, (size_t)2 * c->max_tiles)) return bail(rc);
     if (int rc = c->alloc(&c->stats, 1)) return bail(rc);
     A.stats = c->stats;
-    A.emit_stride = 256 * 8;   // >= any grid_trace (cus * 8), checked below
     if (int rc = c->alloc(&A.emit_slots, (size_t)64 * A.emit_stride)) return bail(rc);
     if ((e = hipMemset(A.emit_slots, 0, (size_t)64 * A.emit_stride * sizeof(unsigned long long))) != hipSuccess)
         return bail(pt::fail(PT_ERR_HIP, std::string("hipMemset: ") + hipGetErrorString(e)));
@@ -1640,7 +1786,7 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
             if (int rc = c->alloc(p, (size_t)P)) return bail(rc);
         if (int rc = c->alloc(&A.hit.mat, (size_t)P)) return bail(rc);
         c->max_t64 = (int)((P + 63) / 64);
-        const size_t hn = (size_t)c->max_t64 * c->nmats;
+        const size_t hn = (size_t)c->max_t64 * c->nmats * sh.spp;
         if (int rc = c->alloc(&c->keys, (size_t)P)) return bail(rc);
         if (int rc = c->alloc(&c->hist, hn)) return bail(rc);
         if (int rc = c->alloc(&c->offs, hn)) return bail(rc);
@@ -1648,20 +1794,6 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
         uint8_t* ws;
         if (int rc = c->alloc(&ws, sc_workspace_bytes((int64_t)hn))) return bail(rc);
         c->scan_ws = ws;
-    }
-    // k_trace has no inter-workgroup dependency: 8 workgroups per CU, grid-stride beyond that.
-    // k_compact_paths is persistent + look-back: co-resident grid (one block/CU below the
-    // occupancy API's answer, which can over-report by one for SGPR-heavy kernels).
-    int cus = 256;
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
-    c->grid_trace = std::max(1, std::min({(int)((P + kBlock - 1) / kBlock), cus * 8, A.emit_stride}));
-    c->grid_compact = std::max(1, std::min(c->max_tiles, cus * resident_per_cu((const void*)k_compact_paths)));
-    for (int f = 0; f < 2; ++f) {   // k_bounce: any grid is correct; one full wave of equal-work
-        int per_cu = 0;              // workgroups avoids a half-empty second wave
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bounce_kernel(f, sh.spp == 1, A.S.ntris > 0), kBlock,
-                                                         0) != hipSuccess || per_cu <= 0)
-            per_cu = 4;
-        c->grid_bounce[f] = std::max(1, std::min({cus * per_cu, kMaxSeg, A.emit_stride}));
     }
     if (const char* pl = std::getenv("PT_PIPELINE")) c->fused = std::string(pl) != "split";
     *out = c;
@@ -1713,6 +1845,7 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
             ++c->compact_launches;
             cur ^= 1;
         } else if (!sorted) {
+            if (b > 0 && !spp1 && (rc = launch_k(c, k_iter_bases, c->grid_trace, st, PT_KIND_COMPACT, A))) return rc;
             rc = launch_k(c, trace_kernel(b == 0, spp1, mesh), c->grid_trace, st,
                           b == 0 ? PT_KIND_FIRST_BOUNCE : PT_KIND_BOUNCE, A);
             if (rc) return rc;
@@ -1728,13 +1861,15 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
             if ((rc = prof_begin(c, st, PT_KIND_SORT, &ev))) return rc;
             hipLaunchKernelGGL(k_isect_hist, dim3(g64), dim3(kBlock), 0, st, A, c->keys, c->hist, c->max_t64);
             HIP_TRY(hipGetLastError());
-            const int64_t hn = (int64_t)c->max_t64 * c->nmats;
+            const int64_t hn = (int64_t)c->max_t64 * c->nmats * A.tile.spp;
             if (sc_scan_exclusive_i32(c->hist, c->offs, hn, c->scan_ws, st) != SC_OK)
                 return pt::fail(PT_ERR_HIP, std::string("material scan: ") + sc_last_error());
             hipLaunchKernelGGL(k_sort_scatter, dim3(g64), dim3(kBlock), 0, st, A, c->keys, c->offs, c->perm, c->max_t64);
             HIP_TRY(hipGetLastError());
             if ((rc = prof_end(ev, st))) return rc;
             A.perm = c->perm;
+            A.sort_offs = c->offs;
+            A.sort_t64 = c->max_t64;
             // shade in sorted order into buf[cur^1] (dense, sorted), then compact back into buf[cur]
             rc = spp1 ? launch_k(c, k_shade_sorted<true>, c->grid_trace, st, PT_KIND_SORT, A)
                       : launch_k(c, k_shade_sorted<false>, c->grid_trace, st, PT_KIND_SORT, A);
@@ -1828,6 +1963,18 @@ int pt_stats(pt_ctx* c, pt_stats_t* out) {
     out->bound_mismatch = s.bound_mismatch;
     return s.err ? pt::fail(PT_ERR_DEVICE, "device-side look-back spin bound was hit") : PT_OK;
 }
+
+#ifdef PT_STAMPS
+int pt_debug_stamps(unsigned long long* out8, int32_t reset) {
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 16));
+    if (reset) {
+        unsigned long long z[16] = {};
+        HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof z));
+    }
+    return PT_OK;
+}
+#endif
 
 int pt_profile_enable(pt_ctx* c, int32_t on) {
     if (!c) return pt::fail(PT_ERR_ARG, "null context");

@@ -726,12 +726,21 @@ int oracle_render_pass(const OGeom* geoms, int ngeoms, const OMaterial* mats, in
         if (fl->sort_by_material) {                                          // pathtrace.cu:479-491
             std::vector<int> ord((size_t)N);
             for (int i = 0; i < N; ++i) ord[i] = i;
-            std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return isect[a].mat < isect[b].mat; });
+            // a batched pass sorts each iteration on its own: key (iteration, material)
+            std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) {
+                return paths[a].iter != paths[b].iter ? paths[a].iter < paths[b].iter : isect[a].mat < isect[b].mat;
+            });
             std::vector<Isect> is2((size_t)N);
             for (int i = 0; i < N; ++i) { tmp[i] = paths[ord[i]]; is2[i] = isect[ord[i]]; }
             for (int i = 0; i < N; ++i) { paths[i] = tmp[i]; isect[i] = is2[i]; }
         }
-        for (int i = 0; i < N; ++i) shade(sc, *fl, paths[i], isect[i], fl->rng_key_pixel ? paths[i].pixel : i);
+        // RNG key (pathtrace.cu:315): the index within the path's own iteration, i.e. what `spp`
+        // sequential pathtrace() calls would use (the array is iteration-major: stable compaction
+        // of slot-ordered paths, and the sort above keeps iterations apart)
+        for (int i = 0, base = 0; i < N; ++i) {
+            if (i > 0 && paths[i].iter != paths[i - 1].iter) base = i;
+            shade(sc, *fl, paths[i], isect[i], fl->rng_key_pixel ? paths[i].pixel : i - base);
+        }
         // relocate_terminated_paths (pathtrace.cu:377-407) == thrust::stable_partition here
         for (int i = 0; i < N; ++i) flags[i] = paths[i].remaining == 0 ? 0 : 1;
         int live = 0;

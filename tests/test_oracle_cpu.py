@@ -212,6 +212,22 @@ def test_render_invariants():
     assert img.sum() > 0 and img_s.sum() > 0
 
 
+@pytest.mark.parametrize("kw", [dict(), dict(sort_by_material=True), dict(russian_roulette=False, ssaa=False)])
+def test_batched_pass_equals_sequential_iterations(kw):
+    """A pass of spp iterations traced together (bench.py's batching) equals spp sequential
+    one-iteration passes — the reference's pathtrace() loop — bit for bit: each path's shading
+    RNG key is its index within its own iteration's compacted (and sorted) array."""
+    sc = _small_scene()
+    fl = O.flags(**kw)
+    batched, live_b = O.render_pass(sc, fl, iter_first=4, spp=3)
+    seq, live_s = None, [0] * sc.depth
+    for it in (4, 5, 6):
+        seq, live = O.render_pass(sc, fl, iter_first=it, image=seq)
+        live_s = [a + b for a, b in zip(live_s, live)]
+    np.testing.assert_array_equal(batched, seq)
+    assert live_b == live_s
+
+
 def test_render_shards_tile_the_image():
     """Rank r of W owns rows y % W == r; shards are disjoint and cover the image,
     and the camera ray of a pixel does not depend on the sharding (raygen key = global pixel)."""

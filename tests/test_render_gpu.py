@@ -128,6 +128,28 @@ def test_tiles_and_batched_samples(cornell_path, rank, world, spp):
     assert st["bounce_live"] == live
 
 
+@pytest.mark.parametrize("kw", [dict(), dict(sortbyMaterial=True)])
+@pytest.mark.parametrize("pipeline", ["fused", "split"])
+def test_batched_pass_equals_sequential_passes(cornell_path, monkeypatch, kw, pipeline):
+    """On the device: one pass of 4 batched iterations == 4 one-iteration passes, bit for bit
+    (per-iteration workgroup layout of k_bounce / k_iter_bases / (iteration, material) sort keys)."""
+    from cuda_pathtracer_amd import PathTracer
+    if pipeline == "split":
+        monkeypatch.setenv("PT_PIPELINE", "split")
+    s, o = _pair(cornell_path, (40, 36))
+    pb = PathTracer(s, _gui(**kw), spp=4)
+    pb.render_pass(3)
+    gb, stb = pb.image(), pb.stats()
+    pb.free()
+    ps = PathTracer(s, _gui(**kw), spp=1)
+    for it in (3, 4, 5, 6):
+        ps.render_pass(it)
+    gs, sts = ps.image(), ps.stats()
+    ps.free()
+    _assert_bitexact(gb, gs, f"batched vs sequential {kw} {pipeline}")
+    assert stb["bounce_live"] == sts["bounce_live"]
+
+
 def test_rng_key_pixel_shards_equal_single_gpu(cornell_path):
     """§8e's shard-invariant mode on the device: with rngKeyPixel the 3-way row shards, assembled,
     equal the 1-GPU image bit for bit — and so does the material-sorted pipeline."""
