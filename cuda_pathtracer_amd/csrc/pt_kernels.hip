@@ -898,25 +898,34 @@ __global__ __launch_bounds__(kBlock) void k_iter_bases(const KArgs A) {
 // the same trace code without compaction.  Here nothing waits on another workgroup, so the grid
 // need not be co-resident and shared GPUs need no claimed schedule.
 constexpr int kMaxSeg = 2048;
-constexpr int kMaxSpp = 64;   // batch iterations per pass (pt_shard.spp)
+constexpr int kMaxSpp = kBlock;   // batch iterations per pass (pt_shard.spp): one thread each
 
 // Segment words of k_bounce: survivor count | batch iteration << 24 (pt_create bounds chunk < 2^24).
 constexpr int kSegItShift = 24;
 constexpr uint32_t kSegCountMask = (1u << kSegItShift) - 1u;
 
-// Thread 0: the launch's workgroup layout from the iteration starts s_ib[0..spp] (see k_bounce):
-// s_lay = {tpb, nseg, iteration of this workgroup (-1: idle), its chunk index in that iteration}.
-__device__ __forceinline__ void plan_layout(const int32_t* s_ib, int spp, int grid, int b, int32_t* s_lay) {
-    int tiles = 0;
-    for (int it = 0; it < spp; ++it) tiles += (s_ib[it + 1] - s_ib[it] + kBlock - 1) / kBlock;
+// The launch's workgroup layout from the iteration starts s_ib[0..spp] (see k_bounce), computed
+// by the whole workgroup (thread t owns iteration t; spp <= kBlock): s_lay = {tpb, nseg, iteration
+// of this workgroup (-1: idle), its chunk index in that iteration}.  s_ib must be visible on entry.
+__device__ __forceinline__ void plan_layout(const int32_t* s_ib, int spp, int grid, int b, int32_t* s_lay,
+                                            uint32_t* s_tmp) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t tl = tid < spp ? (uint32_t)(s_ib[tid + 1] - s_ib[tid] + kBlock - 1) / kBlock : 0u;
+    const uint32_t i1 = lb::wave_inclusive_scan(tl);
+    if (lane == 63) s_tmp[wave] = i1;
+    if (tid == 0) s_lay[2] = -1;
+    __syncthreads();
+    const int tiles = (int)(s_tmp[0] + s_tmp[1] + s_tmp[2] + s_tmp[3]);
     const int tpb = max(1, (tiles + grid - spp - 1) / (grid - spp));
-    int nseg = 0, my_it = -1, my_c = 0;
-    for (int it = 0; it < spp; ++it) {
-        const int g = ((s_ib[it + 1] - s_ib[it] + kBlock - 1) / kBlock + tpb - 1) / tpb;
-        if (b >= nseg && b < nseg + g) { my_it = it; my_c = b - nseg; }
-        nseg += g;
-    }
-    s_lay[0] = tpb; s_lay[1] = nseg; s_lay[2] = my_it; s_lay[3] = my_c;
+    const uint32_t g = (tl + (uint32_t)tpb - 1u) / (uint32_t)tpb;
+    const uint32_t i2 = lb::wave_inclusive_scan(g);
+    if (lane == 63) s_tmp[4 + wave] = i2;
+    __syncthreads();
+    uint32_t pre = i2 - g;
+    for (int q = 0; q < wave; ++q) pre += s_tmp[4 + q];
+    if (tid < spp && b >= (int)pre && b < (int)(pre + g)) { s_lay[2] = tid; s_lay[3] = b - (int)pre; }
+    if (tid == 0) { s_lay[0] = tpb; s_lay[1] = (int)(s_tmp[4] + s_tmp[5] + s_tmp[6] + s_tmp[7]); }
+    __syncthreads();
 }
 
 // Exclusive scan of the previous launch's segment counts into s_pre[0..nseg] (s_pre[nseg] = N),
@@ -955,15 +964,17 @@ __device__ __forceinline__ int scan_segments(const uint32_t* __restrict__ words,
     }
     if (tid == kBlock - 1) s_pre[kMaxSeg] = (int32_t)run;   // nseg == kMaxSeg
     __syncthreads();
-    if (tid == 0) {
-        const int N = s_pre[nseg];
-        s_ib[spp] = N;
-        for (int it = spp - 1; it >= 0; --it)
-            if (s_ib[it] < 0) s_ib[it] = s_ib[it + 1];
-        plan_layout(s_ib, spp, (int)gridDim.x, (int)blockIdx.x, s_lay);
+    const int N = __builtin_amdgcn_readfirstlane(s_pre[nseg]);
+    if (tid == 0) s_ib[spp] = N;
+    __syncthreads();
+    if (tid < spp && s_ib[tid] < 0) {   // no survivor in iteration tid: the next present start
+        int j = tid + 1;                // (a concurrent fill of s_ib[j] writes this same value)
+        while (s_ib[j] < 0) ++j;
+        s_ib[tid] = s_ib[j];
     }
     __syncthreads();
-    return __builtin_amdgcn_readfirstlane(s_pre[nseg]);
+    plan_layout(s_ib, spp, (int)gridDim.x, (int)blockIdx.x, s_lay, s_wsum + 4);
+    return N;
 }
 
 // Segment holding logical index i, searching up from `s` (s_pre[s] <= i).
@@ -985,19 +996,19 @@ __global__ __launch_bounds__(kBlock) void k_bounce(const KArgs A) {
     const int par = A.parity;
     const int spp = A.tile.spp;
     __shared__ int32_t s_lay[4];
+    __shared__ uint32_t s_tmp[12];
     int N, nseg_in = 0, chunk_in = 0;
     if (FIRST) {
         N = A.n_fixed;
         if (tid <= spp) s_ib[tid] = tid * A.tile.npix;
         __syncthreads();
-        if (tid == 0) plan_layout(s_ib, spp, (int)gridDim.x, (int)blockIdx.x, s_lay);
-        __syncthreads();
+        plan_layout(s_ib, spp, (int)gridDim.x, (int)blockIdx.x, s_lay, s_tmp);
     } else {
         if (tid <= spp) s_ib[tid] = -1;
         nseg_in = (int)A.ctl[par].nseg;
         chunk_in = (int)A.ctl[par].chunk;
         N = scan_segments(reinterpret_cast<const uint32_t*>(A.seg) + (size_t)par * kMaxSeg, nseg_in, spp, s_pre, s_ib,
-                          s_lay, s_wc[0]);
+                          s_lay, s_tmp);
     }
     // Workgroups are dealt to the batch iterations in order, none spanning two: iteration s gets
     // ceil(tiles_s / tpb) workgroups of tpb whole tiles.  tpb = ceil(tiles / (grid - spp)) keeps the
@@ -1573,7 +1584,7 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
     pt_shard sh{0, 1, 1, 0};
     if (shard) sh = *shard;
     if (sh.world < 1 || sh.rank < 0 || sh.rank >= sh.world || sh.spp < 1 || sh.spp > kMaxSpp)
-        return pt::fail(PT_ERR_ARG, "bad shard (rank/world, or spp outside 1..64)");
+        return pt::fail(PT_ERR_ARG, "bad shard (rank/world, or spp outside 1..256)");
     const int W = S.camera.res[0], H = S.camera.res[1];
     const int rows = (H - sh.rank + sh.world - 1) / sh.world;
     if (rows <= 0) return pt::fail(PT_ERR_ARG, "empty tile");

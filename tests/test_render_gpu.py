@@ -120,7 +120,7 @@ def test_materials_reflective_refractive():
     assert st["bounce_live"] == live
 
 
-@pytest.mark.parametrize("rank,world,spp", [(0, 2, 1), (1, 2, 1), (0, 1, 2), (1, 3, 3), (2, 4, 4)])
+@pytest.mark.parametrize("rank,world,spp", [(0, 2, 1), (1, 2, 1), (0, 1, 2), (1, 3, 3), (2, 4, 4), (0, 1, 100)])
 def test_tiles_and_batched_samples(cornell_path, rank, world, spp):
     s, o = _pair(cornell_path, (40, 36))
     g, r, st, live = _run(s, o, _gui(), iters=spp * 2, rank=rank, world=world, spp=spp)
