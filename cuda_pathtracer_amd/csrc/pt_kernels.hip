@@ -35,9 +35,10 @@ namespace {
 
 constexpr int kBlock = 256;
 
+// Path state: three 16-byte planes (one dwordx4 load/store each, a wave moving 1 KiB contiguous
+// per instruction): a = (o.xyz, d.x), b = (d.yz, c.rg), c = (c.b, slot, bounces, 0).
 struct PathSoA {
-    float *ox, *oy, *oz, *dx, *dy, *dz, *cr, *cg, *cb;
-    int32_t *slot, *bounces;
+    v4f *a, *b, *c;
 };
 struct HitSoA {
     float *t, *nx, *ny, *nz, *u, *v;
@@ -753,18 +754,17 @@ __device__ __forceinline__ void raygen(const CamDev& cam, const FlagsDev& fl, co
 }
 
 __device__ __forceinline__ void load_path(const PathSoA& B, int i, PathReg& p) {
-    p.o = F3(B.ox[i], B.oy[i], B.oz[i]);
-    p.d = F3(B.dx[i], B.dy[i], B.dz[i]);
-    p.c = F3(B.cr[i], B.cg[i], B.cb[i]);
-    p.slot = B.slot[i];
-    p.bounces = B.bounces[i];
+    const v4f a = B.a[i], b = B.b[i], c = B.c[i];
+    p.o = F3(a[0], a[1], a[2]);
+    p.d = F3(a[3], b[0], b[1]);
+    p.c = F3(b[2], b[3], c[0]);
+    p.slot = __float_as_int(c[1]);
+    p.bounces = __float_as_int(c[2]);
 }
 __device__ __forceinline__ void store_path(const PathSoA& B, int i, const PathReg& p) {
-    B.ox[i] = p.o.x; B.oy[i] = p.o.y; B.oz[i] = p.o.z;
-    B.dx[i] = p.d.x; B.dy[i] = p.d.y; B.dz[i] = p.d.z;
-    B.cr[i] = p.c.x; B.cg[i] = p.c.y; B.cb[i] = p.c.z;
-    B.slot[i] = p.slot;
-    B.bounces[i] = p.bounces;
+    B.a[i] = v4f{p.o.x, p.o.y, p.o.z, p.d.x};
+    B.b[i] = v4f{p.d.y, p.d.z, p.c.x, p.c.y};
+    B.c[i] = v4f{p.c.z, __int_as_float(p.slot), __int_as_float(p.bounces), 0.0f};
 }
 
 // A path that terminated this bounce: its colour is final (finalGather, pathtrace.cu:347-356).
@@ -824,11 +824,10 @@ __device__ __forceinline__ void count_bounce(const KArgs& A, int N) {
     }
 }
 __device__ __forceinline__ void store_survivor(const PathSoA& B, int i, const PathReg& p, bool with_slot) {
-    B.ox[i] = p.o.x; B.oy[i] = p.o.y; B.oz[i] = p.o.z;
-    B.dx[i] = p.d.x; B.dy[i] = p.d.y; B.dz[i] = p.d.z;
-    B.cr[i] = p.c.x; B.cg[i] = p.c.y; B.cb[i] = p.c.z;
-    B.bounces[i] = p.bounces;
-    if (with_slot) B.slot[i] = p.slot;
+    (void)with_slot;
+    B.a[i] = v4f{p.o.x, p.o.y, p.o.z, p.d.x};
+    B.b[i] = v4f{p.d.y, p.d.z, p.c.x, p.c.y};
+    B.c[i] = v4f{p.c.z, __int_as_float(p.slot), __int_as_float(p.bounces), 0.0f};
 }
 
 // Trace one bounce: [raygen] -> intersect -> shade, one path per lane, no barriers and no
@@ -880,8 +879,8 @@ __global__ __launch_bounds__(kBlock) void k_trace(const KArgs A) {
 __global__ __launch_bounds__(kBlock) void k_iter_bases(const KArgs A) {
     const int N = live_count(A);
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < N; i += gridDim.x * blockDim.x) {
-        const int it = A.in.slot[i] / A.tile.npix;
-        if (i == 0 || A.in.slot[i - 1] / A.tile.npix != it) A.ibase[it] = i;
+        const int it = __float_as_int(A.in.c[i][1]) / A.tile.npix;
+        if (i == 0 || __float_as_int(A.in.c[i - 1][1]) / A.tile.npix != it) A.ibase[it] = i;
     }
 }
 
@@ -1105,11 +1104,9 @@ constexpr int kCompactPer = 4;
 constexpr int kCompactTile = kBlock * kCompactPer;
 
 __device__ __forceinline__ void copy_path(const PathSoA& S, const PathSoA& D, int i, int j) {
-    D.ox[j] = S.ox[i]; D.oy[j] = S.oy[i]; D.oz[j] = S.oz[i];
-    D.dx[j] = S.dx[i]; D.dy[j] = S.dy[i]; D.dz[j] = S.dz[i];
-    D.cr[j] = S.cr[i]; D.cg[j] = S.cg[i]; D.cb[j] = S.cb[i];
-    D.slot[j] = S.slot[i];
-    D.bounces[j] = S.bounces[i];
+    D.a[j] = S.a[i];
+    D.b[j] = S.b[i];
+    D.c[j] = S.c[i];
 }
 
 __global__ __launch_bounds__(kBlock) void k_compact_paths(const KArgs A) {
@@ -1208,8 +1205,9 @@ __global__ __launch_bounds__(kBlock) void k_isect_hist(const KArgs A, int32_t* _
         const int i = t64 * 64 + lane;
         int key = -1;
         if (i < N) {
-            const f3 o = F3(A.in.ox[i], A.in.oy[i], A.in.oz[i]);
-            const f3 d = F3(A.in.dx[i], A.in.dy[i], A.in.dz[i]);
+            const v4f pa = A.in.a[i], pb = A.in.b[i];
+            const f3 o = F3(pa[0], pa[1], pa[2]);
+            const f3 d = F3(pa[3], pb[0], pb[1]);
             const Hit h = A.S.ntris > 0 ? closest_hit<true, true>(A.S, A.fl, s_geoms, o, d, &A.stats->bound_mismatch)
                                         : closest_hit<false, true>(A.S, A.fl, s_geoms, o, d, &A.stats->bound_mismatch);
             A.hit.t[i] = h.t;
@@ -1219,7 +1217,7 @@ __global__ __launch_bounds__(kBlock) void k_isect_hist(const KArgs A, int32_t* _
             A.hit.mat[i] = key;
             // batched passes sort by (iteration, material): each iteration is sorted on its own,
             // as `spp` sequential pathtrace() calls would (the array is iteration-major already)
-            key += (A.in.slot[i] / A.tile.npix) * A.S.nmats;
+            key += (__float_as_int(A.in.c[i][1]) / A.tile.npix) * A.S.nmats;
             keys[i] = key;
         }
         const int nkeys = A.S.nmats * A.tile.spp;
@@ -1502,11 +1500,9 @@ void update_bounds(pt_ctx* c, float aperture) {
 }
 
 int alloc_paths(pt_ctx* c, PathSoA& B, size_t P) {
-    float** f[9] = {&B.ox, &B.oy, &B.oz, &B.dx, &B.dy, &B.dz, &B.cr, &B.cg, &B.cb};
-    for (auto* p : f)
-        if (int rc = c->alloc(p, P)) return rc;
-    if (int rc = c->alloc(&B.slot, P)) return rc;
-    return c->alloc(&B.bounces, P);
+    if (int rc = c->alloc(&B.a, P)) return rc;
+    if (int rc = c->alloc(&B.b, P)) return rc;
+    return c->alloc(&B.c, P);
 }
 
 int prof_begin(pt_ctx* c, hipStream_t st, int kind, ProfEv** out) {
