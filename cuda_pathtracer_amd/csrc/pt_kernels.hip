@@ -92,7 +92,7 @@ struct KArgs {
     const int32_t* sort_offs;   // material-sorted mode: scanned (iteration, material, tile) histogram
     int32_t sort_t64;           // its tile count per key
     float* image;          // npix * 3 (AoS float3, tile-local)
-    float* colbuf;         // P * 3 (spp > 1)
+    v4f* colbuf;           // P (spp > 1): final path colour per slot, one 16-byte store
     Ctl* ctl;              // [2]
     uint64_t* status;      // [2][max_tiles] look-back words of k_compact_paths
     int32_t max_tiles;
@@ -778,10 +778,7 @@ __device__ __forceinline__ void retire(const KArgs& A, const PathReg& p) {
             px[2] += p.c.z;
         }
     } else {
-        float* q = A.colbuf + 3 * (size_t)p.slot;
-        q[0] = p.c.x;
-        q[1] = p.c.y;
-        q[2] = p.c.z;
+        A.colbuf[p.slot] = v4f{p.c.x, p.c.y, p.c.z, 0.0f};
     }
 }
 
@@ -1295,11 +1292,11 @@ __global__ __launch_bounds__(kBlock) void k_shade_sorted(const KArgs A) {
 }
 
 // spp > 1: add the per-slot colours in sample order (finalGather as `spp` sequential iterations).
-__global__ void k_finalize_spp(float* __restrict__ image, const float* __restrict__ col, int npix, int spp) {
+__global__ void k_finalize_spp(float* __restrict__ image, const v4f* __restrict__ col, int npix, int spp) {
     for (int lp = blockIdx.x * blockDim.x + threadIdx.x; lp < npix; lp += gridDim.x * blockDim.x) {
         float r = image[3 * (size_t)lp], g = image[3 * (size_t)lp + 1], b = image[3 * (size_t)lp + 2];
         for (int s = 0; s < spp; ++s) {
-            const float* c = col + 3 * ((size_t)s * npix + lp);
+            const v4f c = col[(size_t)s * npix + lp];
             r += c[0]; g += c[1]; b += c[2];
         }
         image[3 * (size_t)lp] = r; image[3 * (size_t)lp + 1] = g; image[3 * (size_t)lp + 2] = b;
@@ -1767,7 +1764,7 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
         if (int rc = alloc_paths(c, c->buf[b], c->path_cap)) return bail(rc);
     if (int rc = c->alloc(&A.image, (size_t)npix * 3)) return bail(rc);
     if (sh.spp > 1)
-        if (int rc = c->alloc(&A.colbuf, (size_t)P * 3)) return bail(rc);
+        if (int rc = c->alloc(&A.colbuf, (size_t)P)) return bail(rc);
     c->max_tiles = (int)((P + kCompactTile - 1) / kCompactTile);   // k_compact_paths tiles
     if (int rc = c->alloc(&A.flags, (size_t)P)) return bail(rc);
     if (int rc = c->alloc(&A.ctl, 2)) return bail(rc);
@@ -1894,7 +1891,7 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
     if (!spp1) {
         const int npix = A.tile.npix;
         hipLaunchKernelGGL(k_finalize_spp, dim3(std::min((npix + 255) / 256, 4096)), dim3(256), 0, st, A.image,
-                           (const float*)A.colbuf, npix, A.tile.spp);
+                           (const v4f*)A.colbuf, npix, A.tile.spp);
         HIP_TRY(hipGetLastError());
     }
     return PT_OK;
