@@ -44,10 +44,12 @@ struct HitSoA {
     float *t, *nx, *ny, *nz, *u, *v;
     int32_t* mat;
 };
-struct Ctl {            // per-parity control block (16 B)
+struct Ctl {            // per-parity control block (32 B)
     uint32_t ticket;       // claimed tile schedule (look-back kernels)
-    uint32_t live;         // path count after k_compact_paths (split / sorted pipelines)
-    uint32_t chunk, nseg;  // segment layout written by k_bounce (fused pipeline)
+    uint32_t live;         // path count: after k_compact_paths (split), of this bounce (sorted)
+    uint32_t chunk, nseg;  // segment layout written by k_bounce / k_sort_shade
+    uint32_t hist_t64;     // sorted pipeline: histogram tiles holding counts (the rest read 0)
+    uint32_t pad[3];
 };
 struct DevStats {
     unsigned long long segments, passes, bounce_live[64];
@@ -88,9 +90,6 @@ struct KArgs {
     TileDev tile;
     PathSoA in, out;
     HitSoA hit;
-    const int32_t* perm;
-    const int32_t* sort_offs;   // material-sorted mode: scanned (iteration, material, tile) histogram
-    int32_t sort_t64;           // its tile count per key
     float* image;          // npix * 3 (AoS float3, tile-local)
     v4f* colbuf;           // P (spp > 1): final path colour per slot, one 16-byte store
     Ctl* ctl;              // [2]
@@ -1179,115 +1178,179 @@ __global__ __launch_bounds__(kBlock) void k_compact_paths(const KArgs A) {
 }
 
 // ---- material-sorted mode (pathtrace.cu:479-491: stable sort_by_key on materialId) ---------
-__global__ __launch_bounds__(kBlock) void k_raygen(const KArgs A) {
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < A.tile.P; i += gridDim.x * blockDim.x) {
-        PathReg p;
-        raygen(A.cam, A.fl, A.tile, i, p);
-        store_path(A.in, i, p);
-    }
-}
+// Material-sorted pipeline (sortbyMaterial), three kernels and one library scan per bounce:
+//   k_sort_isect  [raygen] + closest hit of the logical input (read through the previous
+//                 k_sort_shade's segments), hit record and key (iteration, material) per path,
+//                 per-64-path key histogram (key-major, only the live tiles are rewritten);
+//   scan          of the histogram: every path's stable sorted position base;
+//   k_sort_scatter  perm[sorted position] = physical path index;
+//   k_sort_shade  shades in sorted order (RNG key = sorted index within the iteration,
+//                 pathtrace.cu:315) and compacts the survivors into per-workgroup segments
+//                 exactly like k_bounce — no separate compaction launch or path copy.
+// Hits are stored at the PHYSICAL path index so k_sort_shade needs only perm.
+struct SortArgs {
+    int32_t* keys;     // [P] key of logical path i
+    int32_t* phys;     // [P] physical index of logical path i
+    int32_t* hist;     // [nkeys * max_t64]
+    const int32_t* offs;
+    int32_t* perm;     // [P] sorted position -> physical index
+    int32_t max_t64;
+};
 
-// Intersect + per-wave (64-path "sort tile") histogram of material keys.  hist is key-major:
-// hist[key * max_t64 + t64], written for every t64 < max_t64 so a flat exclusive scan of it
-// yields every path's stable sorted position base.
-__global__ __launch_bounds__(kBlock) void k_isect_hist(const KArgs A, int32_t* __restrict__ keys,
-                                                        int32_t* __restrict__ hist, int max_t64) {
-    __shared__ LGeom s_geoms[kLdsGeoms];
-    const int N = A.n_fixed >= 0 ? A.n_fixed : (int)A.ctl[A.parity].live;
-    const int lane = threadIdx.x & 63;
-    const int waves = gridDim.x * (blockDim.x >> 6);
-    stage_geoms(A.S, s_geoms);
+template <bool FIRST, bool MESH>
+__global__ __launch_bounds__(kBlock) void k_sort_isect(const KArgs A, const SortArgs SA) {
+    __shared__ LGeom s_geoms[MESH ? 1 : kLdsGeoms];
+    __shared__ int32_t s_pre[FIRST ? 1 : kMaxSeg + 1];
+    __shared__ int32_t s_ib[2];
+    __shared__ int32_t s_lay[4];
+    __shared__ uint32_t s_tmp[12];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int par = A.parity;
+    int N, nseg_in = 0, chunk_in = 0;
+    const int t64_prev = (int)A.ctl[par].hist_t64;
+    // no tile of this workgroup is live or holds stale counts: done (before the segment scan)
+    if (!FIRST && (int)blockIdx.x * (kBlock / 64) >= t64_prev && blockIdx.x != 0) return;
+    if (FIRST) {
+        N = A.n_fixed;
+    } else {
+        if (tid < 2) s_ib[tid] = -1;
+        nseg_in = (int)A.ctl[par].nseg;
+        chunk_in = (int)A.ctl[par].chunk;
+        N = scan_segments(reinterpret_cast<const uint32_t*>(A.seg) + (size_t)par * kMaxSeg, nseg_in, 1, s_pre, s_ib,
+                          s_lay, s_tmp);
+    }
+    if (!MESH) stage_geoms(A.S, s_geoms);
     __syncthreads();
-    for (int t64 = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); t64 < max_t64; t64 += waves) {
+    const int t64_live = (N + 63) / 64;
+    // histogram entries past the live tiles must read 0: rewrite up to the previous launch's range
+    const int t64_end = max(t64_live, t64_prev);
+    if (blockIdx.x == 0 && tid == 0) {
+        A.ctl[par ^ 1].hist_t64 = (uint32_t)t64_live;
+        A.ctl[par].live = (uint32_t)N;   // for k_sort_scatter / k_sort_shade of this bounce
+    }
+    if (blockIdx.x == 0) count_bounce(A, N);
+    const int nkeys = A.S.nmats * A.tile.spp;
+    const int waves = gridDim.x * (blockDim.x >> 6);
+    for (int t64 = blockIdx.x * (blockDim.x >> 6) + (tid >> 6); t64 < t64_end; t64 += waves) {
         const int i = t64 * 64 + lane;
         int key = -1;
         if (i < N) {
-            const v4f pa = A.in.a[i], pb = A.in.b[i];
-            const f3 o = F3(pa[0], pa[1], pa[2]);
-            const f3 d = F3(pa[3], pb[0], pb[1]);
-            const Hit h = A.S.ntris > 0 ? closest_hit<true, true>(A.S, A.fl, s_geoms, o, d, &A.stats->bound_mismatch)
-                                        : closest_hit<false, true>(A.S, A.fl, s_geoms, o, d, &A.stats->bound_mismatch);
-            A.hit.t[i] = h.t;
-            A.hit.nx[i] = h.n.x; A.hit.ny[i] = h.n.y; A.hit.nz[i] = h.n.z;
-            A.hit.u[i] = h.u; A.hit.v[i] = h.v;
+            int j = i;
+            PathReg p;
+            if (FIRST) {
+                raygen(A.cam, A.fl, A.tile, i, p);
+                store_path(A.in, i, p);
+            } else {
+                int lo = 0, hi = nseg_in - 1;   // segment of the wave's first path, then walk
+                const int f = t64 * 64;
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (s_pre[mid] <= f) lo = mid; else hi = mid - 1;
+                }
+                const int sg = seg_walk(s_pre, nseg_in, lo, i);
+                j = sg * chunk_in + (i - s_pre[sg]);
+                const v4f pa = A.in.a[j], pb = A.in.b[j], pc = A.in.c[j];
+                p.o = F3(pa[0], pa[1], pa[2]);
+                p.d = F3(pa[3], pb[0], pb[1]);
+                p.slot = __float_as_int(pc[1]);
+            }
+            const Hit h = closest_hit<MESH, true>(A.S, A.fl, s_geoms, p.o, p.d, &A.stats->bound_mismatch);
+            A.hit.t[j] = h.t;
+            A.hit.nx[j] = h.n.x; A.hit.ny[j] = h.n.y; A.hit.nz[j] = h.n.z;
+            A.hit.u[j] = h.u; A.hit.v[j] = h.v;
             key = h.t == -1.0f ? 0 : h.mat;     // misses keep the memset materialId 0 (pathtrace.cu:466)
-            A.hit.mat[i] = key;
+            A.hit.mat[j] = key;
             // batched passes sort by (iteration, material): each iteration is sorted on its own,
             // as `spp` sequential pathtrace() calls would (the array is iteration-major already)
-            key += (__float_as_int(A.in.c[i][1]) / A.tile.npix) * A.S.nmats;
-            keys[i] = key;
+            key += (p.slot / A.tile.npix) * A.S.nmats;
+            SA.keys[i] = key;
+            SA.phys[i] = j;
         }
-        const int nkeys = A.S.nmats * A.tile.spp;
         for (int k0 = 0; k0 < nkeys; k0 += 64) {
             const int k = k0 + lane;
-            const uint64_t dummy = 0;
-            (void)dummy;
             uint32_t cnt = 0;
             // count of lanes whose key == k (k differs per lane): loop over the wave's keys
             for (int src = 0; src < 64; ++src) cnt += (__shfl(key, src, 64) == k) ? 1u : 0u;
-            if (k < nkeys) hist[(size_t)k * max_t64 + t64] = (int32_t)cnt;
+            if (k < nkeys) SA.hist[(size_t)k * SA.max_t64 + t64] = (int32_t)cnt;
         }
     }
 }
 
-__global__ __launch_bounds__(kBlock) void k_sort_scatter(const KArgs A, const int32_t* __restrict__ keys,
-                                                          const int32_t* __restrict__ offs, int32_t* __restrict__ perm,
-                                                          int max_t64) {
-    const int N = A.n_fixed >= 0 ? A.n_fixed : (int)A.ctl[A.parity].live;
+__global__ __launch_bounds__(kBlock) void k_sort_scatter(const KArgs A, const SortArgs SA) {
+    const int N = (int)A.ctl[A.parity].live;
     const int lane = threadIdx.x & 63;
     const int waves = gridDim.x * (blockDim.x >> 6);
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     for (int t64 = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); t64 * 64 < N; t64 += waves) {
         const int i = t64 * 64 + lane;
-        const int key = i < N ? keys[i] : -1;
+        const int key = i < N ? SA.keys[i] : -1;
         uint64_t same = 0;
         for (int src = 0; src < 64; ++src) {
             const int ks = __shfl(key, src, 64);
             same |= (ks == key) ? (1ull << src) : 0ull;
         }
-        if (i < N) perm[offs[(size_t)key * max_t64 + t64] + __popcll(same & lt)] = i;
+        if (i < N) SA.perm[SA.offs[(size_t)key * SA.max_t64 + t64] + __popcll(same & lt)] = SA.phys[i];
     }
 }
 
 template <bool SPP1>
-__global__ __launch_bounds__(kBlock) void k_shade_sorted(const KArgs A) {
+__global__ __launch_bounds__(kBlock) void k_sort_shade(const KArgs A, const SortArgs SA) {
     __shared__ DMaterial s_mats[kLdsMats];
+    __shared__ uint32_t s_wc[2][4];
     __shared__ uint32_t s_cnt;
-    const int N = live_count(A);
-    if ((int)blockIdx.x * kBlock >= N) return;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int par = A.parity;
+    const int N = (int)A.ctl[par].live;
+    const int tiles = (N + kBlock - 1) / kBlock;
+    const int tpb = max(1, (tiles + (int)gridDim.x - 1) / (int)gridDim.x);
+    const int chunk = tpb * kBlock;
+    const int nseg = (tiles + tpb - 1) / tpb;
+    if (blockIdx.x == 0 && tid == 0) {
+        A.ctl[par ^ 1].nseg = (uint32_t)nseg;
+        A.ctl[par ^ 1].chunk = (uint32_t)chunk;
+    }
+    if ((int)blockIdx.x >= nseg) return;
     stage_materials(A, s_mats);
     const bool lds_mats = A.S.nmats <= kLdsMats;
-    count_bounce(A, N);
-    uint32_t emit_cnt = 0;
-    for (int base = blockIdx.x * kBlock; base < N; base += gridDim.x * kBlock) {
-        const int idx = base + (int)threadIdx.x;
-        bool emitted = false;
-        if (idx < N) {
-            const int i = A.perm[idx];
-            PathReg p;
-            load_path(A.in, i, p);
+    const int first = (int)blockIdx.x * chunk;
+    const int last = min(N, first + chunk);
+    uint32_t kept = 0, emit_cnt = 0;
+    int k = 0;
+    for (int base = first; base < last; base += kBlock, ++k) {
+        const int idx = base + tid;
+        bool alive = false, emitted = false;
+        PathReg p;
+        if (idx < last) {
+            const int j = SA.perm[idx];
+            load_path(A.in, j, p);
             Hit h;
-            h.t = A.hit.t[i];
-            h.n = F3(A.hit.nx[i], A.hit.ny[i], A.hit.nz[i]);
-            h.mat = A.hit.mat[i];
-            h.u = A.hit.u[i];
-            h.v = A.hit.v[i];
-            const int iter = A.tile.iter_first + (SPP1 ? 0 : p.slot / A.tile.npix);
+            h.t = A.hit.t[j];
+            h.n = F3(A.hit.nx[j], A.hit.ny[j], A.hit.nz[j]);
+            h.mat = A.hit.mat[j];
+            h.u = A.hit.u[j];
+            h.v = A.hit.v[j];
+            const int it = SPP1 ? 0 : p.slot / A.tile.npix;
             // key: sorted index within the path's own iteration (its keys start at it * nmats)
             const int key = A.fl.rng_pixel ? slot_pixel(A.cam, A.tile, p.slot)
-                                           : idx - (SPP1 ? 0 : A.sort_offs[(size_t)(p.slot / A.tile.npix) * A.S.nmats * A.sort_t64]);
-            const bool alive = lds_mats ? shade(A.S, A.fl, A.tile.depth, iter, key, p, h, s_mats)
-                                        : shade(A.S, A.fl, A.tile.depth, iter, key, p, h, A.S.mats);
-            if (alive) {
-                store_survivor(A.out, idx, p, true);   // sorted order, compacted by k_compact_paths
-            } else {
+                                           : idx - (SPP1 ? 0 : SA.offs[(size_t)it * A.S.nmats * SA.max_t64]);
+            alive = lds_mats ? shade(A.S, A.fl, A.tile.depth, A.tile.iter_first + it, key, p, h, s_mats)
+                             : shade(A.S, A.fl, A.tile.depth, A.tile.iter_first + it, key, p, h, A.S.mats);
+            if (!alive) {
                 emitted = p.c.x != 0.0f || p.c.y != 0.0f || p.c.z != 0.0f;
                 retire<SPP1>(A, p);
             }
-            A.flags[idx] = alive ? 1 : 0;
         }
         emit_cnt += (uint32_t)__popcll(__ballot(emitted));
+        const uint64_t m = __ballot(alive);
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        if (lane == 0) s_wc[k & 1][wave] = (uint32_t)__popcll(m);
+        __syncthreads();
+        const uint32_t w0 = s_wc[k & 1][0], w1 = s_wc[k & 1][1], w2 = s_wc[k & 1][2], w3 = s_wc[k & 1][3];
+        const uint32_t before = (wave > 0 ? w0 : 0u) + (wave > 1 ? w1 : 0u) + (wave > 2 ? w2 : 0u);
+        if (alive) store_path(A.out, first + (int)(kept + before + rank), p);
+        kept += (w0 + w1) + (w2 + w3);
     }
+    if (tid == 0) A.seg[(size_t)(par ^ 1) * kMaxSeg + blockIdx.x] = (int32_t)kept;
     flush_emissive(A, emit_cnt, &s_cnt);
 }
 
@@ -1348,7 +1411,7 @@ struct pt_ctx {
     std::vector<void*> allocs;
     PathSoA buf[2]{};
     int cur = 0;
-    int32_t *keys = nullptr, *hist = nullptr, *offs = nullptr, *perm = nullptr;
+    int32_t *keys = nullptr, *hist = nullptr, *offs = nullptr, *perm = nullptr, *phys = nullptr;
     void* scan_ws = nullptr;
     DevStats* stats = nullptr;
     bool profiling = false;
@@ -1786,14 +1849,17 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
     // hit SoA + sort buffers (material-sorted mode)
     {
         float** f[6] = {&A.hit.t, &A.hit.nx, &A.hit.ny, &A.hit.nz, &A.hit.u, &A.hit.v};
-        for (auto* p : f)
-            if (int rc = c->alloc(p, (size_t)P)) return bail(rc);
-        if (int rc = c->alloc(&A.hit.mat, (size_t)P)) return bail(rc);
+        for (auto* p : f)   // indexed by physical path index (< path_cap)
+            if (int rc = c->alloc(p, c->path_cap)) return bail(rc);
+        if (int rc = c->alloc(&A.hit.mat, c->path_cap)) return bail(rc);
+        if (int rc = c->alloc(&c->phys, (size_t)P)) return bail(rc);
         c->max_t64 = (int)((P + 63) / 64);
         const size_t hn = (size_t)c->max_t64 * c->nmats * sh.spp;
         if (int rc = c->alloc(&c->keys, (size_t)P)) return bail(rc);
         if (int rc = c->alloc(&c->hist, hn)) return bail(rc);
         if (int rc = c->alloc(&c->offs, hn)) return bail(rc);
+        if ((e = hipMemset(c->hist, 0, hn * sizeof(int32_t))) != hipSuccess)   // k_sort_isect's invariant
+            return bail(pt::fail(PT_ERR_HIP, std::string("hipMemset: ") + hipGetErrorString(e)));
         if (int rc = c->alloc(&c->perm, (size_t)P)) return bail(rc);
         uint8_t* ws;
         if (int rc = c->alloc(&ws, sc_workspace_bytes((int64_t)hn))) return bail(rc);
@@ -1859,32 +1925,26 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
                 cur ^= 1;
             }
         } else {
-            if (b == 0 && (rc = launch_k(c, k_raygen, std::min(c->max_t64, 4096), st, PT_KIND_SORT, A))) return rc;
-            const int g64 = std::min((c->max_t64 + 3) / 4, 8192);
+            SortArgs SA{c->keys, c->phys, c->hist, c->offs, c->perm, c->max_t64};
+            const int g64 = std::min((c->max_t64 + 3) / 4, c->grid_trace);   // grid-stride beyond
             ProfEv* ev;
             if ((rc = prof_begin(c, st, PT_KIND_SORT, &ev))) return rc;
-            hipLaunchKernelGGL(k_isect_hist, dim3(g64), dim3(kBlock), 0, st, A, c->keys, c->hist, c->max_t64);
+            if (b == 0 && mesh) hipLaunchKernelGGL((k_sort_isect<true, true>), dim3(g64), dim3(kBlock), 0, st, A, SA);
+            else if (b == 0) hipLaunchKernelGGL((k_sort_isect<true, false>), dim3(g64), dim3(kBlock), 0, st, A, SA);
+            else if (mesh) hipLaunchKernelGGL((k_sort_isect<false, true>), dim3(g64), dim3(kBlock), 0, st, A, SA);
+            else hipLaunchKernelGGL((k_sort_isect<false, false>), dim3(g64), dim3(kBlock), 0, st, A, SA);
             HIP_TRY(hipGetLastError());
             const int64_t hn = (int64_t)c->max_t64 * c->nmats * A.tile.spp;
             if (sc_scan_exclusive_i32(c->hist, c->offs, hn, c->scan_ws, st) != SC_OK)
                 return pt::fail(PT_ERR_HIP, std::string("material scan: ") + sc_last_error());
-            hipLaunchKernelGGL(k_sort_scatter, dim3(g64), dim3(kBlock), 0, st, A, c->keys, c->offs, c->perm, c->max_t64);
+            hipLaunchKernelGGL(k_sort_scatter, dim3(g64), dim3(kBlock), 0, st, A, SA);
+            HIP_TRY(hipGetLastError());
+            if (spp1) hipLaunchKernelGGL(k_sort_shade<true>, dim3(c->grid_bounce[0]), dim3(kBlock), 0, st, A, SA);
+            else hipLaunchKernelGGL(k_sort_shade<false>, dim3(c->grid_bounce[0]), dim3(kBlock), 0, st, A, SA);
             HIP_TRY(hipGetLastError());
             if ((rc = prof_end(ev, st))) return rc;
-            A.perm = c->perm;
-            A.sort_offs = c->offs;
-            A.sort_t64 = c->max_t64;
-            // shade in sorted order into buf[cur^1] (dense, sorted), then compact back into buf[cur]
-            rc = spp1 ? launch_k(c, k_shade_sorted<true>, c->grid_trace, st, PT_KIND_SORT, A)
-                      : launch_k(c, k_shade_sorted<false>, c->grid_trace, st, PT_KIND_SORT, A);
-            if (rc) return rc;
-            if (!last) {
-                KArgs C = A;
-                C.in = c->buf[cur ^ 1];
-                C.out = c->buf[cur];
-                if ((rc = launch_k(c, k_compact_paths, c->grid_compact, st, PT_KIND_COMPACT, C))) return rc;
-                ++c->compact_launches;
-            }
+            ++c->compact_launches;
+            cur ^= 1;
         }
     }
 
