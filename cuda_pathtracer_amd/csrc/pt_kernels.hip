@@ -48,7 +48,7 @@ struct Ctl {            // per-parity control block (32 B)
     uint32_t ticket;       // claimed tile schedule (look-back kernels)
     uint32_t live;         // path count: after k_compact_paths (split), of this bounce (sorted)
     uint32_t chunk, nseg;  // segment layout written by k_bounce / k_sort_shade
-    uint32_t hist_t64;     // sorted pipeline: histogram tiles holding counts (the rest read 0)
+    uint32_t hist_t64;     // sorted pipeline: histogram tiles of the launch (an upper bound for the next)
     uint32_t pad[3];
 };
 struct DevStats {
@@ -1180,79 +1180,112 @@ __global__ __launch_bounds__(kBlock) void k_compact_paths(const KArgs A) {
 // ---- material-sorted mode (pathtrace.cu:479-491: stable sort_by_key on materialId) ---------
 // Material-sorted pipeline (sortbyMaterial), three kernels and one library scan per bounce:
 //   k_sort_isect  [raygen] + closest hit of the logical input (read through the previous
-//                 k_sort_shade's segments), hit record and key (iteration, material) per path,
-//                 per-64-path key histogram (key-major, only the live tiles are rewritten);
+//                 k_sort_shade's segments), hit record and material key per path, and a
+//                 per-64-path material histogram;
 //   scan          of the histogram: every path's stable sorted position base;
-//   k_sort_scatter  perm[sorted position] = physical path index;
+//   k_sort_scatter  perm[sorted position] = physical path index (and re-zeroes the histogram);
 //   k_sort_shade  shades in sorted order (RNG key = sorted index within the iteration,
-//                 pathtrace.cu:315) and compacts the survivors into per-workgroup segments
+//                 pathtrace.cu:315) and compacts the survivors into per-iteration segments
 //                 exactly like k_bounce — no separate compaction launch or path copy.
+// Batched passes sort every iteration on its own (stable sort by (iteration, material), as `spp`
+// sequential pathtrace() calls would).  Each iteration's paths start on a fresh 64-path tile and
+// the histogram is laid out [iteration][material][tile of that iteration]: its flat exclusive
+// scan IS the (iteration, material) sorted position, at nmats * (tiles + spp) entries, whatever spp.
 // Hits are stored at the PHYSICAL path index so k_sort_shade needs only perm.
 struct SortArgs {
-    int32_t* keys;     // [P] key of logical path i
+    int32_t* keys;     // [P] material key of logical path i
     int32_t* phys;     // [P] physical index of logical path i
-    int32_t* hist;     // [nkeys * max_t64]
+    int32_t* hist;     // [nmats * (max_t64 + spp) + 1], all zero between bounces
     const int32_t* offs;
     int32_t* perm;     // [P] sorted position -> physical index
-    int32_t max_t64;
+    int32_t* tbase;    // [spp + 1] first histogram tile of each iteration (this bounce)
+    int32_t* ibase;    // [spp + 1] first logical path of each iteration (this bounce)
 };
+
+// Thread t < spp: s_tb = exclusive scan of the iterations' 64-path tile counts (s_tb[spp] = all).
+__device__ __forceinline__ void iteration_tiles(const int32_t* s_ib, int spp, int32_t* s_tb, uint32_t* s_tmp) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t n = tid < spp ? (uint32_t)(s_ib[tid + 1] - s_ib[tid] + 63) / 64u : 0u;
+    const uint32_t incl = lb::wave_inclusive_scan(n);
+    if (lane == 63) s_tmp[wave] = incl;
+    __syncthreads();
+    uint32_t pre = incl - n;
+    for (int q = 0; q < wave; ++q) pre += s_tmp[q];
+    if (tid < spp) s_tb[tid] = (int32_t)pre;
+    if (tid == 0) s_tb[spp] = (int32_t)(s_tmp[0] + s_tmp[1] + s_tmp[2] + s_tmp[3]);
+    __syncthreads();
+}
+// Iteration owning histogram tile g (the last one starting at or before g: empty ones own none).
+__device__ __forceinline__ int tile_iteration(const int32_t* s_tb, int spp, int g) {
+    int lo = 0, hi = spp - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (s_tb[mid] <= g) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
 
 template <bool FIRST, bool MESH>
 __global__ __launch_bounds__(kBlock) void k_sort_isect(const KArgs A, const SortArgs SA) {
     __shared__ LGeom s_geoms[MESH ? 1 : kLdsGeoms];
     __shared__ int32_t s_pre[FIRST ? 1 : kMaxSeg + 1];
-    __shared__ int32_t s_ib[2];
+    __shared__ int32_t s_ib[kMaxSpp + 1], s_tb[kMaxSpp + 1];
     __shared__ int32_t s_lay[4];
     __shared__ uint32_t s_tmp[12];
     const int tid = threadIdx.x, lane = tid & 63;
     const int par = A.parity;
+    const int spp = A.tile.spp;
+    // tiles never grow within a pass: a workgroup past the previous bounce's tiles has no work
+    if (!FIRST && (int)blockIdx.x * (kBlock / 64) >= (int)A.ctl[par].hist_t64 && blockIdx.x != 0) return;
     int N, nseg_in = 0, chunk_in = 0;
-    const int t64_prev = (int)A.ctl[par].hist_t64;
-    // no tile of this workgroup is live or holds stale counts: done (before the segment scan)
-    if (!FIRST && (int)blockIdx.x * (kBlock / 64) >= t64_prev && blockIdx.x != 0) return;
     if (FIRST) {
         N = A.n_fixed;
+        if (tid <= spp) s_ib[tid] = tid * A.tile.npix;
+        __syncthreads();
     } else {
-        if (tid < 2) s_ib[tid] = -1;
+        if (tid <= spp) s_ib[tid] = -1;
         nseg_in = (int)A.ctl[par].nseg;
         chunk_in = (int)A.ctl[par].chunk;
-        N = scan_segments(reinterpret_cast<const uint32_t*>(A.seg) + (size_t)par * kMaxSeg, nseg_in, 1, s_pre, s_ib,
+        N = scan_segments(reinterpret_cast<const uint32_t*>(A.seg) + (size_t)par * kMaxSeg, nseg_in, spp, s_pre, s_ib,
                           s_lay, s_tmp);
     }
+    iteration_tiles(s_ib, spp, s_tb, s_tmp + 4);
     if (!MESH) stage_geoms(A.S, s_geoms);
     __syncthreads();
-    const int t64_live = (N + 63) / 64;
-    // histogram entries past the live tiles must read 0: rewrite up to the previous launch's range
-    const int t64_end = max(t64_live, t64_prev);
-    if (blockIdx.x == 0 && tid == 0) {
-        A.ctl[par ^ 1].hist_t64 = (uint32_t)t64_live;
-        A.ctl[par].live = (uint32_t)N;   // for k_sort_scatter / k_sort_shade of this bounce
+    const int T = s_tb[spp];
+    if (blockIdx.x == 0) {
+        if (tid <= spp) { SA.tbase[tid] = s_tb[tid]; SA.ibase[tid] = s_ib[tid]; }
+        if (tid == 0) {
+            A.ctl[par ^ 1].hist_t64 = (uint32_t)T;
+            A.ctl[par].live = (uint32_t)N;   // for k_sort_scatter / k_sort_shade of this bounce
+        }
+        count_bounce(A, N);
     }
-    if (blockIdx.x == 0) count_bounce(A, N);
-    const int nkeys = A.S.nmats * A.tile.spp;
+    const int nmats = A.S.nmats;
     const int waves = gridDim.x * (blockDim.x >> 6);
-    for (int t64 = blockIdx.x * (blockDim.x >> 6) + (tid >> 6); t64 < t64_end; t64 += waves) {
-        const int i = t64 * 64 + lane;
+    for (int g = blockIdx.x * (blockDim.x >> 6) + (tid >> 6); g < T; g += waves) {
+        const int it = tile_iteration(s_tb, spp, g);
+        const int t = g - s_tb[it];
+        const int i = s_ib[it] + 64 * t + lane;
         int key = -1;
-        if (i < N) {
+        if (i < s_ib[it + 1]) {
             int j = i;
             PathReg p;
             if (FIRST) {
                 raygen(A.cam, A.fl, A.tile, i, p);
                 store_path(A.in, i, p);
             } else {
-                int lo = 0, hi = nseg_in - 1;   // segment of the wave's first path, then walk
-                const int f = t64 * 64;
+                int lo = 0, hi = nseg_in - 1;   // segment of the tile's first path, then walk
+                const int f = s_ib[it] + 64 * t;
                 while (lo < hi) {
                     const int mid = (lo + hi + 1) >> 1;
                     if (s_pre[mid] <= f) lo = mid; else hi = mid - 1;
                 }
                 const int sg = seg_walk(s_pre, nseg_in, lo, i);
                 j = sg * chunk_in + (i - s_pre[sg]);
-                const v4f pa = A.in.a[j], pb = A.in.b[j], pc = A.in.c[j];
+                const v4f pa = A.in.a[j], pb = A.in.b[j];
                 p.o = F3(pa[0], pa[1], pa[2]);
                 p.d = F3(pa[3], pb[0], pb[1]);
-                p.slot = __float_as_int(pc[1]);
             }
             const Hit h = closest_hit<MESH, true>(A.S, A.fl, s_geoms, p.o, p.d, &A.stats->bound_mismatch);
             A.hit.t[j] = h.t;
@@ -1260,60 +1293,80 @@ __global__ __launch_bounds__(kBlock) void k_sort_isect(const KArgs A, const Sort
             A.hit.u[j] = h.u; A.hit.v[j] = h.v;
             key = h.t == -1.0f ? 0 : h.mat;     // misses keep the memset materialId 0 (pathtrace.cu:466)
             A.hit.mat[j] = key;
-            // batched passes sort by (iteration, material): each iteration is sorted on its own,
-            // as `spp` sequential pathtrace() calls would (the array is iteration-major already)
-            key += (p.slot / A.tile.npix) * A.S.nmats;
             SA.keys[i] = key;
             SA.phys[i] = j;
         }
-        for (int k0 = 0; k0 < nkeys; k0 += 64) {
+        const int tiles_it = s_tb[it + 1] - s_tb[it];
+        for (int k0 = 0; k0 < nmats; k0 += 64) {
             const int k = k0 + lane;
             uint32_t cnt = 0;
             // count of lanes whose key == k (k differs per lane): loop over the wave's keys
             for (int src = 0; src < 64; ++src) cnt += (__shfl(key, src, 64) == k) ? 1u : 0u;
-            if (k < nkeys) SA.hist[(size_t)k * SA.max_t64 + t64] = (int32_t)cnt;
+            if (k < nmats) SA.hist[(size_t)nmats * s_tb[it] + (size_t)k * tiles_it + t] = (int32_t)cnt;
         }
     }
 }
 
 __global__ __launch_bounds__(kBlock) void k_sort_scatter(const KArgs A, const SortArgs SA) {
-    const int N = (int)A.ctl[A.parity].live;
-    const int lane = threadIdx.x & 63;
+    __shared__ int32_t s_ib[kMaxSpp + 1], s_tb[kMaxSpp + 1];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int spp = A.tile.spp;
+    if (tid <= spp) { s_ib[tid] = SA.ibase[tid]; s_tb[tid] = SA.tbase[tid]; }
+    __syncthreads();
+    const int T = s_tb[spp];
+    const int nmats = A.S.nmats;
     const int waves = gridDim.x * (blockDim.x >> 6);
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    for (int t64 = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); t64 * 64 < N; t64 += waves) {
-        const int i = t64 * 64 + lane;
-        const int key = i < N ? SA.keys[i] : -1;
+    for (int g = blockIdx.x * (blockDim.x >> 6) + (tid >> 6); g < T; g += waves) {
+        const int it = tile_iteration(s_tb, spp, g);
+        const int t = g - s_tb[it];
+        const int tiles_it = s_tb[it + 1] - s_tb[it];
+        const int i = s_ib[it] + 64 * t + lane;
+        const bool valid = i < s_ib[it + 1];
+        const int key = valid ? SA.keys[i] : -1;
         uint64_t same = 0;
         for (int src = 0; src < 64; ++src) {
             const int ks = __shfl(key, src, 64);
             same |= (ks == key) ? (1ull << src) : 0ull;
         }
-        if (i < N) SA.perm[SA.offs[(size_t)key * SA.max_t64 + t64] + __popcll(same & lt)] = SA.phys[i];
+        const size_t h0 = (size_t)nmats * s_tb[it] + t;
+        if (valid) SA.perm[SA.offs[h0 + (size_t)key * tiles_it] + __popcll(same & lt)] = SA.phys[i];
+        for (int k = lane; k < nmats; k += 64) SA.hist[h0 + (size_t)k * tiles_it] = 0;   // ready for the next bounce
     }
 }
 
 template <bool SPP1>
 __global__ __launch_bounds__(kBlock) void k_sort_shade(const KArgs A, const SortArgs SA) {
     __shared__ DMaterial s_mats[kLdsMats];
+    __shared__ int32_t s_sb[kMaxSpp + 1];
+    __shared__ int32_t s_lay[4];
+    __shared__ uint32_t s_tmp[8];
     __shared__ uint32_t s_wc[2][4];
     __shared__ uint32_t s_cnt;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int par = A.parity;
-    const int N = (int)A.ctl[par].live;
-    const int tiles = (N + kBlock - 1) / kBlock;
-    const int tpb = max(1, (tiles + (int)gridDim.x - 1) / (int)gridDim.x);
+    const int spp = A.tile.spp;
+    const int nmats = A.S.nmats;
+    // sorted start of every iteration: the scanned histogram at its first tile
+    if (tid <= spp) s_sb[tid] = SA.offs[(size_t)nmats * SA.tbase[tid]];
+    __syncthreads();
+    plan_layout(s_sb, spp, (int)gridDim.x, (int)blockIdx.x, s_lay, s_tmp);
+    const int tpb = __builtin_amdgcn_readfirstlane(s_lay[0]);
+    const int nseg = __builtin_amdgcn_readfirstlane(s_lay[1]);
+    const int my_it = __builtin_amdgcn_readfirstlane(s_lay[2]);
+    const int my_c = __builtin_amdgcn_readfirstlane(s_lay[3]);
     const int chunk = tpb * kBlock;
-    const int nseg = (tiles + tpb - 1) / tpb;
     if (blockIdx.x == 0 && tid == 0) {
         A.ctl[par ^ 1].nseg = (uint32_t)nseg;
         A.ctl[par ^ 1].chunk = (uint32_t)chunk;
     }
-    if ((int)blockIdx.x >= nseg) return;
+    if (my_it < 0) return;
     stage_materials(A, s_mats);
     const bool lds_mats = A.S.nmats <= kLdsMats;
-    const int first = (int)blockIdx.x * chunk;
-    const int last = min(N, first + chunk);
+    const int it_base = __builtin_amdgcn_readfirstlane(s_sb[my_it]);
+    const int first = it_base + my_c * chunk;
+    const int last = min(__builtin_amdgcn_readfirstlane(s_sb[my_it + 1]), first + chunk);
+    const int iter = A.tile.iter_first + my_it;
     uint32_t kept = 0, emit_cnt = 0;
     int k = 0;
     for (int base = first; base < last; base += kBlock, ++k) {
@@ -1329,12 +1382,10 @@ __global__ __launch_bounds__(kBlock) void k_sort_shade(const KArgs A, const Sort
             h.mat = A.hit.mat[j];
             h.u = A.hit.u[j];
             h.v = A.hit.v[j];
-            const int it = SPP1 ? 0 : p.slot / A.tile.npix;
-            // key: sorted index within the path's own iteration (its keys start at it * nmats)
-            const int key = A.fl.rng_pixel ? slot_pixel(A.cam, A.tile, p.slot)
-                                           : idx - (SPP1 ? 0 : SA.offs[(size_t)it * A.S.nmats * SA.max_t64]);
-            alive = lds_mats ? shade(A.S, A.fl, A.tile.depth, A.tile.iter_first + it, key, p, h, s_mats)
-                             : shade(A.S, A.fl, A.tile.depth, A.tile.iter_first + it, key, p, h, A.S.mats);
+            // key: sorted index within the path's own iteration
+            const int key = A.fl.rng_pixel ? slot_pixel(A.cam, A.tile, p.slot) : idx - it_base;
+            alive = lds_mats ? shade(A.S, A.fl, A.tile.depth, iter, key, p, h, s_mats)
+                             : shade(A.S, A.fl, A.tile.depth, iter, key, p, h, A.S.mats);
             if (!alive) {
                 emitted = p.c.x != 0.0f || p.c.y != 0.0f || p.c.z != 0.0f;
                 retire<SPP1>(A, p);
@@ -1347,10 +1398,10 @@ __global__ __launch_bounds__(kBlock) void k_sort_shade(const KArgs A, const Sort
         __syncthreads();
         const uint32_t w0 = s_wc[k & 1][0], w1 = s_wc[k & 1][1], w2 = s_wc[k & 1][2], w3 = s_wc[k & 1][3];
         const uint32_t before = (wave > 0 ? w0 : 0u) + (wave > 1 ? w1 : 0u) + (wave > 2 ? w2 : 0u);
-        if (alive) store_path(A.out, first + (int)(kept + before + rank), p);
+        if (alive) store_path(A.out, (int)blockIdx.x * chunk + (int)(kept + before + rank), p);
         kept += (w0 + w1) + (w2 + w3);
     }
-    if (tid == 0) A.seg[(size_t)(par ^ 1) * kMaxSeg + blockIdx.x] = (int32_t)kept;
+    if (tid == 0) A.seg[(size_t)(par ^ 1) * kMaxSeg + blockIdx.x] = (int32_t)(kept | ((uint32_t)my_it << kSegItShift));
     flush_emissive(A, emit_cnt, &s_cnt);
 }
 
@@ -1411,7 +1462,8 @@ struct pt_ctx {
     std::vector<void*> allocs;
     PathSoA buf[2]{};
     int cur = 0;
-    int32_t *keys = nullptr, *hist = nullptr, *offs = nullptr, *perm = nullptr, *phys = nullptr;
+    int32_t *keys = nullptr, *hist = nullptr, *offs = nullptr, *perm = nullptr, *phys = nullptr, *tbase = nullptr;
+    int64_t hist_n = 0;
     void* scan_ws = nullptr;
     DevStats* stats = nullptr;
     bool profiling = false;
@@ -1854,7 +1906,10 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
         if (int rc = c->alloc(&A.hit.mat, c->path_cap)) return bail(rc);
         if (int rc = c->alloc(&c->phys, (size_t)P)) return bail(rc);
         c->max_t64 = (int)((P + 63) / 64);
-        const size_t hn = (size_t)c->max_t64 * c->nmats * sh.spp;
+        // [iteration][material][tile]: each iteration starts a fresh tile (+1: the end offset)
+        const size_t hn = (size_t)c->nmats * ((size_t)c->max_t64 + sh.spp) + 1;
+        c->hist_n = (int64_t)hn;
+        if (int rc = c->alloc(&c->tbase, (size_t)kMaxSpp + 1)) return bail(rc);
         if (int rc = c->alloc(&c->keys, (size_t)P)) return bail(rc);
         if (int rc = c->alloc(&c->hist, hn)) return bail(rc);
         if (int rc = c->alloc(&c->offs, hn)) return bail(rc);
@@ -1925,7 +1980,7 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
                 cur ^= 1;
             }
         } else {
-            SortArgs SA{c->keys, c->phys, c->hist, c->offs, c->perm, c->max_t64};
+            SortArgs SA{c->keys, c->phys, c->hist, c->offs, c->perm, c->tbase, A.ibase};
             const int g64 = std::min((c->max_t64 + 3) / 4, c->grid_trace);   // grid-stride beyond
             ProfEv* ev;
             if ((rc = prof_begin(c, st, PT_KIND_SORT, &ev))) return rc;
@@ -1934,7 +1989,7 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
             else if (mesh) hipLaunchKernelGGL((k_sort_isect<false, true>), dim3(g64), dim3(kBlock), 0, st, A, SA);
             else hipLaunchKernelGGL((k_sort_isect<false, false>), dim3(g64), dim3(kBlock), 0, st, A, SA);
             HIP_TRY(hipGetLastError());
-            const int64_t hn = (int64_t)c->max_t64 * c->nmats * A.tile.spp;
+            const int64_t hn = c->hist_n;
             if (sc_scan_exclusive_i32(c->hist, c->offs, hn, c->scan_ws, st) != SC_OK)
                 return pt::fail(PT_ERR_HIP, std::string("material scan: ") + sc_last_error());
             hipLaunchKernelGGL(k_sort_scatter, dim3(g64), dim3(kBlock), 0, st, A, SA);
