@@ -8,12 +8,12 @@ entry point raises NativeLibraryError if libpt_amd.so is missing.
 from ._native import LIB_PATH, NativeLibraryError, PtError, lib  # noqa: F401
 from .pathtrace import (  # noqa: F401
     CUBE, MESH, SPHERE, GuiDataContainer, InitDataContainer, PathTracer, Scene, pathtrace, pathtraceFree,
-    pathtraceInit, render, save_image, tonemap)
+    pathtraceInit, render, save_image, save_image_hdr, encode_hdr, tonemap)
 from . import distributed  # noqa: F401
 from .stream_compaction import (Efficient, compact_device, live_indices_device, partition_device,  # noqa: F401
                                 scan_device)
 
 __all__ = ["Scene", "PathTracer", "GuiDataContainer", "Efficient", "scan_device", "compact_device",
-           "partition_device", "live_indices_device", "render", "save_image", "tonemap", "pathtraceInit",
+           "partition_device", "live_indices_device", "render", "save_image", "save_image_hdr", "encode_hdr", "tonemap", "pathtraceInit",
            "pathtraceFree", "pathtrace",
            "InitDataContainer", "lib", "LIB_PATH", "NativeLibraryError", "PtError"]

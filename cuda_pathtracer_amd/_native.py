@@ -133,6 +133,9 @@ SIGNATURES = {
     "pt_profile_read": (_I, [_P, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
     "pt_tonemap": (_I, [_P, _I, _I, _F, _P]),
     "pt_save_png": (_I, [C.c_char_p, _P, _I, _I, _F]),
+    "pt_save_hdr": (_I, [C.c_char_p, _P, _I, _I, _F]),
+    "pt_encode_hdr": (_I, [_P, _I, _I, _F, _P, C.c_int64, _P]),
+    "pt_set_accum": (_I, [_P, _P]),
 }
 
 _lib = None

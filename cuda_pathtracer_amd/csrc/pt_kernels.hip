@@ -2047,6 +2047,13 @@ int pt_get_image(pt_ctx* c, float* host_rgb) {
 
 int pt_get_accum(pt_ctx* c, float* host_rgb) { return pt_get_image(c, host_rgb); }
 
+int pt_set_accum(pt_ctx* c, const float* host_rgb) {
+    if (!c || !host_rgb) return pt::fail(PT_ERR_ARG, "null argument");
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(c->args.image, host_rgb, (size_t)c->args.tile.npix * 3 * sizeof(float), hipMemcpyHostToDevice));
+    return PT_OK;
+}
+
 int pt_copy_image(pt_ctx* c, float* d_rgb, void* stream) {
     if (!c || !d_rgb) return pt::fail(PT_ERR_ARG, "null argument");
     HIP_TRY(hipMemcpyAsync(d_rgb, c->args.image, (size_t)c->args.tile.npix * 3 * sizeof(float),

@@ -3,7 +3,7 @@
 // window — pathtraceInit, `iterations` calls of pathtrace(), saveImage() (main.cpp:88-112) and
 // pathtraceFree().  The camera is the first-frame orbit recompute (done by pt_scene_finalize).
 //
-//   pathtracer_amd SCENEFILE.json [--iterations N] [--out DIR] [--sort] [--no-png]
+//   pathtracer_amd SCENEFILE.json [--iterations N] [--out DIR] [--sort] [--no-png] [--hdr]
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -25,15 +25,17 @@ std::string currentTimeString() {   // preview.cpp:21-28
 }
 
 // saveImage (main.cpp:88-112): divide by the sample count, mirror x, clamp, x255, PNG.
-std::string saveImage(const Scene& scene, const std::string& dir, const std::string& start, int iteration) {
+std::string saveImage(const Scene& scene, const std::string& dir, const std::string& start, int iteration,
+                      bool hdr = false) {
     const float samples = (float)iteration;
     std::ostringstream ss;
     ss << scene.state.imageName << "." << start << "." << samples << "samp";
     std::string filename = ss.str();
     if (!dir.empty()) filename = dir + "/" + filename;
-    filename += ".png";   // Image::savePNG appends the extension (image.cpp:22-24)
+    filename += hdr ? ".hdr" : ".png";   // Image::savePNG / saveHDR append the extension (image.cpp:22-49)
     const int W = scene.state.camera.res[0], H = scene.state.camera.res[1];
-    if (pt_save_png(filename.c_str(), reinterpret_cast<const float*>(scene.state.image.data()), W, H, samples)) {
+    const float* rgb = reinterpret_cast<const float*>(scene.state.image.data());
+    if (hdr ? pt_save_hdr(filename.c_str(), rgb, W, H, samples) : pt_save_png(filename.c_str(), rgb, W, H, samples)) {
         std::fprintf(stderr, "saveImage: %s\n", pt_last_error());
         std::exit(EXIT_FAILURE);
     }
@@ -45,18 +47,19 @@ std::string saveImage(const Scene& scene, const std::string& dir, const std::str
 int main(int argc, char** argv) {
     const std::string startTimeString = currentTimeString();
     if (argc < 2) {
-        std::printf("Usage: %s SCENEFILE.json [--iterations N] [--out DIR] [--sort] [--no-png]\n", argv[0]);
+        std::printf("Usage: %s SCENEFILE.json [--iterations N] [--out DIR] [--sort] [--no-png] [--hdr]\n", argv[0]);
         return 1;
     }
     const char* sceneFile = argv[1];
     int iterations = -1;
     std::string out_dir;
-    bool sort = false, png = true;
+    bool sort = false, png = true, hdr = false;
     for (int i = 2; i < argc; ++i) {
         if (!std::strcmp(argv[i], "--iterations") && i + 1 < argc) iterations = std::atoi(argv[++i]);
         else if (!std::strcmp(argv[i], "--out") && i + 1 < argc) out_dir = argv[++i];
         else if (!std::strcmp(argv[i], "--sort")) sort = true;
         else if (!std::strcmp(argv[i], "--no-png")) png = false;
+        else if (!std::strcmp(argv[i], "--hdr")) hdr = true;   // also write the saveHDR .hdr file
         else {
             std::fprintf(stderr, "unknown argument %s\n", argv[i]);
             return 1;
@@ -82,6 +85,7 @@ int main(int argc, char** argv) {
     std::printf("rendered %d iteration(s) of %s (%dx%d, depth %d) in %.3f s\n", iteration, sceneFile,
                 scene->state.camera.res[0], scene->state.camera.res[1], scene->state.traceDepth, secs);
     if (png) std::printf("wrote %s\n", saveImage(*scene, out_dir, startTimeString, iteration).c_str());
+    if (hdr) std::printf("wrote %s\n", saveImage(*scene, out_dir, startTimeString, iteration, true).c_str());
     pathtraceFree();
     delete guiData;
     delete scene;

@@ -228,6 +228,27 @@ class PathTracer:
         check_pt(lib().pt_get_image(self._h, out.ctypes.data))
         return out
 
+    def set_image(self, image: np.ndarray) -> None:
+        """Resume: load a tile accumulator saved from image() (pt_set_accum)."""
+        img = np.ascontiguousarray(image, dtype=np.float32)
+        if img.shape != (self.rows, self.width, 3):
+            raise ValueError(f"accumulator shape {img.shape} != {(self.rows, self.width, 3)}")
+        check_pt(lib().pt_set_accum(self._h, img.ctypes.data))
+
+    def save_state(self, path: str, iterations_done: int) -> str:
+        """Checkpoint the accumulator and the next iteration index (extension: resume a render)."""
+        np.savez(path, image=self.image(), iterations_done=np.int64(iterations_done),
+                 rank=np.int32(self.rank), world=np.int32(self.world))
+        return str(path)
+
+    def load_state(self, path: str) -> int:
+        """Load a checkpoint written by save_state for the same tile; returns iterations_done."""
+        with np.load(path, allow_pickle=False) as z:
+            if int(z["rank"]) != self.rank or int(z["world"]) != self.world:
+                raise ValueError("checkpoint is for another tile")
+            self.set_image(z["image"])
+            return int(z["iterations_done"])
+
     def copy_image_to(self, dst_ptr: int, stream=None) -> None:
         check_pt(lib().pt_copy_image(self._h, C.c_void_p(dst_ptr), _stream_ptr(stream)))
 
@@ -271,6 +292,23 @@ def tonemap(image: np.ndarray, samples: float) -> np.ndarray:
 def save_image(path: str, image: np.ndarray, samples: float) -> str:
     img = np.ascontiguousarray(image, dtype=np.float32)
     check_pt(lib().pt_save_png(str(path).encode(), img.ctypes.data, img.shape[1], img.shape[0], float(samples)))
+    return str(path)
+
+
+def encode_hdr(image: np.ndarray, samples: float) -> bytes:
+    """Image::saveHDR file bytes (Radiance RGBE, stb_image_write's run-length coding)."""
+    img = np.ascontiguousarray(image, dtype=np.float32)
+    n = C.c_int64(0)
+    check_pt(lib().pt_encode_hdr(img.ctypes.data, img.shape[1], img.shape[0], float(samples), None, 0, C.byref(n)))
+    buf = (C.c_uint8 * n.value)()
+    check_pt(lib().pt_encode_hdr(img.ctypes.data, img.shape[1], img.shape[0], float(samples), buf, n.value,
+                                 C.byref(n)))
+    return bytes(buf)
+
+
+def save_image_hdr(path: str, image: np.ndarray, samples: float) -> str:
+    img = np.ascontiguousarray(image, dtype=np.float32)
+    check_pt(lib().pt_save_hdr(str(path).encode(), img.ctypes.data, img.shape[1], img.shape[0], float(samples)))
     return str(path)
 
 

@@ -209,6 +209,10 @@ int pt_get_image(pt_ctx* c, float* host_rgb);               /* tile accumulator,
 int pt_get_accum(pt_ctx* c, float* host_rgb);               /* §8b name of pt_get_image (pathtrace.cu:524) */
 int pt_copy_image(pt_ctx* c, float* d_rgb, void* stream);   /* device-to-device copy */
 int pt_reset_image(pt_ctx* c, void* stream);
+/* Resume (extension; the reference has none): load a previously saved float accumulator of this
+ * context's tile (npix x float3, as pt_get_accum returns it).  Continuing with the next iteration
+ * indices reproduces an uninterrupted render bit for bit. */
+int pt_set_accum(pt_ctx* c, const float* host_rgb);
 int pt_stats(pt_ctx* c, pt_stats_t* out);                   /* synchronises the context stream */
 /* Per-kernel device timing with hipEvents recorded on the launch stream (for the roofline).  When
  * enabled, pt_render_pass brackets every launch with pooled events; pt_profile_read synchronises
@@ -225,6 +229,12 @@ int pt_profile_read(pt_ctx* c, double ms[4], uint64_t launches[4]);
 int pt_tonemap(const float* rgb, int32_t width, int32_t height, float samples, uint8_t* out);
 /* Writes `path` as an 8-bit RGB PNG of the tonemapped image. */
 int pt_save_png(const char* path, const float* rgb, int32_t width, int32_t height, float samples);
+/* Image::saveHDR (image.cpp:44-49) via stb_image_write's Radiance RGBE writer (vendored by the
+ * reference: external/include/stb_image_write.h:246-387), pixels as saveImage (x-mirrored,
+ * accumulated / samples).  pt_encode_hdr writes the file bytes to `out` (NULL: size only). */
+int pt_save_hdr(const char* path, const float* rgb, int32_t width, int32_t height, float samples);
+int pt_encode_hdr(const float* rgb, int32_t width, int32_t height, float samples, uint8_t* out, int64_t cap,
+                  int64_t* size);
 
 #ifdef __cplusplus
 }

@@ -1,17 +1,22 @@
 # Bench lines for BASELINE.json configs 3-5 (1 GPU), each under its own time limit.
+# Iterations per pass: 16 (bench default) for configs 3 and 4, 4 for the 100k-triangle config 5.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"; mkdir -p gpurun_out
 : > gpurun_out/configs.jsonl
-for c in ${CONFIGS:-cornell_hd_sorted multi_object_4k random_triangles_100k}; do
-  timeout -k 10 300 python bench.py --config $c --steps ${STEPS:-20} --warmup 3 --no-cpu-baseline --no-scan \
-      >> gpurun_out/configs.jsonl 2> gpurun_out/config_$c.err || { echo "config $c failed"; tail -5 gpurun_out/config_$c.err; exit 1; }
-  echo "config $c ok"
-done
+run() {   # name, extra args
+  timeout -k 10 300 python bench.py --config $1 --warmup 2 --no-cpu-baseline --no-scan ${@:2} \
+      >> gpurun_out/configs.jsonl 2> gpurun_out/config_$1.err || { echo "config $1 failed"; tail -5 gpurun_out/config_$1.err; exit 1; }
+  echo "config $1 ${@:2} ok"
+}
+run cornell_hd_sorted --steps 10 || exit 1
+run multi_object_4k --steps 5 || exit 1
+run random_triangles_100k --steps 3 --spp 4 || exit 1
+run random_triangles_100k --steps 3 --spp 4 --bvh-cull || exit 1
 python3 - <<'PY'
 import json
 for line in open("gpurun_out/configs.jsonl"):
     d = json.loads(line)
-    print(d["config"]["workload"][:60], "|", round(d["value"], 1), d["unit"], "| ms/step", round(d["ms_per_step"], 2),
-          "| frac", round(d["roofline"]["frac"], 3))
+    print(d["config"]["workload"][:60], "| spp", d["config"]["spp_per_step"], "|", round(d["value"], 1), d["unit"],
+          "| ms/step", round(d["ms_per_step"], 2), "| frac", round(d["roofline"]["frac"], 3))
 PY

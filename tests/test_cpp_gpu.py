@@ -24,7 +24,7 @@ def test_reference_shaped_stream_compaction_selftest(size_log2):
 
 def test_cli_png_matches_oracle(tmp_path, cornell_path):
     exe = ROOT / "cuda_pathtracer_amd" / "pathtracer_amd"
-    res = subprocess.run([str(exe), cornell_path, "--iterations", "2", "--out", str(tmp_path)],
+    res = subprocess.run([str(exe), cornell_path, "--iterations", "2", "--out", str(tmp_path), "--hdr"],
                          capture_output=True, text=True, timeout=300)
     assert res.returncode == 0, res.stdout + res.stderr
     pngs = list(tmp_path.glob("cornell.*.2samp.png"))
@@ -36,6 +36,13 @@ def test_cli_png_matches_oracle(tmp_path, cornell_path):
     for it in (1, 2):
         img, _ = O.render_pass(sc, O.flags(), it, image=img)
     np.testing.assert_array_equal(got, O.tonemap(img, 2.0))
+    # --hdr: Image::saveHDR of the same accumulator (RGBE: <= 2^-7 of each pixel's largest component)
+    from oracle import hdr_oracle
+    hdrs = list(tmp_path.glob("cornell.*.2samp.hdr"))
+    assert len(hdrs) == 1
+    dec = hdr_oracle.decode_hdr(hdrs[0].read_bytes())
+    ref = (img / np.float32(2.0))[:, ::-1]
+    assert (np.abs(dec - ref) <= ref.max(axis=2, keepdims=True) * 2 ** -7 + 1e-30).all()
 
 
 def test_cli_usage_and_bad_scene(tmp_path):

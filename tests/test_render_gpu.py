@@ -402,3 +402,27 @@ def test_bounded_closest_hit_equals_plain_loop(config_scenes, monkeypatch):
             assert st["bound_mismatch"] == 0, (name, sort, st["bound_mismatch"])
             total += st["segments"]
     assert total > 100_000
+
+
+def test_resume_from_checkpoint_is_bitexact(cornell_path, tmp_path):
+    """Extension: checkpoint the float accumulator after 2 passes, resume in
+    a fresh context at the next iteration index: identical to rendering the 4 passes in one go."""
+    from cuda_pathtracer_amd import PathTracer
+    s, o = _pair(cornell_path, (36, 30))
+    ref = PathTracer(s, _gui(), spp=2)
+    for it in (1, 3, 5, 7):
+        ref.render_pass(it)
+    full = ref.image()
+    ref.free()
+    a = PathTracer(s, _gui(), spp=2)
+    for it in (1, 3):
+        a.render_pass(it)
+    ck = a.save_state(str(tmp_path / "ck.npz"), iterations_done=4)
+    a.free()
+    b = PathTracer(s, _gui(), spp=2)
+    done = b.load_state(ck)
+    assert done == 4
+    for it in (done + 1, done + 3):
+        b.render_pass(it)
+    _assert_bitexact(b.image(), full, "resumed vs uninterrupted")
+    b.free()
