@@ -142,7 +142,8 @@ __device__ __forceinline__ float box_test(const G& g, f3 ro, f3 rd, int& ncode) 
     }
     return -1.0f;
 }
-__device__ __forceinline__ f3 box_normal(const DGeom& g, int code) {
+template <class G>
+__device__ __forceinline__ f3 box_normal(const G& g, int code) {
     f3 n = F3(0.0f, 0.0f, 0.0f);
     if (code >= 0) {
         const float s = (code & 1) ? -1.0f : 1.0f;
@@ -171,7 +172,8 @@ __device__ __forceinline__ float sphere_test(const G& g, f3 r_o, f3 r_d, f3& obj
     const f3 ip = xform_point(g.xf, obj);
     return length(r_o - ip);
 }
-__device__ __forceinline__ f3 sphere_normal(const DGeom& g, f3 obj, bool outside) {
+template <class G>
+__device__ __forceinline__ f3 sphere_normal(const G& g, f3 obj, bool outside) {
     const f3 n = normalize(xform_vector(g.itr, obj));
     return outside ? n : -n;
 }
@@ -411,9 +413,9 @@ __device__ unsigned long long g_stamps[16];   // [0..5] phases, [8..] closest-hi
 #endif
 
 constexpr int kLdsGeoms = 32;
-struct alignas(16) LGeom {   // what the exact tests read: 31 words, one 128-byte LDS row
-    Affine inv, xf;
-    int32_t type;
+struct alignas(16) LGeom {   // what the exact tests and the hit normal read: 47 words, 192 bytes
+    Affine inv, xf, itr;
+    int32_t type, material;
 };
 constexpr float kInf = __builtin_inff();
 
@@ -423,7 +425,9 @@ __device__ __forceinline__ void stage_geoms(const SceneDev& S, LGeom* s_geoms) {
         const DGeom& g = S.geoms[j];
         s_geoms[j].inv = g.inv;
         s_geoms[j].xf = g.xf;
+        s_geoms[j].itr = g.itr;
         s_geoms[j].type = g.type;
+        s_geoms[j].material = g.material;
     }
 }
 
@@ -591,7 +595,7 @@ __device__ __forceinline__ Hit intersect_bounded(const SceneDev& S, const FlagsD
         h.u = h.v = 0.f;
         return h;
     }
-    const DGeom& g = S.geoms[hit_geom];
+    const LGeom& g = s_geoms[hit_geom];
     h.t = t_min;
     h.mat = g.material;
     h.u = h.v = 0.f;
