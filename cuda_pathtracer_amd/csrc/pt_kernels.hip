@@ -985,8 +985,10 @@ __device__ __forceinline__ int seg_walk(const int32_t* s_pre, int nseg, int s, i
 // [raygen] -> intersect -> shade -> segmented compaction (above).
 template <bool FIRST, bool SPP1, bool MESH>
 __global__ __launch_bounds__(kBlock) void k_bounce(const KArgs A) {
-    __shared__ DMaterial s_mats[kLdsMats];
-    __shared__ LGeom s_geoms[MESH ? 1 : kLdsGeoms];
+    // scene tables sized to the scene (dynamic LDS, bounce_lds_bytes): geom rows, then materials
+    extern __shared__ __align__(16) uint8_t s_dyn[];
+    LGeom* s_geoms = reinterpret_cast<LGeom*>(s_dyn);
+    DMaterial* s_mats = reinterpret_cast<DMaterial*>(s_dyn + (MESH || A.S.ngeoms > kLdsGeoms ? 0 : A.S.ngeoms) * sizeof(LGeom));
     __shared__ int32_t s_pre[FIRST ? 1 : kMaxSeg + 1];
     __shared__ int32_t s_ib[kMaxSpp + 1];
     __shared__ uint32_t s_wc[2][4];
@@ -1659,6 +1661,14 @@ int resident_per_cu(const void* kernel) {
     return per_cu;
 }
 
+// Dynamic LDS of k_bounce: the scene's geom rows (analytic scenes of <= kLdsGeoms geoms) and
+// materials (<= kLdsMats); Cornell needs 1.6 KiB instead of a fixed 12 KiB.
+size_t bounce_lds_bytes(const SceneDev& S) {
+    const int g = (S.ntris > 0 || S.ngeoms > kLdsGeoms) ? 0 : S.ngeoms;
+    const int m = std::min(S.nmats, kLdsMats);
+    return (size_t)g * sizeof(LGeom) + (size_t)m * sizeof(DMaterial);
+}
+
 using KernelFn = void (*)(const KArgs);
 KernelFn bounce_kernel(bool first, bool spp1, bool mesh) {
     static const KernelFn table[8] = {
@@ -1676,10 +1686,10 @@ KernelFn trace_kernel(bool first, bool spp1, bool mesh) {
 }
 
 template <typename K>
-int launch_k(pt_ctx* c, K kernel, int grid, hipStream_t st, int kind, const KArgs& a) {
+int launch_k(pt_ctx* c, K kernel, int grid, hipStream_t st, int kind, const KArgs& a, size_t lds = 0) {
     ProfEv* ev;
     if (int rc = prof_begin(c, st, kind, &ev)) return rc;
-    hipLaunchKernelGGL(kernel, dim3(grid), dim3(kBlock), 0, st, a);
+    hipLaunchKernelGGL(kernel, dim3(grid), dim3(kBlock), lds, st, a);
     HIP_TRY(hipGetLastError());
     return prof_end(ev, st);
 }
@@ -1863,7 +1873,7 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
     for (int f = 0; f < 2; ++f) {   // k_bounce: any grid is correct; one full wave of equal-work
         int per_cu = 0;              // workgroups avoids a half-empty second wave
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bounce_kernel(f, sh.spp == 1, A.S.ntris > 0), kBlock,
-                                                         0) != hipSuccess || per_cu <= 0)
+                                                         bounce_lds_bytes(A.S)) != hipSuccess || per_cu <= 0)
             per_cu = 4;
         // > 2 spp workgroups: the per-iteration layout of k_bounce needs grid - spp >= spp
         c->grid_bounce[f] = std::max(2 * sh.spp + 1, std::min({cus * per_cu, kMaxSeg, A.emit_stride}));
@@ -1969,7 +1979,7 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
         int rc;
         if (!sorted && c->fused) {
             rc = launch_k(c, bounce_kernel(b == 0, spp1, mesh), c->grid_bounce[b == 0], st,
-                          b == 0 ? PT_KIND_FIRST_BOUNCE : PT_KIND_BOUNCE, A);
+                          b == 0 ? PT_KIND_FIRST_BOUNCE : PT_KIND_BOUNCE, A, bounce_lds_bytes(A.S));
             if (rc) return rc;
             ++c->compact_launches;
             cur ^= 1;
