@@ -426,3 +426,30 @@ def test_resume_from_checkpoint_is_bitexact(cornell_path, tmp_path):
         b.render_pass(it)
     _assert_bitexact(b.image(), full, "resumed vs uninterrupted")
     b.free()
+
+
+def test_full_size_cornell_batched_equals_sequential(cornell_path):
+    """BASELINE configs[1] at full size (800x800, DEPTH 8): the bench's 16-iteration pass equals 16
+    one-iteration passes bit for bit, and the live-path counts agree (size-independent check
+    of the per-iteration keys, segment layout and buffer capacity at the benchmarked size)."""
+    from cuda_pathtracer_amd import PathTracer, Scene
+    s = Scene(cornell_path)
+    pb = PathTracer(s, _gui(), spp=16)
+    pb.render_pass(1)
+    gb, stb = pb.image(), pb.stats()
+    pb.free()
+    ps = PathTracer(s, _gui(), spp=1)
+    for it in range(1, 17):
+        ps.render_pass(it)
+    gs, sts = ps.image(), ps.stats()
+    ps.free()
+    _assert_bitexact(gb, gs, "800x800: 16 batched vs 16 sequential")
+    assert stb["bounce_live"] == sts["bounce_live"] and stb["bounce_live"][0] == 16 * 800 * 800
+    assert all(b <= a for a, b in zip(stb["bounce_live"], stb["bounce_live"][1:]))
+
+
+@pytest.mark.parametrize("spp", [0, 257])
+def test_bad_batch_size_is_rejected(cornell_path, spp):
+    from cuda_pathtracer_amd import PathTracer, PtError, Scene
+    with pytest.raises(PtError):
+        PathTracer(Scene(cornell_path), _gui(), spp=spp)
