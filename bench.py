@@ -57,6 +57,19 @@ def _traffic_from_profiles(kernel_key: str):
     return best
 
 
+def _host_cpu() -> str:
+    """lscpu-style model name and logical CPU count of this host (SURVEY.md §8d asks for both)."""
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return f"{model}; nproc={os.cpu_count()}"
+
+
 def cpu_baseline_render(seconds_target: float) -> dict:
     """The oracle (serial C++ restatement of the reference renderer) on this host, 1 thread."""
     from oracle import binding as O
@@ -68,7 +81,7 @@ def cpu_baseline_render(seconds_target: float) -> dict:
         total_seg += sum(live)
         total_t += secs
         iters += 1
-    return {"value": total_seg / total_t / 1e6, "unit": "Mray/s", "cores": 1, "kind": "port",
+    return {"value": total_seg / total_t / 1e6, "unit": "Mray/s", "cores": 1, "kind": "port", "host": _host_cpu(),
             "sample": f"{iters} iteration(s) of cornell.json 800x800 DEPTH 8 default flags, "
                       f"{total_seg} segments in {total_t:.2f} s (oracle/pt_oracle.cpp, g++ -O2, 1 thread)"}
 
@@ -80,7 +93,7 @@ def cpu_baseline_scan(n: int = 1 << 20, reps: int = 50) -> dict:
     out = np.zeros_like(a)
     O.lib().oracle_scan(n, out.ctypes.data, a.ctypes.data)  # warm
     ms = O.lib().oracle_time_scan_ms(n, a.ctypes.data, out.ctypes.data, reps) / reps
-    return {"n": n, "ms": ms, "GB/s": 8.0 * n / (ms * 1e-3) / 1e9, "cores": 1, "kind": "port",
+    return {"n": n, "ms": ms, "GB/s": 8.0 * n / (ms * 1e-3) / 1e9, "cores": 1, "kind": "port", "host": _host_cpu(),
             "sample": f"CPU::scan restated (oracle/sc_oracle.cpp), {reps} reps, U[0,50) seed 1234"}
 
 
