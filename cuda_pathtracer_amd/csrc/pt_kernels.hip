@@ -66,6 +66,9 @@ struct SceneDev {
     int32_t ngeoms, nmats, ntris, nnodes;
     int32_t bvh_depth;     // deepest interior node (root = 0): bounds the traversal stack
     float abs_slack;       // absolute slack of the world-distance lower bounds (bound_geom)
+    const struct DPair* __restrict__ pairs;   // child-pair layout of the BVH (bvh_walk_pairs)
+    int32_t root_code;     // code of the root (see DPair), meaningful when pairs != nullptr
+    v4f root_lo, root_hi;  // root box
 };
 struct CamDev {
     float pos[3], view[3], up[3], right[3], pl[2];
@@ -278,10 +281,73 @@ struct PrivStack {
     __device__ void set(int i, int v) const { a[i] = v; }
 };
 
+// Child-pair layout of the same tree: one 64-byte entry per INTERIOR node holding both children's
+// boxes and codes, so deciding where to go from a node costs one fetch instead of one per child.
+//   code >= 0: interior child, entry index * 4 + its split axis;
+//   code <  0: leaf child, -(first triangle * 256 + triangle count) - 1.
+// The boxes tested, their outcomes (aabb_hit) and the near-first order are those of bvh_walk:
+// a child is tested at its parent instead of after being popped, and only passing children are
+// pushed, so the triangles tested, their order and the result are the same; used without the
+// bvh_cull extension and when the tree is shallow enough for the LDS stack (no overflow case).
+struct alignas(16) DPair {
+    v4f lmin, lmax, rmin, rmax;   // .w: left code (lmin.w), unused (lmax.w), right code (rmin.w), unused
+};
+
+template <class Stack>
+__device__ __forceinline__ MeshHit bvh_walk_pairs(const SceneDev& S, f3 o, f3 d, Stack stack) {
+    MeshHit r{false, -1, -1, kFLT_MAX, 0.f, 0.f};
+    const bool neg[3] = {d.x < 0.0f, d.y < 0.0f, d.z < 0.0f};
+    const f3 inv = F3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    {
+        const float bmin[3] = {S.root_lo[0], S.root_lo[1], S.root_lo[2]}, bmax[3] = {S.root_hi[0], S.root_hi[1], S.root_hi[2]};
+        if (!aabb_hit(bmin, bmax, o, inv)) return r;
+    }
+    int top = 0, cur = S.root_code;
+    for (;;) {
+        if (cur < 0) {   // leaf
+            const int c = -cur - 1, first = c >> 8, count = c & 255;
+            for (int k = 0; k < count; ++k) {
+                const DTri tr = S.tris[first + k];
+                float bx, by, bz;
+                if (ray_tri(tr, o, d, bx, by, bz)) {
+                    r.any = true;
+                    if (r.t == -1.0f || bz < r.t) {
+                        r.t = bz; r.bx = bx; r.by = by; r.id = __float_as_int(tr.a[3]); r.idx = first + k;
+                    }
+                }
+            }
+            if (top == 0) break;
+            cur = stack.get(--top);
+            continue;
+        }
+        const DPair P = S.pairs[cur >> 2];
+        const int axis = cur & 3;
+        float lo;
+        const float lmn[3] = {P.lmin[0], P.lmin[1], P.lmin[2]}, lmx[3] = {P.lmax[0], P.lmax[1], P.lmax[2]};
+        const float rmn[3] = {P.rmin[0], P.rmin[1], P.rmin[2]}, rmx[3] = {P.rmax[0], P.rmax[1], P.rmax[2]};
+        const bool hl = aabb_hit(lmn, lmx, o, inv, lo), hr = aabb_hit(rmn, rmx, o, inv, lo);
+        const int cl = __float_as_int(P.lmin[3]), cr = __float_as_int(P.rmin[3]);
+        const bool ng = axis == 0 ? neg[0] : (axis == 1 ? neg[1] : neg[2]);   // right child first
+        const bool h1 = ng ? hr : hl, h2 = ng ? hl : hr;
+        const int c1 = ng ? cr : cl, c2 = ng ? cl : cr;
+        if (h1) {
+            if (h2) stack.set(top++, c2);
+            cur = c1;
+        } else if (h2) {
+            cur = c2;
+        } else {
+            if (top == 0) break;
+            cur = stack.get(--top);
+        }
+    }
+    return r;
+}
+
 __device__ MeshHit bvh_traverse(const SceneDev& S, f3 o, f3 d, bool cull) {
     if (S.nnodes == 0) return MeshHit{false, -1, -1, kFLT_MAX, 0.f, 0.f};
     if (S.bvh_depth < kLdsStack) {
         __shared__ int s_stack[kLdsStack * kBlock];
+        if (S.pairs && !cull) return bvh_walk_pairs(S, o, d, LdsStack{s_stack + threadIdx.x});
         return bvh_walk(S, o, d, cull, LdsStack{s_stack + threadIdx.x});
     }
     int stack[64];
@@ -1520,6 +1586,11 @@ float bits_to_float(int32_t v) {
     std::memcpy(&f, &v, 4);
     return f;
 }
+int32_t __float_as_int_host(float f) {
+    int32_t v;
+    std::memcpy(&v, &f, 4);
+    return v;
+}
 
 Affine to_affine(const float* m) {   // glm column-major 4x4 -> 3x4 + the exact w=0 terms
     Affine a;
@@ -1830,6 +1901,41 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
                     depth[(size_t)S.bvh[i].rchild_idx] = depth[i] + 1;
             }
         A.S.bvh_depth = deepest;
+        // child-pair layout (bvh_walk_pairs): leaves of <= 255 triangles, triangle ids < 2^23
+        bool fits = S.triangles.size() < (1u << 23);
+        for (const DNode& n : nodes)
+            if (__float_as_int_host(n.lo[3]) > 255) fits = false;
+        if (fits) {
+            std::vector<int32_t> pid(nodes.size(), -1);
+            int32_t np = 0;
+            for (size_t i = 0; i < nodes.size(); ++i)
+                if (__float_as_int_host(nodes[i].lo[3]) <= 0) pid[i] = np++;
+            auto code = [&](size_t i) -> int32_t {
+                const int32_t meta = __float_as_int_host(nodes[i].lo[3]), link = __float_as_int_host(nodes[i].hi[3]);
+                if (meta > 0) return -(link * 256 + meta) - 1;
+                return pid[i] * 4 + (-meta - 1);
+            };
+            std::vector<DPair> pairs((size_t)std::max(np, 1));
+            for (size_t i = 0; i < nodes.size(); ++i) {
+                if (pid[i] < 0) continue;
+                const size_t L = i + 1, R = (size_t)__float_as_int_host(nodes[i].hi[3]);
+                DPair& q = pairs[(size_t)pid[i]];
+                for (int k = 0; k < 3; ++k) {
+                    q.lmin[k] = nodes[L].lo[k]; q.lmax[k] = nodes[L].hi[k];
+                    q.rmin[k] = nodes[R].lo[k]; q.rmax[k] = nodes[R].hi[k];
+                }
+                q.lmin[3] = bits_to_float(code(L));
+                q.rmin[3] = bits_to_float(code(R));
+                q.lmax[3] = q.rmax[3] = 0.0f;
+            }
+            DPair* d_pairs;
+            if (int rc = c->alloc(&d_pairs, pairs.size())) return bail(rc);
+            if ((e = hipMemcpy(d_pairs, pairs.data(), pairs.size() * sizeof(DPair), hipMemcpyHostToDevice)) != hipSuccess)
+                return bail(pt::fail(PT_ERR_HIP, std::string("bvh pair upload: ") + hipGetErrorString(e)));
+            A.S.pairs = d_pairs;
+            A.S.root_code = code(0);
+            for (int k = 0; k < 4; ++k) { A.S.root_lo[k] = nodes[0].lo[k]; A.S.root_hi[k] = nodes[0].hi[k]; }
+        }
     }
     if (!S.textures.empty()) {
         std::vector<DTexture> tx(S.textures.size());
