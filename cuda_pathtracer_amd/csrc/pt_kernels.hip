@@ -1130,6 +1130,9 @@ __global__ __launch_bounds__(kBlock) void k_bounce(const KArgs A) {
             const Hit h = closest_hit<MESH, false>(A.S, A.fl, s_geoms, p.o, p.d, &A.stats->bound_mismatch);
             STAMP(t2);
             const int key = A.fl.rng_pixel ? slot_pixel(A.cam, A.tile, p.slot) : i - it_base;
+            // every path entering bounce b has b bounces behind it: a wave-uniform value, so the
+            // shading RNG's (iteration, remaining depth) hash is computed once per wave on the SALU
+            p.bounces = A.bounce;
             alive = lds_mats ? shade(A.S, A.fl, A.tile.depth, iter, key, p, h, s_mats)
                              : shade(A.S, A.fl, A.tile.depth, iter, key, p, h, A.S.mats);
             if (!alive) {
