@@ -40,9 +40,9 @@ constexpr int kBlock = 256;
 struct PathSoA {
     v4f *a, *b, *c;
 };
-struct HitSoA {
-    float *t, *nx, *ny, *nz, *u, *v;
-    int32_t* mat;
+struct HitSoA {   // sorted pipeline: hit record of physical path j, two 16-byte planes
+    v4f* tn;      // (t, n.x, n.y, n.z)
+    v4f* uvm;     // (u, v, material bits, 0)
 };
 struct Ctl {            // per-parity control block (32 B)
     uint32_t ticket;       // claimed tile schedule (look-back kernels)
@@ -1363,11 +1363,9 @@ __global__ __launch_bounds__(kBlock) void k_sort_isect(const KArgs A, const Sort
                 p.d = F3(pa[3], pb[0], pb[1]);
             }
             const Hit h = closest_hit<MESH, true>(A.S, A.fl, s_geoms, p.o, p.d, &A.stats->bound_mismatch);
-            A.hit.t[j] = h.t;
-            A.hit.nx[j] = h.n.x; A.hit.ny[j] = h.n.y; A.hit.nz[j] = h.n.z;
-            A.hit.u[j] = h.u; A.hit.v[j] = h.v;
+            A.hit.tn[j] = v4f{h.t, h.n.x, h.n.y, h.n.z};
             key = h.t == -1.0f ? 0 : h.mat;     // misses keep the memset materialId 0 (pathtrace.cu:466)
-            A.hit.mat[j] = key;
+            A.hit.uvm[j] = v4f{h.u, h.v, __int_as_float(key), 0.0f};
             SA.keys[i] = key;
             SA.phys[i] = j;
         }
@@ -1452,11 +1450,12 @@ __global__ __launch_bounds__(kBlock) void k_sort_shade(const KArgs A, const Sort
             const int j = SA.perm[idx];
             load_path(A.in, j, p);
             Hit h;
-            h.t = A.hit.t[j];
-            h.n = F3(A.hit.nx[j], A.hit.ny[j], A.hit.nz[j]);
-            h.mat = A.hit.mat[j];
-            h.u = A.hit.u[j];
-            h.v = A.hit.v[j];
+            const v4f tn = A.hit.tn[j], uvm = A.hit.uvm[j];
+            h.t = tn[0];
+            h.n = F3(tn[1], tn[2], tn[3]);
+            h.mat = __float_as_int(uvm[2]);
+            h.u = uvm[0];
+            h.v = uvm[1];
             // key: sorted index within the path's own iteration
             const int key = A.fl.rng_pixel ? slot_pixel(A.cam, A.tile, p.slot) : idx - it_base;
             alive = lds_mats ? shade(A.S, A.fl, A.tile.depth, iter, key, p, h, s_mats)
@@ -2025,10 +2024,9 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
         return bail(pt::fail(PT_ERR_HIP, std::string("hipMemset: ") + hipGetErrorString(e)));
     // hit SoA + sort buffers (material-sorted mode)
     {
-        float** f[6] = {&A.hit.t, &A.hit.nx, &A.hit.ny, &A.hit.nz, &A.hit.u, &A.hit.v};
-        for (auto* p : f)   // indexed by physical path index (< path_cap)
-            if (int rc = c->alloc(p, c->path_cap)) return bail(rc);
-        if (int rc = c->alloc(&A.hit.mat, c->path_cap)) return bail(rc);
+        // indexed by physical path index (< path_cap)
+        if (int rc = c->alloc(&A.hit.tn, c->path_cap)) return bail(rc);
+        if (int rc = c->alloc(&A.hit.uvm, c->path_cap)) return bail(rc);
         if (int rc = c->alloc(&c->phys, (size_t)P)) return bail(rc);
         c->max_t64 = (int)((P + 63) / 64);
         // [iteration][material][tile]: each iteration starts a fresh tile (+1: the end offset)
