@@ -479,10 +479,16 @@ __device__ unsigned long long g_stamps[16];   // [0..5] phases, [8..] closest-hi
 #endif
 
 constexpr int kLdsGeoms = 32;
-struct alignas(16) LGeom {   // what the exact tests and the hit normal read: 47 words, 192 bytes
+// What the exact tests and the hit normal read: 47 words, padded to a 52-word (208-byte) row so
+// the rows of up to 16 geoms start in distinct 4-bank windows — lanes of a wave testing different
+// geoms read without LDS bank conflicts (a 48-word row put rows r and r+4 on the same banks:
+// SQ_LDS_BANK_CONFLICT 6.8 M cycles per bounce launch).
+struct alignas(16) LGeom {
     Affine inv, xf, itr;
     int32_t type, material;
+    int32_t pad[5];
 };
+static_assert(sizeof(LGeom) == 208, "LGeom row stride");
 constexpr float kInf = __builtin_inff();
 
 __device__ __forceinline__ void stage_geoms(const SceneDev& S, LGeom* s_geoms) {
