@@ -125,6 +125,31 @@ def scan_bench(torch, dev, n: int, reps: int) -> dict:
                          "frac": gbs / HBM_PEAK_GBS, "traffic": traffic}}
 
 
+def compact_bench(torch, dev, n: int, reps: int) -> dict:
+    """sc_compact_i32 (Efficient::compact, efficient.cu:185-219) on n ints U[0,4) (SC/src/main.cpp's
+    compaction input shape, ~75% kept): algorithmic bytes = 4 B read per element + 4 B per kept."""
+    from cuda_pathtracer_amd._native import check_sc, lib
+    g = torch.Generator(device=dev).manual_seed(4321)
+    a = torch.randint(0, 4, (n,), dtype=torch.int32, device=dev, generator=g)
+    out = torch.empty_like(a)
+    cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+    ws = torch.empty(int(lib().sc_workspace_bytes(n)), dtype=torch.uint8, device=dev)
+    st = torch.cuda.current_stream()
+    for _ in range(3):
+        check_sc(lib().sc_compact_i32(a.data_ptr(), out.data_ptr(), n, cnt.data_ptr(), ws.data_ptr(), st.cuda_stream))
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for e0, e1 in ev:
+        e0.record(st)
+        check_sc(lib().sc_compact_i32(a.data_ptr(), out.data_ptr(), n, cnt.data_ptr(), ws.data_ptr(), st.cuda_stream))
+        e1.record(st)
+    torch.cuda.synchronize()
+    ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in ev]))
+    kept = int(cnt.item())
+    ok = kept == int((a != 0).sum().item()) and bool(torch.equal(out[:kept], a[a != 0]))
+    gbs = (4.0 * n + 4.0 * kept) / (ms * 1e-3) / 1e9
+    return {"n": n, "kept": kept, "ms": ms, "GB/s": gbs, "frac": gbs / HBM_PEAK_GBS, "verified": ok}
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -307,6 +332,7 @@ def main() -> None:
         }
         if not args.no_scan:
             result["scan"] = scan_bench(torch, dev, args.scan_n, args.scan_reps)
+            result["compact"] = compact_bench(torch, dev, args.scan_n, max(3, args.scan_reps // 2))
         if world == 1 and not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline_render(args.cpu_seconds)
             result["cpu_baseline_scan"] = cpu_baseline_scan()

@@ -242,12 +242,33 @@ __device__ __forceinline__ void lag_resolve(const LagTile& L, uint32_t* s_excl, 
 
 // Outputs of a resolved tile, values from LDS parity `par`.
 template <int MODE>
-__device__ __forceinline__ void lag_store(const LagTile& L, int par, const int32_t (*s_data)[kTile],
+__device__ __forceinline__ void lag_store(const LagTile& L, int par, int32_t (*s_data)[kTile],
                                           const uint32_t* s_excl, int num_tiles, int32_t* __restrict__ out,
                                           int64_t* __restrict__ d_count, int32_t* __restrict__ dead) {
     const int tid = threadIdx.x;
     const uint32_t excl = *s_excl;
     const int64_t base = (int64_t)L.tile * kTile;
+    if (MODE == kCompact || MODE == kIndices) {
+        // Compact the tile in LDS (in place of its raw values), then write it out with
+        // wave-contiguous stores: a per-lane `out[run++]` store scatters 4-byte writes across
+        // the wave's 64 different runs.
+        v4i v[kChunks];
+#pragma unroll
+        for (int k = 0; k < kChunks; ++k) v[k] = *reinterpret_cast<const v4i*>(&s_data[par][k * (kThreads * 4) + 4 * tid]);
+        lds_barrier();   // every thread has its values: the buffer can be overwritten
+#pragma unroll
+        for (int k = 0; k < kChunks; ++k) {
+            uint32_t run = L.pre[k];
+            const int64_t e0 = base + (int64_t)k * (kThreads * 4) + 4 * tid;
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if (v[k][e] != 0) s_data[par][run++] = MODE == kCompact ? v[k][e] : (int32_t)(e0 + e);
+        }
+        lds_barrier();
+        for (uint32_t j = tid; j < L.total; j += kThreads) out[(int64_t)excl + j] = s_data[par][j];
+        if (tid == 0 && L.tile == num_tiles - 1) store_count<MODE>(d_count, excl + L.total);
+        return;
+    }
 #pragma unroll
     for (int k = 0; k < kChunks; ++k) {
         const v4i v = *reinterpret_cast<const v4i*>(&s_data[par][k * (kThreads * 4) + 4 * tid]);
