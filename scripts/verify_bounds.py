@@ -4,7 +4,7 @@ or normal bits is counted (PT_AMD_VERIFY_BOUNDS=1, split pipeline, whose rays ar
 kernel's).  Scenes: cornell.json, config 4's multi-object room at reduced size, and randomized
 stress scenes (rotated, thin, overlapping cubes and spheres, glass).  Exit status 1 on any mismatch.
 
-usage: python scripts/verify_bounds.py [passes]
+usage: python scripts/verify_bounds.py [passes] [random scenes]
 """
 import os
 import sys
@@ -23,7 +23,8 @@ out = ROOT / "gpurun_out" / "verify_scenes"
 cases = [("cornell", str(ROOT / "tests" / "scenes" / "cornell.json"), None, False),
          ("cornell_sorted", str(ROOT / "tests" / "scenes" / "cornell.json"), None, True),
          ("multi_object", SG.multi_object(out, res=(960, 540)), None, False)]
-cases += [(f"random_primitives_{s}", SG.random_primitives(out, seed=s), None, s % 2 == 1) for s in range(1, 7)]
+nrand = int(sys.argv[2]) if len(sys.argv) > 2 else 6
+cases += [(f"random_primitives_{s}", SG.random_primitives(out, seed=s), None, s % 2 == 1) for s in range(1, nrand + 1)]
 bad = 0
 for name, path, _, sort in cases:
     sc = P.Scene(path)
