@@ -453,3 +453,18 @@ def test_bad_batch_size_is_rejected(cornell_path, spp):
     from cuda_pathtracer_amd import PathTracer, PtError, Scene
     with pytest.raises(PtError):
         PathTracer(Scene(cornell_path), _gui(), spp=spp)
+
+
+@pytest.mark.parametrize("kw", [dict(), dict(sortbyMaterial=True)])
+def test_every_path_misses(cornell_path, kw):
+    """Camera looking away from the scene: every camera ray misses at bounce 0, later bounces run
+    with no live path (empty segment tables, idle workgroups) — zero image, no device error."""
+    from cuda_pathtracer_amd import PathTracer, Scene
+    s = Scene(cornell_path)
+    s.set_camera((40, 30), 45.0, (0, 5, 10.5), (0, 5, 30.0), (0, 1, 0))
+    s.finalize()
+    o = O.OracleScene.from_json(cornell_path)
+    o.set_camera((40, 30), 45.0, (0, 5, 10.5), (0, 5, 30.0), (0, 1, 0))
+    g, r, st, live = _run(s, o, _gui(**kw), iters=6, spp=3)
+    _assert_bitexact(g, r, f"all miss {kw}")
+    assert st["bounce_live"][0] == 6 * 40 * 30 and st["bounce_live"][1] == 0 and not g.any()
