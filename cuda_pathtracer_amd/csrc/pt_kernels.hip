@@ -3,18 +3,23 @@
 //
 // Reference: path_tracer/src/pathtrace.cu:183-528 (generateRayFromCamera, computeIntersections,
 // shadeMaterials, relocate_terminated_paths, finalGather), intersections.cu, interactions.cu,
-// sceneStructs.h.  MI355X design (DESIGN.md):
-//   * path state and hit records are structure-of-arrays (4-byte lanes, wave-coalesced);
-//   * one persistent 256-thread workgroup loop per bounce: each tile of 256 paths is loaded,
-//     intersected (geoms are wave-uniform -> scalar loads), shaded, and the survivors are
-//     written to the next buffer at their stable rank (wave ballot + mbcnt, 4 wave counts in
-//     LDS, decoupled look-back across tiles).  No hit-record round trip, no memset of all W*H
-//     hit records per bounce, no host round trip for the live count (it stays on the device);
+// sceneStructs.h.  MI355X design (DESIGN.md §2-4):
+//   * path state as three 16-byte planes per path (one dwordx4 per plane, wave-contiguous);
+//   * k_bounce, one launch per bounce: [raygen] -> bounded closest hit (conservative bounds pass
+//     over all geoms, exact reference tests only for candidates) -> shading -> survivors written
+//     in order into this workgroup's segment (wave ballot + mbcnt, 4 wave counts in LDS).  The
+//     next launch scans the segment words in LDS, so no workgroup waits on another; no hit-record
+//     round trip, no memset of W*H hit records per bounce, no host round trip for the live count;
+//   * batched passes: workgroups are dealt to iterations, shading keys are per-iteration
+//     compacted indices, so a pass of spp iterations equals spp pathtrace() calls bit for bit;
 //   * a path's radiance is added to the framebuffer the moment it terminates (each pixel owns
 //     one path per iteration, so this equals finalGather); spp > 1 passes write per-slot colours
 //     and a finalize kernel adds them in sample order;
-//   * material-sorted shading (flag) = stable counting sort: per-wave key histograms, one device
-//     scan, a rank scatter, then a shade+compact kernel reading paths through the permutation.
+//   * material-sorted shading (flag) = stable counting sort over (iteration, material) keys:
+//     k_sort_isect (hit + histogram), one library scan, k_sort_scatter, k_sort_shade (shade in
+//     sorted order + segmented compaction);
+//   * the split pipeline (PT_PIPELINE=split: k_trace + look-back k_compact_paths) is kept for
+//     comparison and for the bounded-hit verification mode.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
