@@ -86,6 +86,34 @@ def cpu_baseline_render(seconds_target: float) -> dict:
                       f"{total_seg} segments in {total_t:.2f} s (oracle/pt_oracle.cpp, g++ -O2, 1 thread)"}
 
 
+def cpu_baseline_render_mt(seconds_target: float, threads: int) -> dict:
+    """The same oracle on `threads` host cores: each thread renders the rows y % threads == t of
+    every iteration (independent pixel shards, as the GPUs of bench.py do; ctypes releases the
+    GIL during the C call).  A labelled multithreaded variant of the reference's serial CPU path."""
+    import threading
+    from oracle import binding as O
+    sc = O.OracleScene.from_json(ROOT / "tests" / "scenes" / "cornell.json")
+    fl = O.flags()
+    total_seg, iters = 0, 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds_target and iters < 256:
+        lives = [None] * threads
+
+        def work(r, it=iters + 1):
+            lives[r] = O.render_pass(sc, fl, it, rank=r, world=threads)[1]
+        ts = [threading.Thread(target=work, args=(r,)) for r in range(threads)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        total_seg += sum(sum(lv) for lv in lives)
+        iters += 1
+    secs = time.perf_counter() - t0
+    return {"value": total_seg / secs / 1e6, "unit": "Mray/s", "cores": threads, "kind": "port", "host": _host_cpu(),
+            "sample": f"{iters} iteration(s) of cornell.json 800x800 DEPTH 8 default flags on {threads} threads "
+                      f"(row shards), {total_seg} segments in {secs:.2f} s (oracle/pt_oracle.cpp, g++ -O2)"}
+
+
 def cpu_baseline_scan(n: int = 1 << 20, reps: int = 50) -> dict:
     from oracle import binding as O
     a = np.random.default_rng(1234).integers(0, 50, n, dtype=np.int32)
@@ -335,6 +363,8 @@ def main() -> None:
             result["compact"] = compact_bench(torch, dev, args.scan_n, max(3, args.scan_reps // 2))
         if world == 1 and not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline_render(args.cpu_seconds)
+            # labelled multithreaded variant: 16 host threads (the box's CPU share per GPU)
+            result["cpu_baseline_mt"] = cpu_baseline_render_mt(args.cpu_seconds / 2, min(16, os.cpu_count() or 1))
             result["cpu_baseline_scan"] = cpu_baseline_scan()
         else:
             result["cpu_baseline"] = None
