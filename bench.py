@@ -2,7 +2,7 @@
 
 Workload (BASELINE.json configs[1]): path_tracer/scenes/cornell.json as-is — 800x800, DEPTH 8,
 default flags.  A step is one render pass.  On N GPUs (one process per GPU, torchrun) rank r owns
-the image rows y % N == r; a pass traces `--spp` (default 16) iterations of those rows per GPU
+the image rows y % N == r; a pass traces `--spp` (default 32) iterations of those rows per GPU
 share, i.e. spp*N samples per pixel of the rank's rows, so every GPU traces spp*800*800 camera
 paths per step (weak scaling).  Batching iterations into one pass is bit-identical to tracing
 them one pass at a time (tests/test_render_gpu.py::test_tiles_and_batched_samples); it fills the
@@ -194,7 +194,7 @@ def main() -> None:
                     help="BASELINE.json workload: cornell (configs[1], the default line) or configs 3-5 "
                          "generated by cuda_pathtracer_amd.scenes")
     ap.add_argument("--bvh-cull", action="store_true", help="pt_flags.bvh_cull extension (mesh scenes)")
-    ap.add_argument("--spp", type=int, default=16,
+    ap.add_argument("--spp", type=int, default=32,
                     help="iterations traced together per pass and GPU (a pass covers spp x N iterations of "
                          "the rank's rows; results are bit-identical to one iteration per pass)")
     args = ap.parse_args()
@@ -251,6 +251,8 @@ def main() -> None:
     scene = P.Scene(scene_path)
     st_r = scene.state()
     spp = world * max(1, args.spp)
+    if spp > 256:   # pt_shard.spp limit (one thread of the bounce kernel's workgroup per iteration)
+        raise SystemExit(f"--spp {args.spp} x {world} GPUs = {spp} iterations per pass > 256")
     pt = P.PathTracer(scene, gui, rank=rank, world=world, spp=spp)
     stream = torch.cuda.current_stream()
     _log(rank, f"[bench] tile rows={pt.rows} npix={pt.npix} paths/pass={pt.npaths} depth={st_r.traceDepth}")

@@ -1078,11 +1078,11 @@ __global__ __launch_bounds__(kBlock) void k_bounce(const KArgs A) {
     int N, nseg_in = 0, chunk_in = 0;
     if (FIRST) {
         N = A.n_fixed;
-        if (tid <= spp) s_ib[tid] = tid * A.tile.npix;
+        for (int j = tid; j <= spp; j += kBlock) s_ib[j] = j * A.tile.npix;   // spp + 1 entries (spp <= kBlock)
         __syncthreads();
         plan_layout(s_ib, spp, (int)gridDim.x, (int)blockIdx.x, s_lay, s_tmp);
     } else {
-        if (tid <= spp) s_ib[tid] = -1;
+        for (int j = tid; j <= spp; j += kBlock) s_ib[j] = -1;
         nseg_in = (int)A.ctl[par].nseg;
         chunk_in = (int)A.ctl[par].chunk;
         N = scan_segments(reinterpret_cast<const uint32_t*>(A.seg) + (size_t)par * kMaxSeg, nseg_in, spp, s_pre, s_ib,
@@ -1326,10 +1326,10 @@ __global__ __launch_bounds__(kBlock) void k_sort_isect(const KArgs A, const Sort
     int N, nseg_in = 0, chunk_in = 0;
     if (FIRST) {
         N = A.n_fixed;
-        if (tid <= spp) s_ib[tid] = tid * A.tile.npix;
+        for (int j = tid; j <= spp; j += kBlock) s_ib[j] = j * A.tile.npix;   // spp + 1 entries (spp <= kBlock)
         __syncthreads();
     } else {
-        if (tid <= spp) s_ib[tid] = -1;
+        for (int j = tid; j <= spp; j += kBlock) s_ib[j] = -1;
         nseg_in = (int)A.ctl[par].nseg;
         chunk_in = (int)A.ctl[par].chunk;
         N = scan_segments(reinterpret_cast<const uint32_t*>(A.seg) + (size_t)par * kMaxSeg, nseg_in, spp, s_pre, s_ib,
@@ -1340,7 +1340,7 @@ __global__ __launch_bounds__(kBlock) void k_sort_isect(const KArgs A, const Sort
     __syncthreads();
     const int T = s_tb[spp];
     if (blockIdx.x == 0) {
-        if (tid <= spp) { SA.tbase[tid] = s_tb[tid]; SA.ibase[tid] = s_ib[tid]; }
+        for (int j = tid; j <= spp; j += kBlock) { SA.tbase[j] = s_tb[j]; SA.ibase[j] = s_ib[j]; }
         if (tid == 0) {
             A.ctl[par ^ 1].hist_t64 = (uint32_t)T;
             A.ctl[par].live = (uint32_t)N;   // for k_sort_scatter / k_sort_shade of this bounce
@@ -1395,7 +1395,7 @@ __global__ __launch_bounds__(kBlock) void k_sort_scatter(const KArgs A, const So
     __shared__ int32_t s_ib[kMaxSpp + 1], s_tb[kMaxSpp + 1];
     const int tid = threadIdx.x, lane = tid & 63;
     const int spp = A.tile.spp;
-    if (tid <= spp) { s_ib[tid] = SA.ibase[tid]; s_tb[tid] = SA.tbase[tid]; }
+    for (int j = tid; j <= spp; j += kBlock) { s_ib[j] = SA.ibase[j]; s_tb[j] = SA.tbase[j]; }
     __syncthreads();
     const int T = s_tb[spp];
     const int nmats = A.S.nmats;
@@ -1432,7 +1432,7 @@ __global__ __launch_bounds__(kBlock) void k_sort_shade(const KArgs A, const Sort
     const int spp = A.tile.spp;
     const int nmats = A.S.nmats;
     // sorted start of every iteration: the scanned histogram at its first tile
-    if (tid <= spp) s_sb[tid] = SA.offs[(size_t)nmats * SA.tbase[tid]];
+    for (int j = tid; j <= spp; j += kBlock) s_sb[j] = SA.offs[(size_t)nmats * SA.tbase[j]];
     __syncthreads();
     plan_layout(s_sb, spp, (int)gridDim.x, (int)blockIdx.x, s_lay, s_tmp);
     const int tpb = __builtin_amdgcn_readfirstlane(s_lay[0]);

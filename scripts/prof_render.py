@@ -1,5 +1,5 @@
 """Render-only workload for rocprofv3 (no torch kernels, no scan): N passes of cornell 800x800,
-`spp=K` iterations per pass (default 16, like bench.py)."""
+`spp=K` iterations per pass (default 32, like bench.py)."""
 import sys
 from pathlib import Path
 ROOT = Path(__file__).resolve().parent.parent
@@ -10,7 +10,7 @@ import cuda_pathtracer_amd as P
 
 passes = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 sort = "sort" in sys.argv[2:]
-spp = next((int(a[4:]) for a in sys.argv[2:] if a.startswith("spp=")), 16)   # bench.py's default batch
+spp = next((int(a[4:]) for a in sys.argv[2:] if a.startswith("spp=")), 32)   # bench.py's default batch
 s = P.Scene(str(ROOT / "tests" / "scenes" / "cornell.json"))
 g = P.GuiDataContainer()
 g.sortbyMaterial = sort

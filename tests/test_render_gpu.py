@@ -120,7 +120,8 @@ def test_materials_reflective_refractive():
     assert st["bounce_live"] == live
 
 
-@pytest.mark.parametrize("rank,world,spp", [(0, 2, 1), (1, 2, 1), (0, 1, 2), (1, 3, 3), (2, 4, 4), (0, 1, 100)])
+@pytest.mark.parametrize("rank,world,spp", [(0, 2, 1), (1, 2, 1), (0, 1, 2), (1, 3, 3), (2, 4, 4), (0, 1, 100),
+                                             (3, 8, 256)])
 def test_tiles_and_batched_samples(cornell_path, rank, world, spp):
     s, o = _pair(cornell_path, (40, 36))
     g, r, st, live = _run(s, o, _gui(), iters=spp * 2, rank=rank, world=world, spp=spp)
@@ -468,3 +469,13 @@ def test_every_path_misses(cornell_path, kw):
     g, r, st, live = _run(s, o, _gui(**kw), iters=6, spp=3)
     _assert_bitexact(g, r, f"all miss {kw}")
     assert st["bounce_live"][0] == 6 * 40 * 30 and st["bounce_live"][1] == 0 and not g.any()
+
+
+@pytest.mark.parametrize("kw", [dict(), dict(sortbyMaterial=True)])
+def test_max_batch_256_iterations(cornell_path, kw):
+    """pt_shard.spp at its limit (256 = one thread of the bounce kernel's workgroup per iteration,
+    the bench's 8-GPU pass): GPU == oracle bit for bit."""
+    s, o = _pair(cornell_path, (12, 10))
+    g, r, st, live = _run(s, o, _gui(**kw), iters=256, spp=256)
+    _assert_bitexact(g, r, f"spp=256 {kw}")
+    assert st["bounce_live"] == live
