@@ -2009,6 +2009,8 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
         c->path_cap = (size_t)kBlock * (size_t)(tiles + sh.spp * tpb);
         if (tpb * kBlock > (long long)kSegCountMask)
             return bail(pt::fail(PT_ERR_ARG, "pass too large for the bounce kernel's segment words (chunk >= 2^24)"));
+        if (c->path_cap > (size_t)0x7fffffff)
+            return bail(pt::fail(PT_ERR_ARG, "pass too large: path buffer index exceeds int32"));
     }
     for (int b = 0; b < 2; ++b)
         if (int rc = alloc_paths(c, c->buf[b], c->path_cap)) return bail(rc);
