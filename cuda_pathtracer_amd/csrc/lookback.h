@@ -110,6 +110,44 @@ __device__ __forceinline__ uint32_t lookback(uint64_t* st, int tile, int lane, u
     return lookback_impl<WINDOWS, false>(st, tile, lane, err, w);
 }
 
+// Static-schedule alternative to the look-back (sc_kernels.hip lag_resolve): the sum of the
+// aggregates of tiles max(0, tile-G+1) .. tile-1, read by one full wave, kWinPolls x 64 per
+// round trip.  Nothing here waits on another tile's look-back, only on aggregates, which every
+// workgroup publishes as soon as it has reduced a tile.
+constexpr int kWinPolls = 8;
+
+__device__ __forceinline__ uint32_t window_sum(const uint64_t* st, int tile, int G, int lane, uint32_t* err) {
+    const int lo = tile - G + 1 > 0 ? tile - G + 1 : 0;
+    uint32_t acc = 0;
+    uint32_t spins = 0;
+    for (int top = tile - 1; top >= lo; top -= 64 * kWinPolls) {
+        uint64_t w[kWinPolls];
+#pragma unroll
+        for (int k = 0; k < kWinPolls; ++k) {
+            const int j = top - 64 * k - lane;
+            w[k] = j >= lo ? poll(st, j) : kFlagAgg;
+        }
+        for (;;) {
+            bool nr = false;
+#pragma unroll
+            for (int k = 0; k < kWinPolls; ++k) nr |= (w[k] >> 62) == 0;
+            if (__ballot(nr) == 0) break;
+            if (++spins > kSpinLimit ||
+                ((spins & 63) == 0 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)) {
+                if (lane == 0) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;   // results wrong and reported; the grid still drains
+            }
+            __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+            for (int k = 0; k < kWinPolls; ++k)
+                if ((w[k] >> 62) == 0) w[k] = poll(st, top - 64 * k - lane);
+        }
+#pragma unroll
+        for (int k = 0; k < kWinPolls; ++k) acc += (uint32_t)w[k];
+    }
+    return wave_sum(acc);
+}
+
 // ---- tile schedules ------------------------------------------------------------------------
 // STATIC (default, fastest): a grid of G workgroups that must all be resident at once (sized by
 // the host from the occupancy with headroom); workgroup b owns tiles b, b+G, b+2G, ...  No

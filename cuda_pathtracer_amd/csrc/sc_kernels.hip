@@ -6,11 +6,12 @@
 // and allocates/frees device memory on every call.  Here one launch streams each element once:
 //   tile = 256 threads x 8 x int4 = 8192 elements, loaded as wave-contiguous 16-byte vectors
 //   (chunk k of a tile is 1 KiB per wave-instruction), per-thread 4-element scan, wave64 DPP scan
-//   of the per-thread sums, 16 wave totals through LDS, then a decoupled look-back across tiles
-//   (lookback.h).  Algorithmic traffic: 8 B/element for scan (4 read + 4 write), 4 B/element +
-//   4 B/kept for compaction.
+//   of the per-thread sums, 16 wave totals through LDS, then the tile's prefix from the
+//   aggregates of the tiles before it (lookback.h: a window sum under the static schedule, a
+//   decoupled look-back when tiles are claimed).  Algorithmic traffic: 8 B/element for scan
+//   (4 read + 4 write), 4 B/element + 4 B/kept for compaction.
 //
-// Kernels: k_scan_lag (16-byte aligned pointers; the look-back of each tile is resolved one
+// Kernels: k_scan_lag (16-byte aligned pointers; the prefix of each tile is resolved one
 // iteration late, see below) and k_scan_tiles (unaligned pointers and the partial tail tile;
 // look-back resolved immediately).  Design history with measurements: DESIGN.md §4,
 // profiles/r01_scan_ab.txt.
@@ -206,6 +207,8 @@ __device__ __forceinline__ void process_tile(const v4i (&cur)[kChunks], int tile
 // of t+2G and reducing t+G: by then every predecessor's aggregate is out, so the look-back
 // rarely spins, and its round trip overlaps the loads in flight.  The deferred tile's raw values
 // wait in LDS (2 x 32 KiB ping-pong); each thread keeps only its 8 per-chunk local offsets.
+// Under the static schedule the look-back itself is replaced by a window sum (lag_resolve):
+// 0.50 -> 0.39 ms for 2^28 ints, 4.2 -> 5.5 TB/s.
 struct LagTile {
     uint32_t pre[kChunks];   // this thread's exclusive local offset of each of its chunks
     uint32_t total;          // tile aggregate
@@ -213,7 +216,7 @@ struct LagTile {
 };
 
 // Reduce tile `cur` into LDS parity `par` and publish its aggregate.
-template <int MODE>
+template <int MODE, bool WINDOW>
 __device__ __forceinline__ void lag_reduce(const v4i (&cur)[kChunks], int tile, int par, int32_t (*s_data)[kTile],
                                            uint32_t (*s_wsum)[kChunks][4], uint64_t* __restrict__ status,
                                            LagTile& L) {
@@ -225,15 +228,25 @@ __device__ __forceinline__ void lag_reduce(const v4i (&cur)[kChunks], int tile, 
     for (int k = 0; k < kChunks; ++k)
         *reinterpret_cast<v4i*>(&s_data[par][k * (kThreads * 4) + 4 * tid]) = cur[k];
     L.tile = tile;
-    if (tid == 0) lb::publish(status, tile, tile == 0 ? lb::kFlagPre : lb::kFlagAgg, L.total);
+    if (tid == 0) lb::publish(status, tile, tile == 0 && !WINDOW ? lb::kFlagPre : lb::kFlagAgg, L.total);
 }
 
 // Wave 0: resolve the deferred tile's prefix, publish it, share it through LDS.
+// WINDOW (static schedule): workgroup b owns tiles b, b+G, ..., so
+//   excl(t) = excl(t-G) + agg(t-G) + sum of agg(t') for t-G < t' < t,
+// where the first two terms are this workgroup's own `carry`.  Only aggregates are ever
+// published and a tile waits for the G-1 aggregates before it, not for a chain of inclusive
+// prefixes hopping from workgroup to workgroup (lb::window_sum).  Otherwise (claimed tiles):
+// decoupled look-back.
+template <bool WINDOW>
 __device__ __forceinline__ void lag_resolve(const LagTile& L, uint32_t* s_excl, uint64_t* __restrict__ status,
-                                            uint32_t* __restrict__ ctl) {
+                                            uint32_t* __restrict__ ctl, uint32_t& carry) {
     const int lane = threadIdx.x & 63;
     uint32_t excl = 0;
-    if (L.tile != 0) {
+    if (WINDOW) {
+        excl = carry + lb::window_sum(status, L.tile, (int)gridDim.x, lane, &ctl[1]);
+        carry = excl + L.total;
+    } else if (L.tile != 0) {
         excl = lb::lookback<kLagWindows>(status, L.tile, lane, &ctl[1]);
         if (lane == 0) lb::publish(status, L.tile, lb::kFlagPre, excl + L.total);
     }
@@ -278,21 +291,21 @@ __device__ __forceinline__ void lag_store(const LagTile& L, int par, int32_t (*s
 }
 
 // One step: prefetch `next` into `pf`, reduce `cur` (= tile), resolve + write the deferred tile.
-template <int MODE>
+template <int MODE, bool WINDOW>
 __device__ __forceinline__ void lag_step(const int32_t* __restrict__ in, const v4i (&cur)[kChunks],
                                          v4i (&pf)[kChunks], int tile, int next, int num_full, int num_tiles,
                                          int par, LagTile& prev, bool& have_prev, int32_t (*s_data)[kTile],
                                          uint32_t (*s_wsum)[kChunks][4], uint32_t* s_excl,
                                          int32_t* __restrict__ out, uint64_t* __restrict__ status,
                                          uint32_t* __restrict__ ctl, int64_t* __restrict__ d_count,
-                                         int32_t* __restrict__ dead) {
+                                         int32_t* __restrict__ dead, uint32_t& carry) {
     // unconditional (clamped) prefetch: a branch here would make the wait-count pass merge
     // "issued"/"skipped" states and drain the prefetch at the first use of the other buffer
     load_full(in, (int64_t)(next < num_full ? next : tile) * kTile, (int)threadIdx.x, pf);
     LagTile L;
-    lag_reduce<MODE>(cur, tile, par, s_data, s_wsum, status, L);
+    lag_reduce<MODE, WINDOW>(cur, tile, par, s_data, s_wsum, status, L);
     if (have_prev) {
-        if ((threadIdx.x >> 6) == 0) lag_resolve(prev, s_excl, status, ctl);
+        if ((threadIdx.x >> 6) == 0) lag_resolve<WINDOW>(prev, s_excl, status, ctl, carry);
         lds_barrier();
         lag_store<MODE>(prev, par ^ 1, s_data, s_excl, num_tiles, out, d_count, dead);
     }
@@ -320,21 +333,41 @@ __global__ __launch_bounds__(kThreads) void k_scan_tiles(const int32_t* __restri
     }
 }
 
-// 16-byte aligned pointers: tiles claimed in chunks (above), each tile's prefix resolved by
-// look-back one step late.
+// The partial tail tile under the static schedule (window prefix, see lag_resolve).
 template <int MODE>
-__global__ __launch_bounds__(kThreads) void k_scan_lag(const int32_t* __restrict__ in, int32_t* __restrict__ out,
-                                                       int64_t n, uint64_t* __restrict__ status,
-                                                       uint32_t* __restrict__ ctl, int64_t* __restrict__ d_count,
-                                                       int32_t* __restrict__ dead, int claimed) {
-    __shared__ __attribute__((aligned(16))) int32_t s_data[2][kTile];
-    __shared__ uint32_t s_wsum[2][kChunks][4];
-    __shared__ uint32_t s_excl;
-    __shared__ int s_ring[lb::kRing];
+__device__ __forceinline__ void window_tail(const v4i (&cur)[kChunks], int tile, int num_tiles, int64_t n,
+                                            int32_t* __restrict__ out, uint64_t* __restrict__ status,
+                                            uint32_t* __restrict__ ctl, int64_t* __restrict__ d_count,
+                                            int32_t* __restrict__ dead, uint32_t (&s_wsum)[kChunks][4],
+                                            uint32_t* s_excl, uint32_t carry) {
+    const int tid = threadIdx.x, lane = tid & 63;
+    uint32_t pre[kChunks];
+    const uint32_t total = tile_offsets<MODE>(cur, s_wsum, pre);
+    if ((tid >> 6) == 0) {
+        const uint32_t excl = carry + lb::window_sum(status, tile, (int)gridDim.x, lane, &ctl[1]);
+        if (lane == 0) *s_excl = excl;
+    }
+    lds_barrier();
+    const uint32_t excl = *s_excl;
+    const int64_t base = (int64_t)tile * kTile;
+#pragma unroll
+    for (int k = 0; k < kChunks; ++k)
+        write_chunk<MODE, false>(cur[k], base + (int64_t)k * (kThreads * 4) + 4 * tid, excl + pre[k], n, out, dead);
+    if (MODE != kScan && tid == 0 && tile == num_tiles - 1) store_count<MODE>(d_count, excl + total);
+}
+
+// 16-byte aligned pointers: each tile's prefix resolved one step late (above).
+template <int MODE, bool WINDOW>
+__device__ __forceinline__ void scan_lag_body(const int32_t* __restrict__ in, int32_t* __restrict__ out, int64_t n,
+                                              uint64_t* __restrict__ status, uint32_t* __restrict__ ctl,
+                                              int64_t* __restrict__ d_count, int32_t* __restrict__ dead,
+                                              int32_t (*s_data)[kTile], uint32_t (*s_wsum)[kChunks][4],
+                                              uint32_t* s_excl, int* s_ring, bool claimed) {
     const int tid = threadIdx.x;
     const int num_tiles = (int)((n + kTile - 1) / kTile);
     const int num_full = (int)(n / kTile);
-    lb::TileSeq q = lb::seq_start(claimed != 0, &ctl[kTicket], s_ring, num_tiles);
+    lb::TileSeq q = lb::seq_start(claimed, &ctl[kTicket], s_ring, num_tiles);
+    uint32_t carry = 0;   // WINDOW: excl + aggregate of this workgroup's previous tile (wave 0)
     if (q.tile < num_full) {
         // two named register buffers, loop unrolled by two: no load destination is ever copied,
         // so the wait-count pass keeps each prefetch in flight across the other buffer's step
@@ -345,29 +378,47 @@ __global__ __launch_bounds__(kThreads) void k_scan_lag(const int32_t* __restrict
         load_full(in, (int64_t)q.tile * kTile, tid, bA);
         for (;;) {
             lb::seq_step(q, &ctl[kTicket]);
-            lag_step<MODE>(in, bA, bB, q.tile, q.next, num_full, num_tiles, par, prev, have_prev, s_data, s_wsum,
-                           &s_excl, out, status, ctl, d_count, dead);
+            lag_step<MODE, WINDOW>(in, bA, bB, q.tile, q.next, num_full, num_tiles, par, prev, have_prev, s_data,
+                                   s_wsum, s_excl, out, status, ctl, d_count, dead, carry);
             lb::seq_advance(q, s_ring);
             par ^= 1;
             if (q.tile >= num_full) break;
             lb::seq_step(q, &ctl[kTicket]);
-            lag_step<MODE>(in, bB, bA, q.tile, q.next, num_full, num_tiles, par, prev, have_prev, s_data, s_wsum,
-                           &s_excl, out, status, ctl, d_count, dead);
+            lag_step<MODE, WINDOW>(in, bB, bA, q.tile, q.next, num_full, num_tiles, par, prev, have_prev, s_data,
+                                   s_wsum, s_excl, out, status, ctl, d_count, dead, carry);
             lb::seq_advance(q, s_ring);
             par ^= 1;
             if (q.tile >= num_full) break;
         }
         // drain: the last reduced tile
-        if ((tid >> 6) == 0) lag_resolve(prev, &s_excl, status, ctl);
+        if ((tid >> 6) == 0) lag_resolve<WINDOW>(prev, s_excl, status, ctl, carry);
         lds_barrier();
-        lag_store<MODE>(prev, par ^ 1, s_data, &s_excl, num_tiles, out, d_count, dead);
+        lag_store<MODE>(prev, par ^ 1, s_data, s_excl, num_tiles, out, d_count, dead);
     }
     // the partial tail tile (the last tile, so nothing waits on this workgroup after it)
     if (q.tile == num_full && num_full < num_tiles) {
         v4i cur[kChunks];
         load_guarded(in, n, (int64_t)q.tile * kTile, tid, cur);
-        process_tile<MODE>(cur, q.tile, num_tiles, n, out, status, ctl, d_count, dead, s_wsum[0], &s_excl);
+        if (WINDOW)
+            window_tail<MODE>(cur, q.tile, num_tiles, n, out, status, ctl, d_count, dead, s_wsum[0], s_excl, carry);
+        else
+            process_tile<MODE>(cur, q.tile, num_tiles, n, out, status, ctl, d_count, dead, s_wsum[0], s_excl);
     }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kThreads) void k_scan_lag(const int32_t* __restrict__ in, int32_t* __restrict__ out,
+                                                       int64_t n, uint64_t* __restrict__ status,
+                                                       uint32_t* __restrict__ ctl, int64_t* __restrict__ d_count,
+                                                       int32_t* __restrict__ dead, int claimed) {
+    __shared__ __attribute__((aligned(16))) int32_t s_data[2][kTile];
+    __shared__ uint32_t s_wsum[2][kChunks][4];
+    __shared__ uint32_t s_excl;
+    __shared__ int s_ring[lb::kRing];
+    if (claimed)
+        scan_lag_body<MODE, false>(in, out, n, status, ctl, d_count, dead, s_data, s_wsum, &s_excl, s_ring, true);
+    else
+        scan_lag_body<MODE, true>(in, out, n, status, ctl, d_count, dead, s_data, s_wsum, &s_excl, s_ring, false);
 }
 
 __global__ void k_append_dead(const int32_t* __restrict__ dead, int32_t* __restrict__ perm,
