@@ -224,9 +224,23 @@ __device__ __forceinline__ void lag_reduce(const v4i (&cur)[kChunks], int tile, 
     // tile_offsets' leading barrier also orders these writes after the previous readers of
     // s_data[par] (the store phase of the step before last)
     L.total = tile_offsets<MODE>(cur, s_wsum[par], L.pre);
+    if (MODE == kCompact || MODE == kIndices) {
+        // The kept elements' tile-local positions are known now: compact into LDS here, so the
+        // deferred store is a plain copy once the tile's prefix is resolved.
+        const int64_t base = (int64_t)tile * kTile;
 #pragma unroll
-    for (int k = 0; k < kChunks; ++k)
-        *reinterpret_cast<v4i*>(&s_data[par][k * (kThreads * 4) + 4 * tid]) = cur[k];
+        for (int k = 0; k < kChunks; ++k) {
+            uint32_t run = L.pre[k];
+            const int32_t e0 = (int32_t)(base + (int64_t)k * (kThreads * 4) + 4 * tid);
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if (cur[k][e] != 0) s_data[par][run++] = MODE == kCompact ? cur[k][e] : e0 + e;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < kChunks; ++k)
+            *reinterpret_cast<v4i*>(&s_data[par][k * (kThreads * 4) + 4 * tid]) = cur[k];
+    }
     L.tile = tile;
     if (tid == 0) lb::publish(status, tile, tile == 0 && !WINDOW ? lb::kFlagPre : lb::kFlagAgg, L.total);
 }
@@ -262,24 +276,23 @@ __device__ __forceinline__ void lag_store(const LagTile& L, int par, int32_t (*s
     const uint32_t excl = *s_excl;
     const int64_t base = (int64_t)L.tile * kTile;
     if (MODE == kCompact || MODE == kIndices) {
-        // Compact the tile in LDS (in place of its raw values), then write it out with
-        // wave-contiguous stores: a per-lane `out[run++]` store scatters 4-byte writes across
-        // the wave's 64 different runs.
-        v4i v[kChunks];
-#pragma unroll
-        for (int k = 0; k < kChunks; ++k) v[k] = *reinterpret_cast<const v4i*>(&s_data[par][k * (kThreads * 4) + 4 * tid]);
-        lds_barrier();   // every thread has its values: the buffer can be overwritten
-#pragma unroll
-        for (int k = 0; k < kChunks; ++k) {
-            uint32_t run = L.pre[k];
-            const int64_t e0 = base + (int64_t)k * (kThreads * 4) + 4 * tid;
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-                if (v[k][e] != 0) s_data[par][run++] = MODE == kCompact ? v[k][e] : (int32_t)(e0 + e);
+        // The tile was compacted in LDS by lag_reduce.  Write it out with wave-contiguous 16-byte
+        // stores (a per-lane `out[run++]` store scatters 4-byte writes across the wave's 64
+        // runs): up to 3 head elements bring out + excl to a 16-byte boundary.
+        const int32_t* src = s_data[par];
+        int32_t* dst = out + excl;
+        const uint32_t total = L.total;
+        const uint32_t head = min((4u - (excl & 3u)) & 3u, total);
+        const uint32_t quads = (total - head) >> 2;
+        if ((uint32_t)tid < head) dst[tid] = src[tid];
+        for (uint32_t q = tid; q < quads; q += kThreads) {
+            const uint32_t j = head + 4 * q;
+            const v4i v = {src[j], src[j + 1], src[j + 2], src[j + 3]};
+            __builtin_nontemporal_store(v, reinterpret_cast<v4i*>(dst + j));
         }
-        lds_barrier();
-        for (uint32_t j = tid; j < L.total; j += kThreads) out[(int64_t)excl + j] = s_data[par][j];
-        if (tid == 0 && L.tile == num_tiles - 1) store_count<MODE>(d_count, excl + L.total);
+        const uint32_t rest = head + 4 * quads;
+        if ((uint32_t)tid < total - rest) dst[rest + tid] = src[rest + tid];
+        if (tid == 0 && L.tile == num_tiles - 1) store_count<MODE>(d_count, excl + total);
         return;
     }
 #pragma unroll
