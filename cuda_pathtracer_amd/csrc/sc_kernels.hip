@@ -224,17 +224,21 @@ __device__ __forceinline__ void lag_reduce(const v4i (&cur)[kChunks], int tile, 
     // tile_offsets' leading barrier also orders these writes after the previous readers of
     // s_data[par] (the store phase of the step before last)
     L.total = tile_offsets<MODE>(cur, s_wsum[par], L.pre);
-    if (MODE == kCompact || MODE == kIndices) {
+    if (MODE != kScan) {
         // The kept elements' tile-local positions are known now: compact into LDS here, so the
-        // deferred store is a plain copy once the tile's prefix is resolved.
+        // deferred store is a plain copy once the tile's prefix is resolved.  Partition: the
+        // dropped indices follow the kept ones, in order (local position li - kept before li).
         const int64_t base = (int64_t)tile * kTile;
 #pragma unroll
         for (int k = 0; k < kChunks; ++k) {
             uint32_t run = L.pre[k];
-            const int32_t e0 = (int32_t)(base + (int64_t)k * (kThreads * 4) + 4 * tid);
+            const int li0 = k * (kThreads * 4) + 4 * tid;
 #pragma unroll
-            for (int e = 0; e < 4; ++e)
-                if (cur[k][e] != 0) s_data[par][run++] = MODE == kCompact ? cur[k][e] : e0 + e;
+            for (int e = 0; e < 4; ++e) {
+                const int32_t idx = (int32_t)(base + li0 + e);
+                if (cur[k][e] != 0) s_data[par][run++] = MODE == kCompact ? cur[k][e] : idx;
+                else if (MODE == kPartition) s_data[par][L.total + (uint32_t)(li0 + e) - run] = idx;
+            }
         }
     } else {
 #pragma unroll
@@ -267,6 +271,23 @@ __device__ __forceinline__ void lag_resolve(const LagTile& L, uint32_t* s_excl, 
     if (lane == 0) *s_excl = excl;
 }
 
+// count consecutive ints from LDS to global memory with wave-contiguous 16-byte stores (a
+// per-lane `out[run++]` store scatters 4-byte writes across the wave's 64 runs); up to 3 head
+// elements bring dst to a 16-byte boundary.
+__device__ __forceinline__ void copy_out(const int32_t* src, int32_t* __restrict__ dst, uint32_t count) {
+    const uint32_t tid = threadIdx.x;
+    const uint32_t head = min((4u - (uint32_t)((reinterpret_cast<uintptr_t>(dst) >> 2) & 3u)) & 3u, count);
+    const uint32_t quads = (count - head) >> 2;
+    if (tid < head) dst[tid] = src[tid];
+    for (uint32_t q = tid; q < quads; q += kThreads) {
+        const uint32_t j = head + 4 * q;
+        const v4i v = {src[j], src[j + 1], src[j + 2], src[j + 3]};
+        __builtin_nontemporal_store(v, reinterpret_cast<v4i*>(dst + j));
+    }
+    const uint32_t rest = head + 4 * quads;
+    if (tid < count - rest) dst[rest + tid] = src[rest + tid];
+}
+
 // Outputs of a resolved tile, values from LDS parity `par`.
 template <int MODE>
 __device__ __forceinline__ void lag_store(const LagTile& L, int par, int32_t (*s_data)[kTile],
@@ -275,24 +296,12 @@ __device__ __forceinline__ void lag_store(const LagTile& L, int par, int32_t (*s
     const int tid = threadIdx.x;
     const uint32_t excl = *s_excl;
     const int64_t base = (int64_t)L.tile * kTile;
-    if (MODE == kCompact || MODE == kIndices) {
-        // The tile was compacted in LDS by lag_reduce.  Write it out with wave-contiguous 16-byte
-        // stores (a per-lane `out[run++]` store scatters 4-byte writes across the wave's 64
-        // runs): up to 3 head elements bring out + excl to a 16-byte boundary.
-        const int32_t* src = s_data[par];
-        int32_t* dst = out + excl;
-        const uint32_t total = L.total;
-        const uint32_t head = min((4u - (excl & 3u)) & 3u, total);
-        const uint32_t quads = (total - head) >> 2;
-        if ((uint32_t)tid < head) dst[tid] = src[tid];
-        for (uint32_t q = tid; q < quads; q += kThreads) {
-            const uint32_t j = head + 4 * q;
-            const v4i v = {src[j], src[j + 1], src[j + 2], src[j + 3]};
-            __builtin_nontemporal_store(v, reinterpret_cast<v4i*>(dst + j));
-        }
-        const uint32_t rest = head + 4 * quads;
-        if ((uint32_t)tid < total - rest) dst[rest + tid] = src[rest + tid];
-        if (tid == 0 && L.tile == num_tiles - 1) store_count<MODE>(d_count, excl + total);
+    if (MODE != kScan) {
+        // The tile was compacted in LDS by lag_reduce: kept values / indices, then (partition)
+        // the dropped indices.
+        copy_out(s_data[par], out + excl, L.total);
+        if (MODE == kPartition) copy_out(s_data[par] + L.total, dead + (base - excl), kTile - L.total);
+        if (tid == 0 && L.tile == num_tiles - 1) store_count<MODE>(d_count, excl + L.total);
         return;
     }
 #pragma unroll
@@ -300,7 +309,6 @@ __device__ __forceinline__ void lag_store(const LagTile& L, int par, int32_t (*s
         const v4i v = *reinterpret_cast<const v4i*>(&s_data[par][k * (kThreads * 4) + 4 * tid]);
         write_chunk<MODE, true>(v, base + (int64_t)k * (kThreads * 4) + 4 * tid, excl + L.pre[k], 0, out, dead);
     }
-    if (MODE != kScan && tid == 0 && L.tile == num_tiles - 1) store_count<MODE>(d_count, excl + L.total);
 }
 
 // One step: prefetch `next` into `pf`, reduce `cur` (= tile), resolve + write the deferred tile.

@@ -20,6 +20,8 @@ st = torch.cuda.current_stream()
 def call():
     if op == "scan":
         check_sc(lib().sc_scan_exclusive_i32(a.data_ptr(), out.data_ptr(), n, ws.data_ptr(), st.cuda_stream))
+    elif op == "partition":
+        check_sc(lib().sc_partition_i32(a.data_ptr(), out.data_ptr(), n, cnt.data_ptr(), ws.data_ptr(), st.cuda_stream))
     else:
         check_sc(lib().sc_compact_i32(a.data_ptr(), out.data_ptr(), n, cnt.data_ptr(), ws.data_ptr(), st.cuda_stream))
 
@@ -36,6 +38,11 @@ torch.cuda.synchronize()
 ms = e0.elapsed_time(e1) / reps
 if op == "scan":
     ok = bool(torch.equal(out[1:] - out[:-1], a[:-1])) and int(out[0].item()) == 0
+    nbytes = 8 * n
+elif op == "partition":
+    idx = torch.arange(n, dtype=torch.int32, device=dev)
+    live = idx[a != 0]
+    ok = int(cnt.item()) == live.numel() and bool(torch.equal(out, torch.cat([live, idx[a == 0]])))
     nbytes = 8 * n
 else:
     kept = a[a != 0]
