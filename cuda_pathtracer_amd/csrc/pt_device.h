@@ -103,6 +103,7 @@ struct DTexture {
 };
 
 typedef float v4f __attribute__((ext_vector_type(4)));
+typedef float v2f __attribute__((ext_vector_type(2)));
 
 // Triangle hot data, 48 bytes = three 16-byte loads: (v0, id bits), (e1, 0), (e2, 0).  The edges
 // e1 = v1 - v0, e2 = v2 - v0 are computed on the host with the same single subtraction glm

@@ -45,9 +45,8 @@ constexpr int kBlock = 256;
 struct PathSoA {
     v4f *a, *b, *c;
 };
-struct HitSoA {   // sorted pipeline: hit record of physical path j, two 16-byte planes
-    v4f* tn;      // (t, n.x, n.y, n.z)
-    v4f* uvm;     // (u, v, material bits, 0)
+struct HitSoA {   // sorted pipeline, textured scenes: texture coordinates of physical path j
+    float* uv;    // [2 * P]
 };
 struct Ctl {            // per-parity control block (32 B)
     uint32_t ticket;       // claimed tile schedule (look-back kernels)
@@ -1278,6 +1277,14 @@ __global__ __launch_bounds__(kBlock) void k_compact_paths(const KArgs A) {
 // the histogram is laid out [iteration][material][tile of that iteration]: its flat exclusive
 // scan IS the (iteration, material) sorted position, at nmats * (tiles + spp) entries, whatever spp.
 // Hits are stored at the PHYSICAL path index so k_sort_shade needs only perm.
+// Path j of the sorted pipeline: state and hit record as ONE 64-byte record, so k_sort_shade's
+// gather in sorted order reads one 64-byte span per path (the 16-byte planes of the fused layout
+// plus two hit planes put five cache lines behind every gathered path):
+//   r0 = (o.xyz, d.x)   r1 = (d.yz, c.rg)   r2 = (c.b, slot, t, material)   r3 = (n.xyz, 0)
+// `bounces` is not stored: every path entering bounce b has b bounces behind it.  Texture
+// coordinates (textured scenes only) go to HitSoA::uv.
+__device__ __forceinline__ v4f* srec(const PathSoA& B, int j) { return B.a + ((size_t)(uint32_t)j << 2); }
+
 struct SortArgs {
     int32_t* keys;     // [P] material key of logical path i
     int32_t* phys;     // [P] physical index of logical path i
@@ -1359,7 +1366,6 @@ __global__ __launch_bounds__(kBlock) void k_sort_isect(const KArgs A, const Sort
             PathReg p;
             if (FIRST) {
                 raygen(A.cam, A.fl, A.tile, i, p);
-                store_path(A.in, i, p);
             } else {
                 int lo = 0, hi = nseg_in - 1;   // segment of the tile's first path, then walk
                 const int f = s_ib[it] + 64 * t;
@@ -1369,24 +1375,40 @@ __global__ __launch_bounds__(kBlock) void k_sort_isect(const KArgs A, const Sort
                 }
                 const int sg = seg_walk(s_pre, nseg_in, lo, i);
                 j = sg * chunk_in + (i - s_pre[sg]);
-                const v4f pa = A.in.a[j], pb = A.in.b[j];
+                const v4f* r = srec(A.in, j);
+                const v4f pa = r[0], pb = r[1];
                 p.o = F3(pa[0], pa[1], pa[2]);
                 p.d = F3(pa[3], pb[0], pb[1]);
             }
             const Hit h = closest_hit<MESH, true>(A.S, A.fl, s_geoms, p.o, p.d, &A.stats->bound_mismatch);
-            A.hit.tn[j] = v4f{h.t, h.n.x, h.n.y, h.n.z};
             key = h.t == -1.0f ? 0 : h.mat;     // misses keep the memset materialId 0 (pathtrace.cu:466)
-            A.hit.uvm[j] = v4f{h.u, h.v, __int_as_float(key), 0.0f};
+            v4f* r = srec(A.in, j);
+            if (FIRST) {
+                r[0] = v4f{p.o.x, p.o.y, p.o.z, p.d.x};
+                r[1] = v4f{p.d.y, p.d.z, p.c.x, p.c.y};
+                r[2] = v4f{p.c.z, __int_as_float(p.slot), h.t, __int_as_float(key)};
+            } else {   // (c.b, slot) were written by the previous k_sort_shade
+                *reinterpret_cast<v2f*>(reinterpret_cast<float*>(r + 2) + 2) = v2f{h.t, __int_as_float(key)};
+            }
+            r[3] = v4f{h.n.x, h.n.y, h.n.z, 0.0f};
+            if (A.S.texs) {
+                A.hit.uv[2 * (size_t)j] = h.u;
+                A.hit.uv[2 * (size_t)j + 1] = h.v;
+            }
             SA.keys[i] = key;
             SA.phys[i] = j;
         }
-        const int tiles_it = s_tb[it + 1] - s_tb[it];
-        for (int k0 = 0; k0 < nmats; k0 += 64) {
-            const int k = k0 + lane;
-            uint32_t cnt = 0;
-            // count of lanes whose key == k (k differs per lane): loop over the wave's keys
-            for (int src = 0; src < 64; ++src) cnt += (__shfl(key, src, 64) == k) ? 1u : 0u;
-            if (k < nmats) SA.hist[(size_t)nmats * s_tb[it] + (size_t)k * tiles_it + t] = (int32_t)cnt;
+        // this tile's count of every material present: one ballot per distinct key in the wave
+        // (the histogram is all zero on entry; k_sort_scatter re-zeroes exactly these entries)
+        const size_t h0 = (size_t)nmats * s_tb[it] + t;
+        const size_t tiles_it = (size_t)(s_tb[it + 1] - s_tb[it]);
+        uint64_t rem = __ballot(key >= 0);
+        while (rem) {
+            const int src = __builtin_ctzll(rem);
+            const int kk = __builtin_amdgcn_readlane(key, src);
+            const uint64_t m = __ballot(key == kk);
+            if (lane == src) SA.hist[h0 + (size_t)kk * tiles_it] = (int32_t)__popcll(m);
+            rem &= ~m;
         }
     }
 }
@@ -1408,14 +1430,20 @@ __global__ __launch_bounds__(kBlock) void k_sort_scatter(const KArgs A, const So
         const int i = s_ib[it] + 64 * t + lane;
         const bool valid = i < s_ib[it + 1];
         const int key = valid ? SA.keys[i] : -1;
-        uint64_t same = 0;
-        for (int src = 0; src < 64; ++src) {
-            const int ks = __shfl(key, src, 64);
-            same |= (ks == key) ? (1ull << src) : 0ull;
-        }
         const size_t h0 = (size_t)nmats * s_tb[it] + t;
-        if (valid) SA.perm[SA.offs[h0 + (size_t)key * tiles_it] + __popcll(same & lt)] = SA.phys[i];
-        for (int k = lane; k < nmats; k += 64) SA.hist[h0 + (size_t)k * tiles_it] = 0;   // ready for the next bounce
+        // rank among the tile's lanes with the same key: one ballot per distinct key in the wave;
+        // the histogram entries k_sort_isect set are zeroed again for the next bounce
+        uint32_t rank = 0;
+        uint64_t rem = __ballot(valid);
+        while (rem) {
+            const int src = __builtin_ctzll(rem);
+            const int kk = __builtin_amdgcn_readlane(key, src);
+            const uint64_t m = __ballot(key == kk);
+            if (key == kk) rank = (uint32_t)__popcll(m & lt);
+            if (lane == src) SA.hist[h0 + (size_t)kk * tiles_it] = 0;
+            rem &= ~m;
+        }
+        if (valid) SA.perm[SA.offs[h0 + (size_t)key * tiles_it] + rank] = SA.phys[i];
     }
 }
 
@@ -1459,14 +1487,25 @@ __global__ __launch_bounds__(kBlock) void k_sort_shade(const KArgs A, const Sort
         PathReg p;
         if (idx < last) {
             const int j = SA.perm[idx];
-            load_path(A.in, j, p);
+            const v4f* r = srec(A.in, j);
+            const v4f r0 = r[0], r1 = r[1], r2 = r[2], r3 = r[3];
+            p.o = F3(r0[0], r0[1], r0[2]);
+            p.d = F3(r0[3], r1[0], r1[1]);
+            p.c = F3(r1[2], r1[3], r2[0]);
+            p.slot = __float_as_int(r2[1]);
+            p.bounces = A.bounce;
             Hit h;
-            const v4f tn = A.hit.tn[j], uvm = A.hit.uvm[j];
-            h.t = tn[0];
-            h.n = F3(tn[1], tn[2], tn[3]);
-            h.mat = __float_as_int(uvm[2]);
-            h.u = uvm[0];
-            h.v = uvm[1];
+            h.t = r2[2];
+            h.mat = __float_as_int(r2[3]);
+            h.n = F3(r3[0], r3[1], r3[2]);
+            h.u = h.v = 0.0f;
+            if (A.S.texs && h.t > 0.0f) {
+                const bool tex = lds_mats ? s_mats[h.mat].texture_id != -1 : A.S.mats[h.mat].texture_id != -1;
+                if (tex) {
+                    h.u = A.hit.uv[2 * (size_t)j];
+                    h.v = A.hit.uv[2 * (size_t)j + 1];
+                }
+            }
             // key: sorted index within the path's own iteration
             const int key = A.fl.rng_pixel ? slot_pixel(A.cam, A.tile, p.slot) : idx - it_base;
             alive = lds_mats ? shade(A.S, A.fl, A.tile.depth, iter, key, p, h, s_mats)
@@ -1483,7 +1522,13 @@ __global__ __launch_bounds__(kBlock) void k_sort_shade(const KArgs A, const Sort
         __syncthreads();
         const uint32_t w0 = s_wc[k & 1][0], w1 = s_wc[k & 1][1], w2 = s_wc[k & 1][2], w3 = s_wc[k & 1][3];
         const uint32_t before = (wave > 0 ? w0 : 0u) + (wave > 1 ? w1 : 0u) + (wave > 2 ? w2 : 0u);
-        if (alive) store_path(A.out, (int)blockIdx.x * chunk + (int)(kept + before + rank), p);
+        if (alive) {   // the whole 64-byte record (k_sort_isect fills in t, material and n)
+            v4f* r = srec(A.out, (int)blockIdx.x * chunk + (int)(kept + before + rank));
+            r[0] = v4f{p.o.x, p.o.y, p.o.z, p.d.x};
+            r[1] = v4f{p.d.y, p.d.z, p.c.x, p.c.y};
+            r[2] = v4f{p.c.z, __int_as_float(p.slot), 0.0f, 0.0f};
+            r[3] = v4f{0.0f, 0.0f, 0.0f, 0.0f};
+        }
         kept += (w0 + w1) + (w2 + w3);
     }
     if (tid == 0) A.seg[(size_t)(par ^ 1) * kMaxSeg + blockIdx.x] = (int32_t)(kept | ((uint32_t)my_it << kSegItShift));
@@ -1701,10 +1746,13 @@ void update_bounds(pt_ctx* c, float aperture) {
     c->args.S.abs_slack = (float)std::ldexp(R + 1.0, -17);
 }
 
+// One block of 4P planes per parity: the fused / split pipelines use the first three as the
+// a, b, c planes; the sorted pipeline uses the block as P 64-byte records (srec).
 int alloc_paths(pt_ctx* c, PathSoA& B, size_t P) {
-    if (int rc = c->alloc(&B.a, P)) return rc;
-    if (int rc = c->alloc(&B.b, P)) return rc;
-    return c->alloc(&B.c, P);
+    if (int rc = c->alloc(&B.a, 4 * P)) return rc;
+    B.b = B.a + P;
+    B.c = B.a + 2 * P;
+    return PT_OK;
 }
 
 int prof_begin(pt_ctx* c, hipStream_t st, int kind, ProfEv** out) {
@@ -2038,8 +2086,7 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
     // hit SoA + sort buffers (material-sorted mode)
     {
         // indexed by physical path index (< path_cap)
-        if (int rc = c->alloc(&A.hit.tn, c->path_cap)) return bail(rc);
-        if (int rc = c->alloc(&A.hit.uvm, c->path_cap)) return bail(rc);
+        if (int rc = c->alloc(&A.hit.uv, 2 * (size_t)c->path_cap)) return bail(rc);
         if (int rc = c->alloc(&c->phys, (size_t)P)) return bail(rc);
         c->max_t64 = (int)((P + 63) / 64);
         // [iteration][material][tile]: each iteration starts a fresh tile (+1: the end offset)
