@@ -322,7 +322,8 @@ def main() -> None:
     avg_ms = b_ms / max(b_n, 1)
     achieved = per_launch_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS, "traffic": _traffic_from_profiles("k_bounce"),
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": None if gui.sortbyMaterial else _traffic_from_profiles("k_bounce"),
                 "kernel": kernel_name, "avg_launch_ms": avg_ms, "launches": b_n,
                 "segments_per_launch": seg_bounce / max(b_n, 1),
                 "algorithmic_bytes_per_launch": per_launch_bytes,
