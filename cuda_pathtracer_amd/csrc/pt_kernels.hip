@@ -89,6 +89,7 @@ struct FlagsDev {
 };
 struct TileDev {
     int32_t W, rank, world, npix, spp, P, depth, iter_first;
+    uint64_t wdiv;   // ceil(2^40 / W) when npix * W < 2^40 (then lp / W == lp * wdiv >> 40), else 0
 };
 struct KArgs {
     SceneDev S;
@@ -797,10 +798,10 @@ __device__ __forceinline__ bool shade(const SceneDev& S, const FlagsDev& fl, int
 }
 
 // generateRayFromCamera (pathtrace.cu:183-227) for tile slot `slot`.
-__device__ __forceinline__ void raygen(const CamDev& cam, const FlagsDev& fl, const TileDev& T, int slot, PathReg& p) {
-    const int s = slot / T.npix;
-    const int lp = slot - s * T.npix;
-    const int row = lp / T.W;
+// Path `slot` = iteration s of the pass, tile-local pixel lp.
+__device__ __forceinline__ void raygen_at(const CamDev& cam, const FlagsDev& fl, const TileDev& T, int slot, int s, int lp,
+                                          PathReg& p) {
+    const int row = T.wdiv ? (int)(((uint64_t)(uint32_t)lp * T.wdiv) >> 40) : lp / T.W;
     const int x = lp - row * T.W;
     const int y = row * T.world + T.rank;
     const int index = x + y * cam.res[0];
@@ -830,6 +831,10 @@ __device__ __forceinline__ void raygen(const CamDev& cam, const FlagsDev& fl, co
     }
     p.slot = slot;
     p.bounces = 0;
+}
+__device__ __forceinline__ void raygen(const CamDev& cam, const FlagsDev& fl, const TileDev& T, int slot, PathReg& p) {
+    const int s = slot / T.npix;
+    raygen_at(cam, fl, T, slot, s, slot - s * T.npix, p);
 }
 
 __device__ __forceinline__ void load_path(const PathSoA& B, int i, PathReg& p) {
@@ -1131,7 +1136,7 @@ __global__ __launch_bounds__(kBlock) void k_bounce(const KArgs A) {
         STAMP(t0);
         if (i < last) {
             if (FIRST) {
-                raygen(A.cam, A.fl, A.tile, i, p);
+                raygen_at(A.cam, A.fl, A.tile, i, my_it, i - it_base, p);   // (a workgroup holds one iteration)
             } else {
                 const int s = seg_walk(s_pre, nseg_in, seg, i);
                 load_path(A.in, s * chunk_in + (i - s_pre[s]), p);
@@ -2027,7 +2032,8 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
     A.cam.pl[1] = cam.pixel_length[1];
     A.cam.res[0] = W;
     A.cam.res[1] = H;
-    A.tile = TileDev{W, sh.rank, sh.world, (int)npix, sh.spp, (int)P, S.depth, 1};
+    A.tile = TileDev{W, sh.rank, sh.world, (int)npix, sh.spp, (int)P, S.depth, 1, 0};
+    if ((double)npix * (double)W < 0x1p40) A.tile.wdiv = ((1ull << 40) + (uint64_t)W - 1) / (uint64_t)W;
 
     A.emit_stride = 256 * 8;   // >= any grid_trace (cus * 8) / grid_bounce
     // k_trace has no inter-workgroup dependency: 8 workgroups per CU, grid-stride beyond that.
