@@ -86,7 +86,8 @@ struct DGeom {
     float r2w, tslack;
     float kcs, kc3;
     float wlo[3], whi[3], back;
-    int32_t bkind;   // 0: never hit (mesh), 1: oriented cube, 2: sphere, 3: world-box cube
+    int32_t bkind;   // 0: never hit (mesh), 1: oriented cube, 2: sphere, 3: world-box cube,
+                     // 4: uniformly scaled sphere (world-space dot products)
 };
 
 struct DMaterial {   // == pt_material

@@ -478,6 +478,11 @@ __device__ __forceinline__ Hit intersect_scene(const SceneDev& S, const FlagsDev
 // non-first bounce kernel, each phase closed by s_waitcnt 0 (so the split perturbs the schedule).
 #ifdef PT_STAMPS
 __device__ unsigned long long g_stamps[16];   // [0..5] phases, [8..] closest-hit counters
+#ifdef PT_STAMPS_FIRST
+constexpr bool kStampFirst = true;    // phase stamps of the first bounce (raygen in "load")
+#else
+constexpr bool kStampFirst = false;   // phase stamps of bounces >= 1
+#endif
 #define STAMP(v) do { __builtin_amdgcn_s_waitcnt(0); v = __builtin_amdgcn_s_memtime(); } while (0)
 #else
 #define STAMP(v) do { } while (0)
@@ -526,10 +531,25 @@ __device__ __forceinline__ float bound_geom(const G& g, f3 ro, f3 rd, f3 invd, f
         return fmaxf(fmaxf(E, 0.0f) * rl - g.back, 0.0f) * g.tslack;
     }
     if (kind == 0) return kInf;
-    const f3 qo = xform_point(g.inv, ro);
-    const f3 qv = xform_vector(g.inv, rd);   // un-normalized: world parameter = object parameter
-    const float a = dot(qv, qv);
-    float lo;
+    float a, b, q2, lo;
+    f3 qo, qv;
+    if (kind == 4) {
+        // sphere whose transform is a uniform scale (any rotation): the object-space dot products
+        // are rotation invariant, so they come from world space: w = ro - centre, scaled by
+        // is2 = |inv v|^2 / |v|^2 (wlo = centre, whi[0] = is2; wider margins, update_bounds)
+        const f3 w = F3(ro.x - g.wlo[0], ro.y - g.wlo[1], ro.z - g.wlo[2]);
+        a = dot(rd, rd) * g.whi[0];
+        b = dot(w, rd) * g.whi[0];
+        q2 = dot(w, w) * g.whi[0];
+    } else {
+        qo = xform_point(g.inv, ro);
+        qv = xform_vector(g.inv, rd);   // un-normalized: world parameter = object parameter
+        a = dot(qv, qv);
+        if (kind == 2) {
+            b = dot(qo, qv);
+            q2 = dot(qo, qo);
+        }
+    }
     if (kind == 1) {
         float E = -kInf, X = kInf;
 #pragma unroll
@@ -542,8 +562,6 @@ __device__ __forceinline__ float bound_geom(const G& g, f3 ro, f3 rd, f3 invd, f
         if (E > X || X < 0.0f) return kInf;
         lo = fmaxf(E, 0.0f);
     } else {
-        const float b = dot(qo, qv);
-        const float q2 = dot(qo, qo);
         if (b > 0.0f && q2 - 0.25f > (q2 + 1.0f) * (g.kcs * rinf + g.kc3)) return kInf;   // departing
         const float disc = b * b - a * (q2 - g.r2w);
         if (disc < 0.0f) return kInf;
@@ -1176,7 +1194,7 @@ __global__ __launch_bounds__(kBlock) void k_bounce(const KArgs A) {
 #endif
     }
 #ifdef PT_STAMPS
-    if (!FIRST && lane == 0)
+    if (FIRST == kStampFirst && lane == 0)
         for (int q = 0; q < 6; ++q) atomicAdd(&g_stamps[q], st_acc[q]);
 #endif
     if (tid == 0) A.seg[(size_t)(par ^ 1) * kMaxSeg + blockIdx.x] = (int32_t)(kept | ((uint32_t)my_it << kSegItShift));
@@ -1694,6 +1712,30 @@ void update_bounds(pt_ctx* c, float aperture) {
         d.kcs = (float)std::ldexp(cs, -18);
         d.kc3 = (float)std::ldexp(c3 + 2.0, -18);
         d.bkind = d.type == PT_GEOM_CUBE ? 1 : (d.type == PT_GEOM_SPHERE ? 2 : 0);
+        if (d.type == PT_GEOM_SPHERE) {
+            // uniform scale (x rotation): G = L^T L = sigma^2 I up to delta, L = the linear part of inv
+            double G[3][3], tr = 0.0, dev = 0.0;
+            for (int i = 0; i < 3; ++i)
+                for (int j = 0; j < 3; ++j) {
+                    G[i][j] = 0.0;
+                    for (int a = 0; a < 3; ++a) G[i][j] += (double)d.inv.c[i][a] * (double)d.inv.c[j][a];
+                }
+            for (int i = 0; i < 3; ++i) tr += G[i][i];
+            const double s2 = tr / 3.0;
+            for (int i = 0; i < 3; ++i)
+                for (int j = 0; j < 3; ++j) dev = std::max(dev, std::fabs(G[i][j] - (i == j ? s2 : 0.0)));
+            if (s2 > 0.0 && dev <= std::ldexp(s2, -20)) {
+                // the world-space dot products differ from the object-space ones by the
+                // non-uniformity (<= 2^-20 relative) and the rounding of w = ro - centre (within the
+                // 4 ulp of S_a assumed above): margins doubled
+                for (int k = 0; k < 3; ++k) d.wlo[k] = d.xf.c[3][k];
+                d.whi[0] = (float)s2;
+                d.r2w = (float)(0.25 + std::ldexp((smax + 1.0) * (smax + 1.0), -15));
+                d.kcs *= 2.0f;
+                d.kc3 *= 2.0f;
+                d.bkind = 4;
+            }
+        }
         if (d.type == PT_GEOM_CUBE) {   // world box of the widened cube, if the transform is axis-aligned
             double M[3][3], X[3][3];
             for (int r = 0; r < 3; ++r)
