@@ -1626,9 +1626,23 @@ struct pt_ctx {
     std::vector<DGeom> hgeoms;    // host copy of the geom table (bounds re-derived by pt_set_flags)
     DGeom* d_geoms = nullptr;
     double scene_ext = 0.0;       // max |coordinate| over every surface and the camera position
+    // Batched passes (spp > 1): pass p's path colours go to colbuf half h = p & 1 and are added
+    // into the image by k_finalize_spp on fin_stream, concurrently with the next pass's bounces
+    // on the caller's stream (memory-bound finalize beside the VALU-bound first bounce).  A pass
+    // waits for the finalize still reading its half; image readers wait for the last one.
+    v4f* colbuf = nullptr;        // 2 x P
+    hipStream_t fin_stream = nullptr;
+    hipEvent_t ev_pass[2] = {}, ev_fin[2] = {};
+    bool fin_out[2] = {false, false};
+    int col_half = 0, last_fin = -1;
 
     ~pt_ctx() {
         for (auto& e : events) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
+        for (int h = 0; h < 2; ++h) {
+            if (ev_pass[h]) (void)hipEventDestroy(ev_pass[h]);
+            if (ev_fin[h]) (void)hipEventDestroy(ev_fin[h]);
+        }
+        if (fin_stream) (void)hipStreamDestroy(fin_stream);
         for (void* p : allocs) (void)hipFree(p);
     }
     template <typename T>
@@ -2112,7 +2126,14 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
         if (int rc = alloc_paths(c, c->buf[b], c->path_cap)) return bail(rc);
     if (int rc = c->alloc(&A.image, (size_t)npix * 3)) return bail(rc);
     if (sh.spp > 1)
-        if (int rc = c->alloc(&A.colbuf, (size_t)P)) return bail(rc);
+        if (int rc = c->alloc(&c->colbuf, 2 * (size_t)P)) return bail(rc);
+        A.colbuf = c->colbuf;
+        if ((e = hipStreamCreateWithFlags(&c->fin_stream, hipStreamNonBlocking)) != hipSuccess)
+            return bail(pt::fail(PT_ERR_HIP, std::string("hipStreamCreate: ") + hipGetErrorString(e)));
+        for (int h = 0; h < 2; ++h)
+            if ((e = hipEventCreateWithFlags(&c->ev_pass[h], hipEventDisableTiming)) != hipSuccess ||
+                (e = hipEventCreateWithFlags(&c->ev_fin[h], hipEventDisableTiming)) != hipSuccess)
+                return bail(pt::fail(PT_ERR_HIP, std::string("hipEventCreate: ") + hipGetErrorString(e)));
     c->max_tiles = (int)((P + kCompactTile - 1) / kCompactTile);   // k_compact_paths tiles
     if (int rc = c->alloc(&A.flags, (size_t)P)) return bail(rc);
     if (int rc = c->alloc(&A.ctl, 2)) return bail(rc);
@@ -2186,6 +2207,11 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
     const bool sorted = c->flags.sort_by_material != 0;
     const bool mesh = A.S.ntris > 0;
     int cur = 0;   // paths start in buf[0]
+    const int h = c->col_half;
+    if (!spp1) {
+        A.colbuf = c->colbuf + (size_t)h * (size_t)A.tile.P;
+        if (c->fin_out[h]) HIP_TRY(hipStreamWaitEvent(st, c->ev_fin[h], 0));   // pass p-2's finalize
+    }
     for (int b = 0; b < c->depth; ++b) {
         const bool last = b == c->depth - 1;   // every path is dead after the last bounce
         A.parity = (int)(c->compact_launches & 1);
@@ -2236,16 +2262,29 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
 
     if (!spp1) {
         const int npix = A.tile.npix;
-        hipLaunchKernelGGL(k_finalize_spp, dim3(std::min((npix + 255) / 256, 4096)), dim3(256), 0, st, A.image,
-                           (const v4f*)A.colbuf, npix, A.tile.spp);
+        HIP_TRY(hipEventRecord(c->ev_pass[h], st));
+        HIP_TRY(hipStreamWaitEvent(c->fin_stream, c->ev_pass[h], 0));
+        hipLaunchKernelGGL(k_finalize_spp, dim3(std::min((npix + 255) / 256, 4096)), dim3(256), 0, c->fin_stream,
+                           A.image, (const v4f*)A.colbuf, npix, A.tile.spp);
         HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(c->ev_fin[h], c->fin_stream));
+        c->fin_out[h] = true;
+        c->last_fin = h;
+        c->col_half = h ^ 1;
     }
+    return PT_OK;
+}
+
+// Work on `st` that reads or writes the image first waits for the last deferred finalize.
+static int wait_finalize(pt_ctx* c, hipStream_t st) {
+    if (c->last_fin >= 0) HIP_TRY(hipStreamWaitEvent(st, c->ev_fin[c->last_fin], 0));
     return PT_OK;
 }
 
 int pt_preview_rgba(pt_ctx* c, int32_t iter, uint8_t* d_rgba, void* stream) {
     if (!c || !d_rgba || iter <= 0) return pt::fail(PT_ERR_ARG, "bad argument");
     const int npix = c->args.tile.npix;
+    if (int rc = wait_finalize(c, (hipStream_t)stream)) return rc;
     hipLaunchKernelGGL(k_preview, dim3(std::min((npix + 255) / 256, 4096)), dim3(256), 0, (hipStream_t)stream,
                        (const float*)c->args.image, d_rgba, npix, iter);
     HIP_TRY(hipGetLastError());
@@ -2287,6 +2326,7 @@ int pt_set_accum(pt_ctx* c, const float* host_rgb) {
 
 int pt_copy_image(pt_ctx* c, float* d_rgb, void* stream) {
     if (!c || !d_rgb) return pt::fail(PT_ERR_ARG, "null argument");
+    if (int rc = wait_finalize(c, (hipStream_t)stream)) return rc;
     HIP_TRY(hipMemcpyAsync(d_rgb, c->args.image, (size_t)c->args.tile.npix * 3 * sizeof(float),
                            hipMemcpyDeviceToDevice, (hipStream_t)stream));
     return PT_OK;
@@ -2294,6 +2334,7 @@ int pt_copy_image(pt_ctx* c, float* d_rgb, void* stream) {
 
 int pt_reset_image(pt_ctx* c, void* stream) {
     if (!c) return pt::fail(PT_ERR_ARG, "null context");
+    if (int rc = wait_finalize(c, (hipStream_t)stream)) return rc;
     HIP_TRY(hipMemsetAsync(c->args.image, 0, (size_t)c->args.tile.npix * 3 * sizeof(float), (hipStream_t)stream));
     return PT_OK;
 }
