@@ -479,3 +479,33 @@ def test_max_batch_256_iterations(cornell_path, kw):
     g, r, st, live = _run(s, o, _gui(**kw), iters=256, spp=256)
     _assert_bitexact(g, r, f"spp=256 {kw}")
     assert st["bounce_live"] == live
+
+
+def test_deferred_finalize_is_ordered_with_image_calls(cornell_path):
+    """Batched passes add their colours into the image on a side stream (pt_render_pass): the
+    asynchronous image entry points on the caller's stream must see every finished pass, a reset
+    must drop what came before it, and three passes in a row (both colour halves reused) must equal
+    the same passes rendered with a read after each."""
+    import torch
+    from cuda_pathtracer_amd import PathTracer
+    s, _ = _pair(cornell_path, (40, 32))
+    st = torch.cuda.current_stream()
+    a = PathTracer(s, _gui(), spp=3)
+    for it in (1, 4, 7):
+        a.render_pass(it, st)
+    dev = torch.empty((a.rows, a.width, 3), dtype=torch.float32, device="cuda")
+    a.copy_image_to(dev.data_ptr(), st)     # async on the caller's stream, no host sync before it
+    torch.cuda.synchronize()
+    b = PathTracer(s, _gui(), spp=3)
+    for it in (1, 4, 7):
+        b.render_pass(it, st)
+        b.image()                           # synchronous read after every pass
+    _assert_bitexact(dev.cpu().numpy(), b.image(), "async copy vs synchronous reads")
+    # reset, then one more pass: only that pass's colours remain
+    a.reset_image(st)
+    a.render_pass(10, st)
+    c = PathTracer(s, _gui(), spp=3)
+    c.render_pass(10, st)
+    _assert_bitexact(a.image(), c.image(), "reset then pass vs a fresh context")
+    for p in (a, b, c):
+        p.free()
