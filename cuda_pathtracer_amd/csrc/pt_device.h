@@ -88,6 +88,7 @@ struct DGeom {
     float wlo[3], whi[3], back;
     int32_t bkind;   // 0: never hit (mesh), 1: oriented cube, 2: sphere, 3: world-box cube,
                      // 4: uniformly scaled sphere (world-space dot products)
+    int32_t orig;    // SceneDev::bgeoms rows: index of this geom in SceneDev::geoms
 };
 
 struct DMaterial {   // == pt_material

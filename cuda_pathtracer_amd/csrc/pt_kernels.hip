@@ -62,6 +62,8 @@ struct DevStats {
 
 struct SceneDev {
     const DGeom* __restrict__ geoms;
+    const DGeom* __restrict__ bgeoms;   // the geoms ordered by bkind (DGeom::orig = index in geoms)
+    int32_t bk[6];                      // bgeoms[bk[k] .. bk[k+1]) have bkind k
     const DMaterial* __restrict__ mats;
     const DTri* __restrict__ tris;
     const DTriAttr* __restrict__ attrs;
@@ -516,9 +518,9 @@ __device__ __forceinline__ void stage_geoms(const SceneDev& S, LGeom* s_geoms) {
 // Lower bound on the exact test's world distance for geom g (before the scene's absolute slack),
 // +inf when the exact test surely misses.  Rounding here is irrelevant: only the widened bounds,
 // the relative slack and the comparisons' direction matter (NaNs fall through to "candidate").
-template <class G>
+template <int KIND, class G>
 __device__ __forceinline__ float bound_geom(const G& g, f3 ro, f3 rd, f3 invd, float rl, float rinf) {
-    const int kind = g.bkind;
+    constexpr int kind = KIND;
     if (kind == 3) {   // world box: t = (plane - o) / d (subtract first: exact zeros in d stay safe)
         float E = -kInf, X = kInf;
 #pragma unroll
@@ -635,9 +637,12 @@ __device__ __forceinline__ Hit intersect_bounded(const SceneDev& S, const FlagsD
         uint32_t cand = 0u;   // every geom with a finite bound
         const float rinf = fmaxf(fmaxf(fabsf(ro.x), fabsf(ro.y)), fabsf(ro.z));
         const f3 invd = F3(__builtin_amdgcn_rcpf(rd.x), __builtin_amdgcn_rcpf(rd.y), __builtin_amdgcn_rcpf(rd.z));
-        const auto* G = as_const(S.geoms);
-        for (int i = 0; i < S.ngeoms; ++i) {
-            const float lo = bound_geom(G[i], ro, rd, invd, rl, rinf) - S.abs_slack;
+        // one branch-free loop per bound kind (geoms sorted by kind on the host), so the scalar
+        // loads of the next geom need not wait for this one's kind; the candidates' identity and
+        // order do not matter to the result (pass 2 below), only the set of bounds
+        const auto* B = as_const(S.bgeoms);
+        auto insert = [&](float lo, int i) {
+            lo -= S.abs_slack;
             cand |= lo < kInf ? (1u << i) : 0u;
             const bool c1 = lo < lo1, c2 = lo < lo2, c3 = lo < lo3;
             lo3 = c2 ? lo2 : (c3 ? lo : lo3);
@@ -645,7 +650,11 @@ __device__ __forceinline__ Hit intersect_bounded(const SceneDev& S, const FlagsD
             g2 = c1 ? g1 : (c2 ? i : g2);
             lo1 = c1 ? lo : lo1;
             g1 = c1 ? i : g1;
-        }
+        };
+        for (int j = S.bk[3]; j < S.bk[4]; ++j) insert(bound_geom<3>(B[j], ro, rd, invd, rl, rinf), B[j].orig);
+        for (int j = S.bk[4]; j < S.bk[5]; ++j) insert(bound_geom<4>(B[j], ro, rd, invd, rl, rinf), B[j].orig);
+        for (int j = S.bk[1]; j < S.bk[2]; ++j) insert(bound_geom<1>(B[j], ro, rd, invd, rl, rinf), B[j].orig);
+        for (int j = S.bk[2]; j < S.bk[3]; ++j) insert(bound_geom<2>(B[j], ro, rd, invd, rl, rinf), B[j].orig);
         // pass 2: exact tests in increasing-bound order while a bound does not exceed the best hit
         auto take = [&](int gi) {
             int code;
@@ -1625,6 +1634,7 @@ struct pt_ctx {
     size_t path_cap = 0;          // entries per path buffer (>= P, see pt_create)
     std::vector<DGeom> hgeoms;    // host copy of the geom table (bounds re-derived by pt_set_flags)
     DGeom* d_geoms = nullptr;
+    DGeom* d_bgeoms = nullptr;    // the same geoms ordered by bound kind (SceneDev::bgeoms)
     double scene_ext = 0.0;       // max |coordinate| over every surface and the camera position
     // Batched passes (spp > 1): pass p's path colours go to colbuf half h = p & 1 and are added
     // into the image by k_finalize_spp on fin_stream, concurrently with the next pass's bounces
@@ -1887,6 +1897,26 @@ int launch_k(pt_ctx* c, K kernel, int grid, hipStream_t st, int kind, const KArg
     return prof_end(ev, st);
 }
 
+// SceneDev::bgeoms: the geom table stably ordered by bkind, each row keeping its index in `orig`.
+int upload_bound_order(pt_ctx* c) {
+    std::vector<DGeom> b;
+    int32_t bk[6] = {0, 0, 0, 0, 0, 0};
+    for (int k = 0; k < 5; ++k) {
+        bk[k] = (int32_t)b.size();
+        for (size_t i = 0; i < c->hgeoms.size(); ++i)
+            if (c->hgeoms[i].bkind == k) {
+                b.push_back(c->hgeoms[i]);
+                b.back().orig = (int32_t)i;
+            }
+    }
+    bk[5] = (int32_t)b.size();
+    if (b.size() != c->hgeoms.size()) return pt::fail(PT_ERR_ARG, "geom with an unknown bound kind");
+    HIP_TRY(hipMemcpy(c->d_bgeoms, b.data(), b.size() * sizeof(DGeom), hipMemcpyHostToDevice));
+    c->args.S.bgeoms = c->d_bgeoms;
+    for (int k = 0; k < 6; ++k) c->args.S.bk[k] = bk[k];
+    return PT_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1960,6 +1990,7 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
     DMaterial* d_mats;
     if (int rc = c->alloc(&d_geoms, dg.size())) return bail(rc);
     c->d_geoms = d_geoms;
+    if (int rc = c->alloc(&c->d_bgeoms, dg.size())) return bail(rc);
     if (int rc = c->alloc(&d_mats, S.materials.size())) return bail(rc);
     if ((e = hipMemcpy(d_geoms, dg.data(), dg.size() * sizeof(DGeom), hipMemcpyHostToDevice)) != hipSuccess ||
         (e = hipMemcpy(d_mats, S.materials.data(), S.materials.size() * sizeof(DMaterial), hipMemcpyHostToDevice)) != hipSuccess)
@@ -1967,6 +1998,7 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
     static_assert(sizeof(DMaterial) == sizeof(pt_material), "material layout");
     static_assert(sizeof(DNode) == 32 && sizeof(DTri) == 48, "packed device layouts");
     A.S.geoms = d_geoms;
+    if (int rc = upload_bound_order(c)) return bail(rc);
     A.S.mats = d_mats;
     A.S.ngeoms = (int)dg.size();
     A.S.nmats = (int)S.materials.size();
@@ -2193,6 +2225,7 @@ int pt_set_flags(pt_ctx* c, const pt_flags* f) {
         update_bounds(c, f->aperture);
         HIP_TRY(hipDeviceSynchronize());
         HIP_TRY(hipMemcpy(c->d_geoms, c->hgeoms.data(), c->hgeoms.size() * sizeof(DGeom), hipMemcpyHostToDevice));
+        if (int rc = upload_bound_order(c)) return rc;
     }
     return PT_OK;
 }
