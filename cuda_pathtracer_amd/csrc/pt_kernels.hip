@@ -518,7 +518,9 @@ __device__ __forceinline__ void stage_geoms(const SceneDev& S, LGeom* s_geoms) {
 // Lower bound on the exact test's world distance for geom g (before the scene's absolute slack),
 // +inf when the exact test surely misses.  Rounding here is irrelevant: only the widened bounds,
 // the relative slack and the comparisons' direction matter (NaNs fall through to "candidate").
-template <int KIND, class G>
+// SEL: selects instead of early returns (same value): no branch between one geom's scalar loads and
+// the next's — faster for the divergent rays of later bounces, slower for camera rays.
+template <int KIND, bool SEL, class G>
 __device__ __forceinline__ float bound_geom(const G& g, f3 ro, f3 rd, f3 invd, float rl, float rinf) {
     constexpr int kind = KIND;
     if (kind == 3) {   // world box: t = (plane - o) / d (subtract first: exact zeros in d stay safe)
@@ -529,11 +531,13 @@ __device__ __forceinline__ float bound_geom(const G& g, f3 ro, f3 rd, f3 invd, f
             E = fmaxf(E, fminf(t1, t2));
             X = fminf(X, fmaxf(t1, t2));
         }
-        if (E > X || X < 0.0f) return kInf;
-        return fmaxf(fmaxf(E, 0.0f) * rl - g.back, 0.0f) * g.tslack;
+        if (!SEL && (E > X || X < 0.0f)) return kInf;
+        const float v = fmaxf(fmaxf(E, 0.0f) * rl - g.back, 0.0f) * g.tslack;
+        return (E > X || X < 0.0f) ? kInf : v;
     }
     if (kind == 0) return kInf;
     float a, b, q2, lo;
+    bool miss;
     f3 qo, qv;
     if (kind == 4) {
         // sphere whose transform is a uniform scale (any rotation): the object-space dot products
@@ -561,20 +565,24 @@ __device__ __forceinline__ float bound_geom(const G& g, f3 ro, f3 rd, f3 invd, f
             E = fmaxf(E, fminf(t1, t2));
             X = fminf(X, fmaxf(t1, t2));
         }
-        if (E > X || X < 0.0f) return kInf;
+        miss = E > X || X < 0.0f;
+        if (!SEL && miss) return kInf;
         lo = fmaxf(E, 0.0f);
     } else {
-        if (b > 0.0f && q2 - 0.25f > (q2 + 1.0f) * (g.kcs * rinf + g.kc3)) return kInf;   // departing
+        const bool departing = b > 0.0f && q2 - 0.25f > (q2 + 1.0f) * (g.kcs * rinf + g.kc3);
+        if (!SEL && departing) return kInf;
         const float disc = b * b - a * (q2 - g.r2w);
-        if (disc < 0.0f) return kInf;
+        if (!SEL && disc < 0.0f) return kInf;
         const float sq = __builtin_amdgcn_sqrtf(disc), ia = __builtin_amdgcn_rcpf(a);
         const float eps = (fabsf(b) + sq) * ia * 0x1p-16f;
-        if ((sq - b) * ia < -eps) return kInf;
+        miss = departing || disc < 0.0f || (sq - b) * ia < -eps;
+        if (!SEL && miss) return kInf;
         lo = fmaxf((-b - sq) * ia - eps, 0.0f);
     }
     // pointOnRay pulls the hit back by 1e-4 along the NORMALIZED object direction: 1e-4/|qv| here
     const float back = 1.0002e-4f * __builtin_amdgcn_rsqf(a);
-    return fmaxf(lo - back, 0.0f) * rl * g.tslack;
+    const float v = fmaxf(lo - back, 0.0f) * rl * g.tslack;
+    return miss ? kInf : v;
 }
 
 // Exact test of one geom from its LDS row: boxIntersectionTest (intersections.cu:3-58) and
@@ -622,6 +630,7 @@ __device__ __forceinline__ float exact_geom(const LGeom& L, f3 r_o, f3 r_d, int&
     return length(r_o - ip);
 }
 
+template <bool SEL>
 __device__ __forceinline__ Hit intersect_bounded(const SceneDev& S, const FlagsDev& fl, const LGeom* s_geoms, f3 ro,
                                                  f3 rd) {
     const float rl = __builtin_amdgcn_sqrtf(dot(rd, rd));
@@ -651,10 +660,10 @@ __device__ __forceinline__ Hit intersect_bounded(const SceneDev& S, const FlagsD
             lo1 = c1 ? lo : lo1;
             g1 = c1 ? i : g1;
         };
-        for (int j = S.bk[3]; j < S.bk[4]; ++j) insert(bound_geom<3>(B[j], ro, rd, invd, rl, rinf), B[j].orig);
-        for (int j = S.bk[4]; j < S.bk[5]; ++j) insert(bound_geom<4>(B[j], ro, rd, invd, rl, rinf), B[j].orig);
-        for (int j = S.bk[1]; j < S.bk[2]; ++j) insert(bound_geom<1>(B[j], ro, rd, invd, rl, rinf), B[j].orig);
-        for (int j = S.bk[2]; j < S.bk[3]; ++j) insert(bound_geom<2>(B[j], ro, rd, invd, rl, rinf), B[j].orig);
+        for (int j = S.bk[3]; j < S.bk[4]; ++j) insert(bound_geom<3, SEL>(B[j], ro, rd, invd, rl, rinf), B[j].orig);
+        for (int j = S.bk[4]; j < S.bk[5]; ++j) insert(bound_geom<4, SEL>(B[j], ro, rd, invd, rl, rinf), B[j].orig);
+        for (int j = S.bk[1]; j < S.bk[2]; ++j) insert(bound_geom<1, SEL>(B[j], ro, rd, invd, rl, rinf), B[j].orig);
+        for (int j = S.bk[2]; j < S.bk[3]; ++j) insert(bound_geom<2, SEL>(B[j], ro, rd, invd, rl, rinf), B[j].orig);
         // pass 2: exact tests in increasing-bound order while a bound does not exceed the best hit
         auto take = [&](int gi) {
             int code;
@@ -710,11 +719,11 @@ __device__ __forceinline__ Hit intersect_bounded(const SceneDev& S, const FlagsD
 // The closest hit of the kernels: bounded for analytic scenes that fit the LDS geom table.
 // CHECK: compiled-in diagnostic re-run (k_trace and the sorted pipeline only, so the fused
 // kernel's code stays small): verify with PT_PIPELINE=split, whose rays are the fused kernel's.
-template <bool MESH, bool CHECK>
+template <bool MESH, bool CHECK, bool SEL = false>
 __device__ __forceinline__ Hit closest_hit(const SceneDev& S, const FlagsDev& fl, const LGeom* s_geoms, f3 ro, f3 rd,
                                            uint32_t* mismatch) {
     if (MESH || S.ngeoms > kLdsGeoms) return intersect_scene<MESH>(S, fl, ro, rd);
-    const Hit h = intersect_bounded(S, fl, s_geoms, ro, rd);
+    const Hit h = intersect_bounded<SEL>(S, fl, s_geoms, ro, rd);
     if (CHECK && fl.verify) {
         const Hit r = intersect_scene<false>(S, fl, ro, rd);
         if (__float_as_uint(h.t) != __float_as_uint(r.t) || h.mat != r.mat ||
@@ -1169,7 +1178,7 @@ __global__ __launch_bounds__(kBlock) void k_bounce(const KArgs A) {
                 load_path(A.in, s * chunk_in + (i - s_pre[s]), p);
             }
             STAMP(t1);
-            const Hit h = closest_hit<MESH, false>(A.S, A.fl, s_geoms, p.o, p.d, &A.stats->bound_mismatch);
+            const Hit h = closest_hit<MESH, false, !FIRST>(A.S, A.fl, s_geoms, p.o, p.d, &A.stats->bound_mismatch);
             STAMP(t2);
             const int key = A.fl.rng_pixel ? slot_pixel(A.cam, A.tile, p.slot) : i - it_base;
             // every path entering bounce b has b bounces behind it: a wave-uniform value, so the
