@@ -2166,7 +2166,7 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
     for (int b = 0; b < 2; ++b)
         if (int rc = alloc_paths(c, c->buf[b], c->path_cap)) return bail(rc);
     if (int rc = c->alloc(&A.image, (size_t)npix * 3)) return bail(rc);
-    if (sh.spp > 1)
+    if (sh.spp > 1) {
         if (int rc = c->alloc(&c->colbuf, 2 * (size_t)P)) return bail(rc);
         A.colbuf = c->colbuf;
         if ((e = hipStreamCreateWithFlags(&c->fin_stream, hipStreamNonBlocking)) != hipSuccess)
@@ -2175,6 +2175,7 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
             if ((e = hipEventCreateWithFlags(&c->ev_pass[h], hipEventDisableTiming)) != hipSuccess ||
                 (e = hipEventCreateWithFlags(&c->ev_fin[h], hipEventDisableTiming)) != hipSuccess)
                 return bail(pt::fail(PT_ERR_HIP, std::string("hipEventCreate: ") + hipGetErrorString(e)));
+    }
     c->max_tiles = (int)((P + kCompactTile - 1) / kCompactTile);   // k_compact_paths tiles
     if (int rc = c->alloc(&A.flags, (size_t)P)) return bail(rc);
     if (int rc = c->alloc(&A.ctl, 2)) return bail(rc);
