@@ -970,7 +970,7 @@ __global__ __launch_bounds__(kBlock) void k_trace(const KArgs A) {
             PathReg p;
             if (FIRST) raygen(A.cam, A.fl, A.tile, i, p);
             else load_path(A.in, i, p);
-            const Hit h = closest_hit<MESH, true>(A.S, A.fl, s_geoms, p.o, p.d, &A.stats->bound_mismatch);
+            const Hit h = closest_hit<MESH, true, !FIRST>(A.S, A.fl, s_geoms, p.o, p.d, &A.stats->bound_mismatch);
             const int it = SPP1 ? 0 : p.slot / A.tile.npix;
             const int iter = A.tile.iter_first + it;
             // key: index within the path's own iteration (k_iter_bases; see k_bounce)
@@ -1421,7 +1421,7 @@ __global__ __launch_bounds__(kBlock) void k_sort_isect(const KArgs A, const Sort
                 p.o = F3(pa[0], pa[1], pa[2]);
                 p.d = F3(pa[3], pb[0], pb[1]);
             }
-            const Hit h = closest_hit<MESH, true>(A.S, A.fl, s_geoms, p.o, p.d, &A.stats->bound_mismatch);
+            const Hit h = closest_hit<MESH, true, !FIRST>(A.S, A.fl, s_geoms, p.o, p.d, &A.stats->bound_mismatch);
             key = h.t == -1.0f ? 0 : h.mat;     // misses keep the memset materialId 0 (pathtrace.cu:466)
             v4f* r = srec(A.in, j);
             if (FIRST) {
