@@ -131,6 +131,7 @@ SIGNATURES = {
     "pt_stats": (_I, [_P, C.POINTER(Stats)]),
     "pt_profile_enable": (_I, [_P, _I]),
     "pt_profile_read": (_I, [_P, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
+    "pt_profile_read_busy": (_I, [_P, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
     "pt_tonemap": (_I, [_P, _I, _I, _F, _P]),
     "pt_save_png": (_I, [C.c_char_p, _P, _I, _I, _F]),
     "pt_save_hdr": (_I, [C.c_char_p, _P, _I, _I, _F]),

@@ -114,6 +114,7 @@ struct KArgs {
     DevStats* stats;
     unsigned long long* emit_slots;   // [64 bounces][emit_stride]: per-workgroup emissive counts
     int32_t emit_stride;
+    int32_t count_pass;    // this launch sequence counts the pass in DevStats::passes (lane 0)
 };
 
 // ------------------------------------------------------------------------------------------
@@ -937,7 +938,7 @@ __device__ __forceinline__ void count_bounce(const KArgs& A, int N) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         atomicAdd(&A.stats->bounce_live[A.bounce], (unsigned long long)N);
         atomicAdd(&A.stats->segments, (unsigned long long)N);
-        if (A.bounce == 0) atomicAdd(&A.stats->passes, 1ull);   // (no separate ~4 us launch per pass)
+        if (A.bounce == 0 && A.count_pass) atomicAdd(&A.stats->passes, 1ull);   // (no separate ~4 us launch per pass)
     }
 }
 __device__ __forceinline__ void store_survivor(const PathSoA& B, int i, const PathReg& p, bool with_slot) {
@@ -1650,6 +1651,19 @@ struct pt_ctx {
     // on the caller's stream (memory-bound finalize beside the VALU-bound first bounce).  A pass
     // waits for the finalize still reading its half; image readers wait for the last one.
     v4f* colbuf = nullptr;        // 2 x P
+    // Lanes (fused pipeline, spp >= 2): a pass's iterations are split in two; lane 0 traces the
+    // first ceil(spp/2) on the caller's stream with the buffers above, lane 1 the rest on
+    // lane_stream with its own path buffers and control words.  The lanes are independent (every
+    // path's RNG keys and colour slot depend only on its iteration), so one lane's first bounce,
+    // short tail bounces and launch gaps overlap the other's work.  PT_AMD_LANES=1 disables.
+    int lanes = 1;
+    PathSoA lbuf[2]{};
+    Ctl* lctl = nullptr;
+    int32_t* lseg = nullptr;
+    unsigned long long* lemit = nullptr;
+    uint64_t llaunches = 0;
+    hipStream_t lane_stream = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     hipStream_t fin_stream = nullptr;
     hipEvent_t ev_pass[2] = {}, ev_fin[2] = {};
     bool fin_out[2] = {false, false};
@@ -1662,6 +1676,9 @@ struct pt_ctx {
             if (ev_fin[h]) (void)hipEventDestroy(ev_fin[h]);
         }
         if (fin_stream) (void)hipStreamDestroy(fin_stream);
+        if (ev_fork) (void)hipEventDestroy(ev_fork);
+        if (ev_join) (void)hipEventDestroy(ev_join);
+        if (lane_stream) (void)hipStreamDestroy(lane_stream);
         for (void* p : allocs) (void)hipFree(p);
     }
     template <typename T>
@@ -2153,16 +2170,17 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
     // ---- path state, image, control ----
     // k_bounce writes workgroup b's survivors at b * chunk: with the per-iteration layout the last
     // segment can end past P by < spp chunks (tiles <= P/256 + spp, tpb <= ceil(tiles / (grid - spp))).
-    {
+    auto path_cap = [&](long long paths, long long spp, size_t* cap) {
         const long long g = std::min(c->grid_bounce[0], c->grid_bounce[1]);
-        const long long tiles = (P + kBlock - 1) / kBlock + sh.spp;
-        const long long tpb = (tiles + g - sh.spp - 1) / (g - sh.spp);
-        c->path_cap = (size_t)kBlock * (size_t)(tiles + sh.spp * tpb);
+        const long long tiles = (paths + kBlock - 1) / kBlock + spp;
+        const long long tpb = (tiles + g - spp - 1) / (g - spp);
+        *cap = (size_t)kBlock * (size_t)(tiles + spp * tpb);
         if (tpb * kBlock > (long long)kSegCountMask)
-            return bail(pt::fail(PT_ERR_ARG, "pass too large for the bounce kernel's segment words (chunk >= 2^24)"));
-        if (c->path_cap > (size_t)0x7fffffff)
-            return bail(pt::fail(PT_ERR_ARG, "pass too large: path buffer index exceeds int32"));
-    }
+            return pt::fail(PT_ERR_ARG, "pass too large for the bounce kernel's segment words (chunk >= 2^24)");
+        if (*cap > (size_t)0x7fffffff) return pt::fail(PT_ERR_ARG, "pass too large: path buffer index exceeds int32");
+        return (int)PT_OK;
+    };
+    if (int rc = path_cap(P, sh.spp, &c->path_cap)) return bail(rc);
     for (int b = 0; b < 2; ++b)
         if (int rc = alloc_paths(c, c->buf[b], c->path_cap)) return bail(rc);
     if (int rc = c->alloc(&A.image, (size_t)npix * 3)) return bail(rc);
@@ -2188,6 +2206,28 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
     if ((e = hipMemset(A.emit_slots, 0, (size_t)64 * A.emit_stride * sizeof(unsigned long long))) != hipSuccess)
         return bail(pt::fail(PT_ERR_HIP, std::string("hipMemset: ") + hipGetErrorString(e)));
     A.max_tiles = c->max_tiles;
+    A.count_pass = 1;
+    {
+        const char* lv = std::getenv("PT_AMD_LANES");
+        if (sh.spp >= 2 && !(lv && std::atoi(lv) == 1)) {   // lane 1: floor(spp / 2) iterations
+            const int n1 = sh.spp / 2;
+            size_t cap1 = 0;
+            if (int rc = path_cap((long long)n1 * (long long)npix, n1, &cap1)) return bail(rc);
+            for (int b = 0; b < 2; ++b)
+                if (int rc = alloc_paths(c, c->lbuf[b], cap1)) return bail(rc);
+            if (int rc = c->alloc(&c->lctl, 2)) return bail(rc);
+            if (int rc = c->alloc(&c->lseg, (size_t)2 * kMaxSeg)) return bail(rc);
+            if (int rc = c->alloc(&c->lemit, (size_t)64 * A.emit_stride)) return bail(rc);
+            if ((e = hipMemset(c->lctl, 0, 2 * sizeof(Ctl))) != hipSuccess ||
+                (e = hipMemset(c->lseg, 0, (size_t)2 * kMaxSeg * sizeof(int32_t))) != hipSuccess ||
+                (e = hipMemset(c->lemit, 0, (size_t)64 * A.emit_stride * sizeof(unsigned long long))) != hipSuccess ||
+                (e = hipStreamCreateWithFlags(&c->lane_stream, hipStreamNonBlocking)) != hipSuccess ||
+                (e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming)) != hipSuccess ||
+                (e = hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming)) != hipSuccess)
+                return bail(pt::fail(PT_ERR_HIP, std::string("lane setup: ") + hipGetErrorString(e)));
+            c->lanes = 2;
+        }
+    }
     if ((e = hipMemset(A.image, 0, (size_t)npix * 3 * sizeof(float))) != hipSuccess ||
         (e = hipMemset(A.ctl, 0, 2 * sizeof(Ctl))) != hipSuccess ||
         (e = hipMemset(A.seg, 0, (size_t)2 * kMaxSeg * sizeof(int32_t))) != hipSuccess ||
@@ -2255,7 +2295,44 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
         A.colbuf = c->colbuf + (size_t)h * (size_t)A.tile.P;
         if (c->fin_out[h]) HIP_TRY(hipStreamWaitEvent(st, c->ev_fin[h], 0));   // pass p-2's finalize
     }
-    for (int b = 0; b < c->depth; ++b) {
+    if (!sorted && c->fused && c->lanes == 2 && !spp1) {
+        const int npix = A.tile.npix;
+        const int n1 = A.tile.spp / 2, n0 = A.tile.spp - n1;
+        KArgs L[2] = {A, A};
+        L[0].tile.spp = n0;
+        L[0].tile.P = n0 * npix;
+        L[1].tile.spp = n1;
+        L[1].tile.P = n1 * npix;
+        L[1].tile.iter_first = iter_first + n0;
+        L[1].colbuf = A.colbuf + (size_t)n0 * (size_t)npix;
+        L[1].ctl = c->lctl;
+        L[1].seg = c->lseg;
+        L[1].emit_slots = c->lemit;
+        L[1].count_pass = 0;
+        const hipStream_t ls[2] = {st, c->lane_stream};
+        const PathSoA* bufs[2] = {c->buf, c->lbuf};
+        uint64_t* cnt[2] = {&c->compact_launches, &c->llaunches};
+        HIP_TRY(hipEventRecord(c->ev_fork, st));   // after the wait for this colour half above
+        HIP_TRY(hipStreamWaitEvent(c->lane_stream, c->ev_fork, 0));
+        int lcur[2] = {0, 0};
+        for (int b = 0; b < c->depth; ++b)
+            for (int l = 0; l < 2; ++l) {
+                KArgs& a = L[l];
+                a.parity = (int)(*cnt[l] & 1);
+                a.bounce = b;
+                a.n_fixed = b == 0 ? a.tile.P : -1;
+                a.in = bufs[l][lcur[l]];
+                a.out = bufs[l][lcur[l] ^ 1];
+                if (int rc = launch_k(c, bounce_kernel(b == 0, false, mesh), c->grid_bounce[b == 0], ls[l],
+                                      b == 0 ? PT_KIND_FIRST_BOUNCE : PT_KIND_BOUNCE, a, bounce_lds_bytes(a.S)))
+                    return rc;
+                ++*cnt[l];
+                lcur[l] ^= 1;
+            }
+        HIP_TRY(hipEventRecord(c->ev_join, c->lane_stream));
+        HIP_TRY(hipStreamWaitEvent(st, c->ev_join, 0));
+    }
+    for (int b = 0; b < c->depth && !(!sorted && c->fused && c->lanes == 2 && !spp1); ++b) {
         const bool last = b == c->depth - 1;   // every path is dead after the last bounce
         A.parity = (int)(c->compact_launches & 1);
         A.bounce = b;
@@ -2390,6 +2467,11 @@ int pt_stats(pt_ctx* c, pt_stats_t* out) {
     std::vector<unsigned long long> slots((size_t)64 * c->args.emit_stride);
     HIP_TRY(hipMemcpy(slots.data(), c->args.emit_slots, slots.size() * sizeof(unsigned long long),
                       hipMemcpyDeviceToHost));
+    if (c->lemit) {   // lane 1's per-workgroup counts
+        std::vector<unsigned long long> l1(slots.size());
+        HIP_TRY(hipMemcpy(l1.data(), c->lemit, l1.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        for (size_t j = 0; j < slots.size(); ++j) slots[j] += l1[j];
+    }
     std::memset(out, 0, sizeof *out);
     out->segments = s.segments;
     out->passes = s.passes;
@@ -2423,19 +2505,35 @@ int pt_profile_enable(pt_ctx* c, int32_t on) {
     return PT_OK;
 }
 
-int pt_profile_read(pt_ctx* c, double ms[4], uint64_t launches[4]) {
+int pt_profile_read_busy(pt_ctx* c, double ms[4], double busy_ms[4], uint64_t launches[4]) {
     if (!c || !ms || !launches) return pt::fail(PT_ERR_ARG, "null argument");
-    for (int k = 0; k < 4; ++k) { ms[k] = 0.0; launches[k] = 0; }
+    std::vector<std::pair<double, double>> iv[4];   // per kind: [start, end) after the first event
+    for (int k = 0; k < 4; ++k) { ms[k] = 0.0; launches[k] = 0; if (busy_ms) busy_ms[k] = 0.0; }
     for (size_t i = 0; i < c->ev_used; ++i) {
         ProfEv& ev = c->events[i];
         HIP_TRY(hipEventSynchronize(ev.b));
-        float t = 0.f;
+        float t = 0.f, t0 = 0.f;
         HIP_TRY(hipEventElapsedTime(&t, ev.a, ev.b));
+        HIP_TRY(hipEventElapsedTime(&t0, c->events[0].a, ev.a));
         ms[ev.kind] += t;
         launches[ev.kind] += 1;
+        iv[ev.kind].push_back({(double)t0, (double)t0 + (double)t});
     }
+    if (busy_ms)   // union of each kind's launch intervals: lanes run kernels of one kind concurrently
+        for (int k = 0; k < 4; ++k) {
+            std::sort(iv[k].begin(), iv[k].end());
+            double end = -1e300;
+            for (const auto& x : iv[k]) {
+                if (x.first > end) { busy_ms[k] += x.second - x.first; end = x.second; }
+                else if (x.second > end) { busy_ms[k] += x.second - end; end = x.second; }
+            }
+        }
     c->ev_used = 0;
     return PT_OK;
+}
+
+int pt_profile_read(pt_ctx* c, double ms[4], uint64_t launches[4]) {
+    return pt_profile_read_busy(c, ms, nullptr, launches);
 }
 
 }  // extern "C"

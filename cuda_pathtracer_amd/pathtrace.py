@@ -273,11 +273,13 @@ class PathTracer:
     KINDS = ("first_bounce", "bounce", "compact", "sort")
 
     def profile_read(self) -> dict:
-        """{kind: (summed ms, launches)} since the previous read (HIP events on the launch stream)."""
+        """{kind: (summed ms, launches, busy ms)} since the previous read (HIP events on the launch
+        streams); busy ms = the union of the kind's launch intervals (lanes overlap launches)."""
         ms = (C.c_double * 4)()
+        busy = (C.c_double * 4)()
         n = (C.c_uint64 * 4)()
-        check_pt(lib().pt_profile_read(self._h, ms, n))
-        return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(self.KINDS)}
+        check_pt(lib().pt_profile_read_busy(self._h, ms, busy, n))
+        return {k: (float(ms[i]), int(n[i]), float(busy[i])) for i, k in enumerate(self.KINDS)}
 
 
 def tonemap(image: np.ndarray, samples: float) -> np.ndarray:

@@ -223,6 +223,10 @@ int pt_stats(pt_ctx* c, pt_stats_t* out);                   /* synchronises the 
 #define PT_KIND_SORT 3           /* material-sorted mode: raygen/isect/scan/scatter/shade      */
 int pt_profile_enable(pt_ctx* c, int32_t on);
 int pt_profile_read(pt_ctx* c, double ms[4], uint64_t launches[4]);
+/* Same, plus busy_ms[kind]: the length of the union of that kind's launch intervals.  Batched
+ * passes of the fused pipeline run two lanes of iterations concurrently (pt_render_pass), so
+ * launches of one kind overlap and busy_ms < ms. */
+int pt_profile_read_busy(pt_ctx* c, double ms[4], double busy_ms[4], uint64_t launches[4]);
 
 /* ---- image output ---------------------------------------------------------------------- */
 /* saveImage + Image::savePNG pixel math: out[3*(y*W + (W-1-x)) + k] = uchar(clamp(rgb/spp,0,1)*255). */
