@@ -10,3 +10,4 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gp
     python3 "$R/bench.py" --steps 50 --no-cpu-baseline --scan-reps 5 > "$R/gpurun_out/prof_bench.json" 2> "$R/gpurun_out/prof_bench.err" \
     || { echo "rocprof failed rc=$?"; tail -20 "$R/gpurun_out/prof_bench.err"; exit 1; }
 find "$R/gpurun_out/prof" -name "*stats*" | head
+python3 "$R/scripts/trace_busy.py" "$(find "$R/gpurun_out/prof" -name "*kernel_trace.csv" | head -1)" | tee "$R/gpurun_out/prof/busy.txt"
