@@ -333,6 +333,9 @@ def main() -> None:
                                                   os.environ.get("PT_AMD_LANES") != "1" and
                                                   os.environ.get("PT_PIPELINE") != "split") else 1,
                 "achieved_definition": "184 B x segments of bounces >= 1 / union of their launch intervals",
+                # the same bytes per launch over the average launch duration: with two lanes each
+                # launch shares the GPU with the other lane's, so this understates the kernel
+                "achieved_per_launch": per_launch_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0,
                 "segments_per_launch": seg_bounce / max(b_n, 1),
                 "algorithmic_bytes_per_launch": per_launch_bytes,
                 "kernel_min_bytes_per_launch": kernel_min / max(b_n, 1)}
