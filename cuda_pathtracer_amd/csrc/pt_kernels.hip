@@ -1577,6 +1577,96 @@ __global__ __launch_bounds__(kBlock) void k_sort_shade(const KArgs A, const Sort
     flush_emissive(A, emit_cnt, &s_cnt);
 }
 
+// Exclusive scan of the sorted pipeline's histogram when two lanes share the GPU: reduce, scan of
+// the tile sums (one workgroup), rescan.  No workgroup waits on another, so unlike the library's
+// single-pass scan (whose static schedule needs its whole grid co-resident) two of these can run
+// side by side.  The histogram is small (nmats x paths / 64 ints) and cache-resident.
+constexpr int kHistPer = 16;                       // ints per thread
+constexpr int kHistTile = kBlock * kHistPer;       // 4096
+
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_w, uint32_t* total) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t incl = lb::wave_inclusive_scan(v);
+    __syncthreads();   // previous users of s_w are done
+    if (lane == 63) s_w[wave] = incl;
+    __syncthreads();
+    uint32_t before = 0;
+    for (int w = 0; w < wave; ++w) before += s_w[w];
+    *total = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+    return before + incl - v;
+}
+
+typedef int v4i_h __attribute__((ext_vector_type(4)));
+// this thread's 16 consecutive ints (four 16-byte loads; guarded at the end of the array)
+__device__ __forceinline__ void hist_load(const int32_t* __restrict__ in, int64_t n, int64_t base, uint32_t (&x)[kHistPer]) {
+    if (base + kHistPer <= n) {
+#pragma unroll
+        for (int q = 0; q < kHistPer / 4; ++q) {
+            const v4i_h v = *reinterpret_cast<const v4i_h*>(in + base + 4 * q);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) x[4 * q + e] = (uint32_t)v[e];
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < kHistPer; ++k) x[k] = base + k < n ? (uint32_t)in[base + k] : 0u;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_hist_sums(const int32_t* __restrict__ in, int64_t n,
+                                                      uint32_t* __restrict__ sums) {
+    __shared__ uint32_t s_w[4];
+    const int64_t base = (int64_t)blockIdx.x * kHistTile + (int64_t)threadIdx.x * kHistPer;
+    uint32_t x[kHistPer], v = 0;
+    hist_load(in, n, base, x);
+#pragma unroll
+    for (int k = 0; k < kHistPer; ++k) v += x[k];
+    uint32_t total;
+    (void)block_excl_scan(v, s_w, &total);
+    if (threadIdx.x == 0) sums[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(kBlock) void k_hist_scan_sums(uint32_t* __restrict__ sums, int tiles) {
+    __shared__ uint32_t s_w[4];
+    const int per = (tiles + kBlock - 1) / kBlock;
+    const int j0 = (int)threadIdx.x * per;
+    uint32_t v = 0;
+    for (int j = j0; j < j0 + per && j < tiles; ++j) v += sums[j];
+    uint32_t total;
+    uint32_t run = block_excl_scan(v, s_w, &total);
+    for (int j = j0; j < j0 + per && j < tiles; ++j) {
+        const uint32_t x = sums[j];
+        sums[j] = run;
+        run += x;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_hist_apply(const int32_t* __restrict__ in, int32_t* __restrict__ out,
+                                                       int64_t n, const uint32_t* __restrict__ sums) {
+    __shared__ uint32_t s_w[4];
+    const int64_t base = (int64_t)blockIdx.x * kHistTile + (int64_t)threadIdx.x * kHistPer;
+    uint32_t x[kHistPer], v = 0;
+    hist_load(in, n, base, x);
+#pragma unroll
+    for (int k = 0; k < kHistPer; ++k) v += x[k];
+    uint32_t total;
+    uint32_t run = block_excl_scan(v, s_w, &total) + sums[blockIdx.x];
+    if (base + kHistPer <= n) {
+#pragma unroll
+        for (int q = 0; q < kHistPer / 4; ++q) {
+            v4i_h o;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) { o[e] = (int32_t)run; run += x[4 * q + e]; }
+            *reinterpret_cast<v4i_h*>(out + base + 4 * q) = o;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < kHistPer; ++k) {
+            if (base + k < n) out[base + k] = (int32_t)run;
+            run += x[k];
+        }
+    }
+}
+
 // spp > 1: add the per-slot colours in sample order (finalGather as `spp` sequential iterations).
 __global__ void k_finalize_spp(float* __restrict__ image, const v4f* __restrict__ col, int npix, int spp) {
     for (int lp = blockIdx.x * blockDim.x + threadIdx.x; lp < npix; lp += gridDim.x * blockDim.x) {
@@ -1664,6 +1754,14 @@ struct pt_ctx {
     uint64_t llaunches = 0;
     hipStream_t lane_stream = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    struct SortSet {   // lane 1's material-sort buffers (lane 0 uses the context's own)
+        int32_t *keys = nullptr, *phys = nullptr, *hist = nullptr, *offs = nullptr, *perm = nullptr;
+        int32_t *tbase = nullptr, *ibase = nullptr;
+        float* uv = nullptr;
+        void* ws = nullptr;
+        int64_t hist_n = 0;
+        int max_t64 = 0;
+    } lsort;
     hipStream_t fin_stream = nullptr;
     hipEvent_t ev_pass[2] = {}, ev_fin[2] = {};
     bool fin_out[2] = {false, false};
@@ -2254,6 +2352,29 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
         if (int rc = c->alloc(&ws, sc_workspace_bytes((int64_t)hn))) return bail(rc);
         c->scan_ws = ws;
     }
+    if (c->lanes == 2) {   // lane 1's sort buffers, sized for its floor(spp / 2) iterations
+        auto& L = c->lsort;
+        const int n1 = sh.spp / 2;
+        const long long P1 = (long long)n1 * (long long)npix;
+        size_t cap1 = 0;
+        if (int rc = path_cap(P1, n1, &cap1)) return bail(rc);
+        L.max_t64 = (int)((P1 + 63) / 64);
+        const size_t hn = (size_t)c->nmats * ((size_t)L.max_t64 + n1) + 1;
+        L.hist_n = (int64_t)hn;
+        uint8_t* ws;
+        if (int rc = c->alloc(&L.uv, 2 * cap1)) return bail(rc);
+        if (int rc = c->alloc(&L.phys, (size_t)P1)) return bail(rc);
+        if (int rc = c->alloc(&L.keys, (size_t)P1)) return bail(rc);
+        if (int rc = c->alloc(&L.perm, (size_t)P1)) return bail(rc);
+        if (int rc = c->alloc(&L.tbase, (size_t)kMaxSpp + 1)) return bail(rc);
+        if (int rc = c->alloc(&L.ibase, (size_t)kMaxSpp + 1)) return bail(rc);
+        if (int rc = c->alloc(&L.hist, hn)) return bail(rc);
+        if (int rc = c->alloc(&L.offs, hn)) return bail(rc);
+        if (int rc = c->alloc(&ws, sc_workspace_bytes((int64_t)hn))) return bail(rc);
+        L.ws = ws;
+        if ((e = hipMemset(L.hist, 0, hn * sizeof(int32_t))) != hipSuccess)
+            return bail(pt::fail(PT_ERR_HIP, std::string("hipMemset: ") + hipGetErrorString(e)));
+    }
     if (const char* pl = std::getenv("PT_PIPELINE")) c->fused = std::string(pl) != "split";
     *out = c;
     return PT_OK;
@@ -2295,7 +2416,40 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
         A.colbuf = c->colbuf + (size_t)h * (size_t)A.tile.P;
         if (c->fin_out[h]) HIP_TRY(hipStreamWaitEvent(st, c->ev_fin[h], 0));   // pass p-2's finalize
     }
-    if (!sorted && c->fused && c->lanes == 2 && !spp1) {
+    const bool laned = (sorted || c->fused) && c->lanes == 2 && !spp1;
+    // One bounce of the material-sorted pipeline on stream s.  With two lanes the histogram scan
+    // is k_hist_sums / k_hist_scan_sums / k_hist_apply (no co-residency needed: the other lane's
+    // scan may run at the same time); alone, the library's single-pass scan.
+    auto sort_bounce = [&](const KArgs& a, const SortArgs& sa, int64_t hn, void* ws, int max_t64, hipStream_t s,
+                           int b) -> int {
+        const int g64 = std::min((max_t64 + 3) / 4, c->grid_trace);   // grid-stride beyond
+        ProfEv* ev;
+        if (int rc = prof_begin(c, s, PT_KIND_SORT, &ev)) return rc;
+        if (b == 0 && mesh) hipLaunchKernelGGL((k_sort_isect<true, true>), dim3(g64), dim3(kBlock), 0, s, a, sa);
+        else if (b == 0) hipLaunchKernelGGL((k_sort_isect<true, false>), dim3(g64), dim3(kBlock), 0, s, a, sa);
+        else if (mesh) hipLaunchKernelGGL((k_sort_isect<false, true>), dim3(g64), dim3(kBlock), 0, s, a, sa);
+        else hipLaunchKernelGGL((k_sort_isect<false, false>), dim3(g64), dim3(kBlock), 0, s, a, sa);
+        HIP_TRY(hipGetLastError());
+        int32_t* offs = const_cast<int32_t*>(sa.offs);
+        if (laned) {
+            const int tiles = (int)((hn + kHistTile - 1) / kHistTile);
+            uint32_t* sums = static_cast<uint32_t*>(ws);   // tiles words (the workspace holds >= hn)
+            hipLaunchKernelGGL(k_hist_sums, dim3(tiles), dim3(kBlock), 0, s, (const int32_t*)sa.hist, hn, sums);
+            hipLaunchKernelGGL(k_hist_scan_sums, dim3(1), dim3(kBlock), 0, s, sums, tiles);
+            hipLaunchKernelGGL(k_hist_apply, dim3(tiles), dim3(kBlock), 0, s, (const int32_t*)sa.hist, offs, hn,
+                               (const uint32_t*)sums);
+            HIP_TRY(hipGetLastError());
+        } else if (sc_scan_exclusive_i32(sa.hist, offs, hn, ws, s) != SC_OK) {
+            return pt::fail(PT_ERR_HIP, std::string("material scan: ") + sc_last_error());
+        }
+        hipLaunchKernelGGL(k_sort_scatter, dim3(g64), dim3(kBlock), 0, s, a, sa);
+        HIP_TRY(hipGetLastError());
+        if (spp1) hipLaunchKernelGGL(k_sort_shade<true>, dim3(c->grid_bounce[0]), dim3(kBlock), 0, s, a, sa);
+        else hipLaunchKernelGGL(k_sort_shade<false>, dim3(c->grid_bounce[0]), dim3(kBlock), 0, s, a, sa);
+        HIP_TRY(hipGetLastError());
+        return prof_end(ev, s);
+    };
+    if (laned) {
         const int npix = A.tile.npix;
         const int n1 = A.tile.spp / 2, n0 = A.tile.spp - n1;
         KArgs L[2] = {A, A};
@@ -2309,6 +2463,14 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
         L[1].seg = c->lseg;
         L[1].emit_slots = c->lemit;
         L[1].count_pass = 0;
+        L[1].hit.uv = c->lsort.uv;
+        L[1].ibase = c->lsort.ibase;
+        const SortArgs SL[2] = {{c->keys, c->phys, c->hist, c->offs, c->perm, c->tbase, A.ibase},
+                                {c->lsort.keys, c->lsort.phys, c->lsort.hist, c->lsort.offs, c->lsort.perm,
+                                 c->lsort.tbase, c->lsort.ibase}};
+        const int64_t lhn[2] = {c->hist_n, c->lsort.hist_n};
+        void* lws[2] = {c->scan_ws, c->lsort.ws};
+        const int lt64[2] = {c->max_t64, c->lsort.max_t64};
         const hipStream_t ls[2] = {st, c->lane_stream};
         const PathSoA* bufs[2] = {c->buf, c->lbuf};
         uint64_t* cnt[2] = {&c->compact_launches, &c->llaunches};
@@ -2323,16 +2485,19 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
                 a.n_fixed = b == 0 ? a.tile.P : -1;
                 a.in = bufs[l][lcur[l]];
                 a.out = bufs[l][lcur[l] ^ 1];
-                if (int rc = launch_k(c, bounce_kernel(b == 0, false, mesh), c->grid_bounce[b == 0], ls[l],
-                                      b == 0 ? PT_KIND_FIRST_BOUNCE : PT_KIND_BOUNCE, a, bounce_lds_bytes(a.S)))
+                if (sorted) {
+                    if (int rc = sort_bounce(a, SL[l], lhn[l], lws[l], lt64[l], ls[l], b)) return rc;
+                } else if (int rc = launch_k(c, bounce_kernel(b == 0, false, mesh), c->grid_bounce[b == 0], ls[l],
+                                             b == 0 ? PT_KIND_FIRST_BOUNCE : PT_KIND_BOUNCE, a, bounce_lds_bytes(a.S))) {
                     return rc;
+                }
                 ++*cnt[l];
                 lcur[l] ^= 1;
             }
         HIP_TRY(hipEventRecord(c->ev_join, c->lane_stream));
         HIP_TRY(hipStreamWaitEvent(st, c->ev_join, 0));
     }
-    for (int b = 0; b < c->depth && !(!sorted && c->fused && c->lanes == 2 && !spp1); ++b) {
+    for (int b = 0; b < c->depth && !laned; ++b) {
         const bool last = b == c->depth - 1;   // every path is dead after the last bounce
         A.parity = (int)(c->compact_launches & 1);
         A.bounce = b;
@@ -2357,24 +2522,8 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
                 cur ^= 1;
             }
         } else {
-            SortArgs SA{c->keys, c->phys, c->hist, c->offs, c->perm, c->tbase, A.ibase};
-            const int g64 = std::min((c->max_t64 + 3) / 4, c->grid_trace);   // grid-stride beyond
-            ProfEv* ev;
-            if ((rc = prof_begin(c, st, PT_KIND_SORT, &ev))) return rc;
-            if (b == 0 && mesh) hipLaunchKernelGGL((k_sort_isect<true, true>), dim3(g64), dim3(kBlock), 0, st, A, SA);
-            else if (b == 0) hipLaunchKernelGGL((k_sort_isect<true, false>), dim3(g64), dim3(kBlock), 0, st, A, SA);
-            else if (mesh) hipLaunchKernelGGL((k_sort_isect<false, true>), dim3(g64), dim3(kBlock), 0, st, A, SA);
-            else hipLaunchKernelGGL((k_sort_isect<false, false>), dim3(g64), dim3(kBlock), 0, st, A, SA);
-            HIP_TRY(hipGetLastError());
-            const int64_t hn = c->hist_n;
-            if (sc_scan_exclusive_i32(c->hist, c->offs, hn, c->scan_ws, st) != SC_OK)
-                return pt::fail(PT_ERR_HIP, std::string("material scan: ") + sc_last_error());
-            hipLaunchKernelGGL(k_sort_scatter, dim3(g64), dim3(kBlock), 0, st, A, SA);
-            HIP_TRY(hipGetLastError());
-            if (spp1) hipLaunchKernelGGL(k_sort_shade<true>, dim3(c->grid_bounce[0]), dim3(kBlock), 0, st, A, SA);
-            else hipLaunchKernelGGL(k_sort_shade<false>, dim3(c->grid_bounce[0]), dim3(kBlock), 0, st, A, SA);
-            HIP_TRY(hipGetLastError());
-            if ((rc = prof_end(ev, st))) return rc;
+            const SortArgs SA{c->keys, c->phys, c->hist, c->offs, c->perm, c->tbase, A.ibase};
+            if ((rc = sort_bounce(A, SA, c->hist_n, c->scan_ws, c->max_t64, st, b))) return rc;
             ++c->compact_launches;
             cur ^= 1;
         }
