@@ -329,9 +329,9 @@ def main() -> None:
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": None if gui.sortbyMaterial else _traffic_from_profiles("k_bounce"),
                 "kernel": kernel_name, "avg_launch_ms": avg_ms, "launches": b_n,
-                "busy_ms": b_busy, "lanes": 2 if (spp > 1 and not gui.sortbyMaterial and
-                                                  os.environ.get("PT_AMD_LANES") != "1" and
-                                                  os.environ.get("PT_PIPELINE") != "split") else 1,
+                "busy_ms": b_busy, "lanes": 2 if (spp > 1 and os.environ.get("PT_AMD_LANES") != "1" and
+                                                  (gui.sortbyMaterial or os.environ.get("PT_PIPELINE") != "split"))
+                                           else 1,
                 "achieved_definition": "184 B x segments of bounces >= 1 / union of their launch intervals",
                 # the same bytes per launch over the average launch duration: with two lanes each
                 # launch shares the GPU with the other lane's, so this understates the kernel
