@@ -306,7 +306,7 @@ def main() -> None:
     b_ms, b_n, b_busy = prof["bounce"]
     if b_n == 0:   # material-sorted pipeline: its kernels are all profiled under "sort"
         b_ms, b_n = prof["sort"][0], max(1, prof_passes * (st_r.traceDepth - 1))
-        b_busy = b_ms
+        b_busy = prof["sort"][2]   # union over both lanes (includes the first bounce's sort kernels)
     f_ms, f_n, _ = prof["first_bounce"]
     depth = st_r.traceDepth
     plive = [b - a for a, b in zip(sp0["bounce_live"], sp1["bounce_live"])]
