@@ -12,10 +12,18 @@ timed region).  value = all ranks' traced segments / max-over-ranks wall time / 
 
 Roofline: the dominant kernel is the fused bounce kernel k_bounce<false,...> (bounces >= 1).
 Its average launch time comes from HIP events recorded on its launch stream over a profiled
-segment of the same workload; its algorithmic bytes per launch are SURVEY.md §8d's 184 B per
-traced segment (ray 24 + hit write 28 + hit read 28 + path read 48 + write 48 + compaction 8)
-x the segments that launch traces.  The fused kernel itself needs only
-44 B in + 44 B per survivor + 24 B per emissive hit, reported as kernel_min_bytes.
+segment of the same workload (rocprofv3 --kernel-trace --stats of the same command agrees:
+profiles/r02_*); its algorithmic bytes per launch are SURVEY.md §8d's 184 B per traced segment
+(ray 24 + hit write 28 + hit read 28 + path read 48 + write 48 + compaction 8) x the segments that
+launch traces.  roofline.frac = those bytes / the average launch duration / 8 TB/s,
+per launch.  Batched passes run two lanes of iterations whose launches overlap; the bytes over the
+union of the launch intervals are reported separately (roofline.aggregate).  The fused kernel itself
+needs only 44 B in + 44 B per survivor + 24 B per emissive hit (kernel_min_bytes).
+Measured in the same run (N = 1): rocprofv3 --pmc passes over the same workload (scripts/pmc.py)
+give the kernel's fabric traffic per launch (roofline.traffic, FETCH_SIZE x 2 + WRITE_SIZE) and its
+VALU wave-instructions (roofline.valu_issue: against the chip's VALU issue rate, 256 CUs x 4 SIMDs x
+2.4 GHz / 2 cycles per wave64 instruction, MI355X_MICROARCH.md) — the kernel is issue/latency-bound,
+not bandwidth-bound (roofline.limiter).
 The scan kernel is measured separately at n = 2^28 (8 B/element, 2 GiB, beyond the 256 MiB MALL).
 """
 from __future__ import annotations
@@ -34,6 +42,7 @@ sys.path.insert(0, str(ROOT))
 
 METRIC = "Mray/s (paths×bounces/s) on Cornell scene + scan GB/s vs HBM peak, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+VALU_PEAK = 256 * 4 * 2.4e9 / 2   # wave64 VALU instructions/s: 4 SIMD-32 per CU, 2 cycles each (same guide)
 SEGMENT_BYTES = 184            # SURVEY.md §8d algorithmic bytes per traced segment
 PATH_BYTES = 44                # fused kernel's path state: o(12) d(12) c(12) slot(4) bounces(4)
 FB_RMW_BYTES = 24              # float3 read + write
@@ -42,19 +51,6 @@ FB_RMW_BYTES = 24              # float3 read + write
 def _log(rank, *a):
     if rank == 0:
         print(*a, file=sys.stderr, flush=True)
-
-
-def _traffic_from_profiles(kernel_key: str):
-    """HBM bytes per launch from the committed rocprofv3 PMC measurement (profiles/*traffic*.json)."""
-    best = None
-    for p in sorted((ROOT / "profiles").glob("*traffic*.json")):
-        try:
-            d = json.loads(p.read_text())
-        except Exception:
-            continue
-        if kernel_key in d:
-            best = d[kernel_key]
-    return best
 
 
 def _host_cpu() -> str:
@@ -115,6 +111,7 @@ def cpu_baseline_render_mt(seconds_target: float, threads: int) -> dict:
 
 
 def cpu_baseline_scan(n: int = 1 << 20, reps: int = 50) -> dict:
+    """CPU::scan (cpu.cu:16-33) restated, 1 thread, timed like PerformanceTimer (common.h:61-80)."""
     from oracle import binding as O
     a = np.random.default_rng(1234).integers(0, 50, n, dtype=np.int32)
     a[-1] = 0
@@ -123,6 +120,26 @@ def cpu_baseline_scan(n: int = 1 << 20, reps: int = 50) -> dict:
     ms = O.lib().oracle_time_scan_ms(n, a.ctypes.data, out.ctypes.data, reps) / reps
     return {"n": n, "ms": ms, "GB/s": 8.0 * n / (ms * 1e-3) / 1e9, "cores": 1, "kind": "port", "host": _host_cpu(),
             "sample": f"CPU::scan restated (oracle/sc_oracle.cpp), {reps} reps, U[0,50) seed 1234"}
+
+
+def cpu_baseline_compact(n: int = 1 << 20, reps: int = 20) -> dict:
+    """CPU::compactWithScan and CPU::compactWithoutScan (cpu.cu:40-79) restated, 1 thread, on
+    SC/src/main.cpp's compaction input shape (U[0,4), last element 0; ~75% kept).  GB/s at the
+    algorithmic 4 B read per element + 4 B written per kept element."""
+    import ctypes as C
+    from oracle import binding as O
+    a = np.random.default_rng(4321).integers(0, 4, n, dtype=np.int32)
+    a[-1] = 0
+    out = np.zeros_like(a)
+    res = {"n": n, "cores": 1, "kind": "port", "host": _host_cpu(),
+           "sample": f"oracle/sc_oracle.cpp, {reps} reps, U[0,4) seed 4321"}
+    for name, fn in (("with_scan", O.lib().oracle_time_compact_ms),
+                     ("without_scan", O.lib().oracle_time_compact_without_scan_ms)):
+        cnt = C.c_int64(0)
+        fn(n, a.ctypes.data, out.ctypes.data, 1, C.byref(cnt))  # warm
+        ms = fn(n, a.ctypes.data, out.ctypes.data, reps, C.byref(cnt)) / reps
+        res[name] = {"ms": ms, "kept": cnt.value, "GB/s": (4.0 * n + 4.0 * cnt.value) / (ms * 1e-3) / 1e9}
+    return res
 
 
 def scan_bench(torch, dev, n: int, reps: int) -> dict:
@@ -147,10 +164,9 @@ def scan_bench(torch, dev, n: int, reps: int) -> dict:
     ok = bool(torch.equal(out[1:] - out[:-1], a[:-1])) and int(out[0].item()) == 0
     del P
     gbs = 8.0 * n / (ms * 1e-3) / 1e9
-    traffic = _traffic_from_profiles("scan")
     return {"n": n, "ms": ms, "ms_min": times[0], "GB/s": gbs, "verified": ok,
             "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": gbs / HBM_PEAK_GBS, "traffic": traffic}}
+                         "frac": gbs / HBM_PEAK_GBS}}
 
 
 def compact_bench(torch, dev, n: int, reps: int) -> dict:
@@ -178,16 +194,69 @@ def compact_bench(torch, dev, n: int, reps: int) -> dict:
     return {"n": n, "kept": kept, "ms": ms, "GB/s": gbs, "frac": gbs / HBM_PEAK_GBS, "verified": ok}
 
 
+def _pmc_leg(args, scene_path, spp_pass, sorted_, avg_ms, kernel_prefix, seg_per_launch, busy_ms, launches):
+    """rocprofv3 --pmc passes over the same workload (scripts/pmc.py): fabric traffic and VALU
+    wave-instructions per launch of the dominant kernel, and its wave-state split."""
+    sys.path.insert(0, str(ROOT / "scripts"))
+    import pmc
+    wl = [str(args.pmc_passes), f"spp={spp_pass}", f"scene={scene_path}"] + (["sort"] if sorted_ else []) + \
+         (["bvhcull"] if args.bvh_cull else [])
+    out_dir = ROOT / "gpurun_out" / "bench_pmc"
+    res = pmc.collect(wl, out_dir, timeout=args.pmc_timeout)
+    (out_dir / "summary.json").write_text(json.dumps(res, indent=1))
+    if sorted_:   # the sorted pipeline: every kernel of a bounce, per traced segment
+        ks = {k: m for k, m in res.get("kernels", {}).items()
+              if k.startswith(("k_sort_", "k_hist_", "k_scan_lag", "k_scan_tiles"))}
+        if not ks or not all("bytes_per_launch" in m for m in ks.values()):
+            return {"pmc": res["_passes"]}
+        total = sum(m["bytes_per_launch"] * m["launches"] for m in ks.values())
+        segs = res.get("segments") or 0
+        return {"pmc": res["_passes"], "traffic_per_segment": total / segs if segs else None,
+                "traffic_definition": "FETCH_SIZE x 2 + WRITE_SIZE of every sorted-pipeline kernel over the "
+                                      "profiled passes / their traced segments (all bounces)",
+                "traffic_kernels": sorted(ks)}
+    m = pmc.pick(res, kernel_prefix)
+    if m is None or "bytes_per_launch" not in m:
+        return {"pmc": res["_passes"]}
+    out = {"pmc": res["_passes"], "traffic": m["bytes_per_launch"],
+           "traffic_per_segment": m["bytes_per_launch"] / max(seg_per_launch, 1.0),
+           "traffic_frac": m["bytes_per_launch"] / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+    if "SQ_INSTS_VALU" in m:
+        valu = m["SQ_INSTS_VALU"]
+        wc = max(m.get("SQ_WAVE_CYCLES", 0.0), 1.0)
+        act, wi, wa = (m.get("SQ_ACTIVE_INST_ANY", 0.0) / wc, m.get("SQ_WAIT_INST_ANY", 0.0) / wc,
+                       m.get("SQ_WAIT_ANY", 0.0) / wc)
+        dur = m.get("dur_ns_sq", 0.0)
+        out["valu_issue"] = {
+            "unit": "wave64 VALU instr/s", "peak": VALU_PEAK,
+            "instructions_per_launch": valu, "instructions_per_segment": valu / max(seg_per_launch, 1.0),
+            "achieved": valu / (avg_ms * 1e-3), "frac": valu / (avg_ms * 1e-3) / VALU_PEAK,
+            "aggregate_frac": valu * launches / (busy_ms * 1e-3) / VALU_PEAK if busy_ms > 0 else None,
+            "salu_per_launch": m.get("SQ_INSTS_SALU"),
+            "effective_clock_ghz": m["GRBM_GUI_ACTIVE"] / 8.0 / dur if dur > 0 and "GRBM_GUI_ACTIVE" in m else None,
+            "definition": "SQ_INSTS_VALU per launch / HIP-event average launch duration / (256 CUs x 4 SIMDs x "
+                          "2.4 GHz / 2 cycles per wave64 VALU instruction)"}
+        out["wave_states"] = {"issuing": act, "waiting_on_issue": wi, "waiting_on_memory_or_barrier": wa,
+                              "waves_per_launch": m.get("SQ_WAVES")}
+        out["limiter"] = (f"VALU issue + latency, not bandwidth: waves issue {act:.0%} of their cycles, wait on "
+                          f"dependencies/arbitration {wi:.0%}, on memory/LDS/barriers {wa:.0%}; fabric traffic "
+                          f"{out['traffic_frac']:.0%} of the HBM peak")
+    return out
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--scan-n", type=int, default=1 << 28)
     ap.add_argument("--scan-reps", type=int, default=20)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-scan", action="store_true")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 --pmc passes (traffic, VALU issue)")
+    ap.add_argument("--pmc-passes", type=int, default=6)
+    ap.add_argument("--pmc-timeout", type=int, default=150)
     ap.add_argument("--scene", default=str(ROOT / "tests" / "scenes" / "cornell.json"))
     ap.add_argument("--config", default="cornell", choices=["cornell", "cornell_hd_sorted", "multi_object_4k",
                                                            "random_triangles_100k"],
@@ -195,8 +264,14 @@ def main() -> None:
                          "generated by cuda_pathtracer_amd.scenes")
     ap.add_argument("--bvh-cull", action="store_true", help="pt_flags.bvh_cull extension (mesh scenes)")
     ap.add_argument("--spp", type=int, default=32,
-                    help="iterations traced together per pass and GPU (a pass covers spp x N iterations of "
-                         "the rank's rows; results are bit-identical to one iteration per pass)")
+                    help="iterations per pass and GPU-share: a pass traces spp x N iterations of the rank's rows "
+                         "(so every GPU's pass has the 1-GPU pass's size); results are bit-identical to one "
+                         "iteration per pass")
+    ap.add_argument("--scaling", choices=["strong", "weak"], default="strong",
+                    help="strong (default): a step renders a FIXED batch of --samples samples per pixel of the "
+                         "whole image, split over the N GPUs by rows (8/N passes of 32N iterations at 256); "
+                         "weak: a step is one pass of spp x N iterations of the rank's rows")
+    ap.add_argument("--samples", type=int, default=256, help="strong scaling: samples per pixel per step")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -250,15 +325,22 @@ def main() -> None:
     gui.bvhCull = bool(args.bvh_cull)
     scene = P.Scene(scene_path)
     st_r = scene.state()
-    spp = world * max(1, args.spp)
+    spp = world * max(1, args.spp)          # iterations per pass of this rank's rows
+    passes_per_step = 1
+    if args.scaling == "strong":
+        passes_per_step = max(1, args.samples // spp)
+        if args.samples % passes_per_step:
+            raise SystemExit(f"--samples {args.samples} does not split into {passes_per_step} equal passes")
+        spp = args.samples // passes_per_step
     if spp > 256:   # pt_shard.spp limit (one thread of the bounce kernel's workgroup per iteration)
-        raise SystemExit(f"--spp {args.spp} x {world} GPUs = {spp} iterations per pass > 256")
+        raise SystemExit(f"{spp} iterations per pass > 256 (pt_shard.spp limit)")
     pt = P.PathTracer(scene, gui, rank=rank, world=world, spp=spp)
     stream = torch.cuda.current_stream()
-    _log(rank, f"[bench] tile rows={pt.rows} npix={pt.npix} paths/pass={pt.npaths} depth={st_r.traceDepth}")
+    _log(rank, f"[bench] {args.scaling} scaling: tile rows={pt.rows} npix={pt.npix} paths/pass={pt.npaths} "
+               f"passes/step={passes_per_step} depth={st_r.traceDepth}")
 
     it = 1
-    for _ in range(args.warmup):
+    for _ in range(args.warmup * passes_per_step):
         pt.render_pass(it, stream)
         it += spp
     torch.cuda.synchronize()
@@ -268,7 +350,7 @@ def main() -> None:
     tile = torch.empty((pt.rows, pt.width, 3), dtype=torch.float32, device=dev)
     barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(args.steps * passes_per_step):
         pt.render_pass(it, stream)
         it += spp
     # single RCCL gather of the framebuffer tiles to rank 0
@@ -282,7 +364,7 @@ def main() -> None:
     # Kernel-level timing for the roofline: a profiled segment of the same workload right after
     # the timed region (HIP events bracket every launch on its stream; events inside the timed
     # region would add inter-kernel gaps to `value`).
-    prof_passes = min(args.steps, 50)
+    prof_passes = min(args.steps * passes_per_step, 50)
     pt.profile(True)
     pt.profile_read()
     sp0 = pt.stats()
@@ -295,7 +377,6 @@ def main() -> None:
 
     seg = s1["segments"] - s0["segments"]
     live = [b - a for a, b in zip(s0["bounce_live"], s1["bounce_live"])]
-    emit = [b - a for a, b in zip(s0["bounce_emit"], s1["bounce_emit"])]
     t_max = elapsed
     seg_all = seg
     if dist is not None:
@@ -304,6 +385,7 @@ def main() -> None:
 
     # roofline of the dominant kernel (bounces >= 1), over the profiled segment
     b_ms, b_n, b_busy = prof["bounce"]
+    sorted_ = bool(gui.sortbyMaterial)
     if b_n == 0:   # material-sorted pipeline: its kernels are all profiled under "sort"
         b_ms, b_n = prof["sort"][0], max(1, prof_passes * (st_r.traceDepth - 1))
         b_busy = prof["sort"][2]   # union over both lanes (includes the first bounce's sort kernels)
@@ -313,32 +395,30 @@ def main() -> None:
     pemit = [b - a for a, b in zip(sp0["bounce_emit"], sp1["bounce_emit"])]
     seg_bounce = sum(plive[1:depth])
     mesh = scene.counts()[2] > 0
-    kernel_name = ("material-sorted pipeline (raygen/isect+hist/scan/scatter/shade/compact)" if gui.sortbyMaterial
-                   else f"k_bounce<false,{'true' if spp == 1 else 'false'},{'true' if mesh else 'false'}>")
+    kprefix = f"k_bounce<false, {'true' if spp == 1 else 'false'}, {'true' if mesh else 'false'}>"
+    kernel_name = ("material-sorted pipeline (isect+hist / scan / scatter / shade+compact)" if sorted_ else kprefix)
     kernel_min = 0
     for b in range(1, depth):
         n_out = plive[b + 1] if b + 1 < depth else 0
         kernel_min += PATH_BYTES * plive[b] + PATH_BYTES * n_out + FB_RMW_BYTES * pemit[b]
     per_launch_bytes = SEGMENT_BYTES * seg_bounce / max(b_n, 1)
     avg_ms = b_ms / max(b_n, 1)
-    # Batched passes run two lanes of iterations concurrently (pt_render_pass), so two k_bounce
-    # launches overlap: achieved = the bounce launches' algorithmic bytes over the union of their
-    # execution intervals (= per-launch bytes / average duration when launches do not overlap).
-    achieved = SEGMENT_BYTES * seg_bounce / (b_busy * 1e-3) / 1e9 if b_busy > 0 else 0.0
+    achieved = per_launch_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    lanes = 2 if (spp > 1 and os.environ.get("PT_AMD_LANES") != "1" and
+                  (sorted_ or os.environ.get("PT_PIPELINE") != "split")) else 1
     roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS,
-                "traffic": None if gui.sortbyMaterial else _traffic_from_profiles("k_bounce"),
-                "kernel": kernel_name, "avg_launch_ms": avg_ms, "launches": b_n,
-                "busy_ms": b_busy, "lanes": 2 if (spp > 1 and os.environ.get("PT_AMD_LANES") != "1" and
-                                                  (gui.sortbyMaterial or os.environ.get("PT_PIPELINE") != "split"))
-                                           else 1,
-                "achieved_definition": "184 B x segments of bounces >= 1 / union of their launch intervals",
-                # the same bytes per launch over the average launch duration: with two lanes each
-                # launch shares the GPU with the other lane's, so this understates the kernel
-                "achieved_per_launch": per_launch_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0,
+                "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                "definition": "184 B (SURVEY.md §8d) x segments per launch / HIP-event average launch duration",
+                "kernel": kernel_name, "avg_launch_ms": avg_ms, "launches": b_n, "lanes": lanes,
                 "segments_per_launch": seg_bounce / max(b_n, 1),
                 "algorithmic_bytes_per_launch": per_launch_bytes,
-                "kernel_min_bytes_per_launch": kernel_min / max(b_n, 1)}
+                "kernel_min_bytes_per_launch": kernel_min / max(b_n, 1),
+                # two lanes' launches overlap: the same bytes over the union of the launch intervals
+                "aggregate": {"busy_ms": b_busy,
+                              "achieved": SEGMENT_BYTES * seg_bounce / (b_busy * 1e-3) / 1e9 if b_busy > 0 else 0.0,
+                              "frac": SEGMENT_BYTES * seg_bounce / (b_busy * 1e-3) / 1e9 / HBM_PEAK_GBS
+                              if b_busy > 0 else 0.0,
+                              "definition": "184 B x segments of bounces >= 1 / union of their launch intervals"}}
 
     result = None
     if rank == 0:
@@ -346,6 +426,12 @@ def main() -> None:
             full = D.assemble([t.cpu().numpy() for t in rows_all], scene.camera().res[1], world)
             assert np.isfinite(full).all()
         value = seg_all / t_max / 1e6
+        strong = args.scaling == "strong"
+        desc = (f"cornell.json 800x800 DEPTH 8 default flags; a step = {args.samples} samples per pixel of the whole "
+                f"image, split over the GPUs by rows (each rank: {passes_per_step} pass(es) of {spp} iterations of "
+                f"its rows y%N==rank; bit-identical to one iteration per pass); fused bounce kernel" if strong else
+                f"cornell.json 800x800 DEPTH 8 default flags; a step = one pass of {spp} iteration(s) of the rank's "
+                f"rows y%N==rank per GPU (bit-identical to one iteration per pass); fused bounce kernel")
         result = {
             "metric": METRIC,
             "value": value,
@@ -355,21 +441,20 @@ def main() -> None:
             "warmup": args.warmup,
             "ms_per_step": t_max / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (bundled cornell.json scene; camera rays generated on device)" if workload is None
                     else "synthetic (generated scene, cuda_pathtracer_amd/scenes.py; camera rays generated on device)",
-            "config": {"workload": workload or (f"cornell.json 800x800 DEPTH 8 default flags; a step = one render pass "
-                                                f"of {max(1, args.spp)} iteration(s) per GPU-share (rows y%N==rank, "
-                                                f"{max(1, args.spp)}*N samples per pixel of those rows; bit-identical "
-                                                f"to one iteration per pass); fused bounce kernel"),
+            "config": {"workload": workload or desc,
                        "scene": Path(scene_path).name, "resolution": list(scene.camera().res), "depth": depth,
-                       "spp_per_step": spp, "paths_per_gpu_per_step": pt.npaths,
-                       "parallelism": f"pixel-tile x{world} + RCCL gather"},
+                       "samples_per_step": (args.samples if strong else spp * world),
+                       "iterations_per_pass": spp, "passes_per_step": passes_per_step,
+                       "paths_per_gpu_per_pass": pt.npaths,
+                       "parallelism": f"pixel rows x{world} + RCCL gather"},
             "roofline": roofline,
             "segments": seg_all,
-            "bounce_live_per_pass": [x / args.steps for x in live],
+            "bounce_live_per_step": [x / args.steps for x in live],
             "first_bounce_avg_ms": f_ms / max(f_n, 1),
         }
         if not args.no_scan:
@@ -380,12 +465,20 @@ def main() -> None:
             # labelled multithreaded variant: 16 host threads (the box's CPU share per GPU)
             result["cpu_baseline_mt"] = cpu_baseline_render_mt(args.cpu_seconds / 2, min(16, os.cpu_count() or 1))
             result["cpu_baseline_scan"] = cpu_baseline_scan()
+            result["cpu_baseline_scan_2e28"] = cpu_baseline_scan(1 << 28, 3)
+            result["cpu_baseline_compact"] = cpu_baseline_compact()
         else:
             result["cpu_baseline"] = None
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
     pt.free()
+    if rank == 0 and world == 1 and not args.no_pmc:
+        try:
+            extra = _pmc_leg(args, scene_path, spp, sorted_, avg_ms, kprefix, seg_bounce / max(b_n, 1), b_busy, b_n)
+        except Exception as e:   # profiling is evidence, not the measurement: never fail the bench line
+            extra = {"pmc_error": repr(e)}
+        roofline.update(extra)
     if rank == 0:
         print(json.dumps(result), flush=True)
 

@@ -95,6 +95,8 @@ SIGNATURES = {
     "sc_efficient_compact": (_I, [C.c_int, _P, _P, _IP]),
     "sc_timer_gpu_ms": (C.c_float, []),
     "sc_set_tile_schedule": (_I, [_I]),
+    "sc_workspace_check": (_I, [_P]),
+    "sc_workspace_error_word": (_P, [_P]),
     # pt_amd.h
     "pt_last_error": (C.c_char_p, []),
     "pt_flags_default": (None, [C.POINTER(Flags)]),

@@ -110,10 +110,26 @@ def build_cpp_tests(verbose: bool = False, force: bool = False) -> list[Path]:
     return outs
 
 
+PIN_DIR = ROOT / "tests" / "pin"
+PIN_LIB = PIN_DIR / "build" / "libthrust_pin.so"
+
+
+def build_pin(verbose: bool = False, force: bool = False) -> Path:
+    """Test infrastructure: rocThrust (system ROCm, not reference code) behind a small C ABI, to pin
+    the oracle's restatement of the reference's Thrust calls (tests/pin/thrust_pin.hip)."""
+    src = PIN_DIR / "thrust_pin.hip"
+    PIN_LIB.parent.mkdir(exist_ok=True)
+    if force or _stale(PIN_LIB, [src]):
+        _run([HIPCC, "-x", "hip", f"--offload-arch={ARCH}", "-O2", "-std=c++17", "-fPIC", "-shared",
+              "-ffp-contract=off", "-o", str(PIN_LIB), str(src)], verbose)
+    return PIN_LIB
+
+
 def build_all(verbose: bool = False, force: bool = False) -> None:
     build_native(verbose, force)
     build_oracle(verbose, force)
     build_cpp_tests(verbose, force)
+    build_pin(verbose, force)
 
 
 if __name__ == "__main__":

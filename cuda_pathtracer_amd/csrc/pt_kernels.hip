@@ -1335,6 +1335,7 @@ struct SortArgs {
     int32_t* perm;     // [P] sorted position -> physical index
     int32_t* tbase;    // [spp + 1] first histogram tile of each iteration (this bounce)
     int32_t* ibase;    // [spp + 1] first logical path of each iteration (this bounce)
+    const uint32_t* scan_err;   // the library scan's error word (sc_workspace_error_word), or null
 };
 
 // Thread t < spp: s_tb = exclusive scan of the iterations' 64-path tile counts (s_tb[spp] = all).
@@ -1460,6 +1461,9 @@ __global__ __launch_bounds__(kBlock) void k_sort_scatter(const KArgs A, const So
     const int tid = threadIdx.x, lane = tid & 63;
     const int spp = A.tile.spp;
     for (int j = tid; j <= spp; j += kBlock) { s_ib[j] = SA.ibase[j]; s_tb[j] = SA.tbase[j]; }
+    // a stalled library scan (static schedule on a shared GPU) left invalid offsets: report it
+    // through DevStats::err, which pt_stats turns into PT_ERR_DEVICE
+    if (SA.scan_err && blockIdx.x == 0 && tid == 0 && *SA.scan_err) atomicOr(&A.stats->err, 2u);
     __syncthreads();
     const int T = s_tb[spp];
     const int nmats = A.S.nmats;
@@ -2431,7 +2435,9 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
         else hipLaunchKernelGGL((k_sort_isect<false, false>), dim3(g64), dim3(kBlock), 0, s, a, sa);
         HIP_TRY(hipGetLastError());
         int32_t* offs = const_cast<int32_t*>(sa.offs);
-        if (laned) {
+        SortArgs sx = sa;
+        sx.scan_err = nullptr;
+        if (laned || c->flags.shared_gpu) {   // no co-residency needed (another lane or process may hold CUs)
             const int tiles = (int)((hn + kHistTile - 1) / kHistTile);
             uint32_t* sums = static_cast<uint32_t*>(ws);   // tiles words (the workspace holds >= hn)
             hipLaunchKernelGGL(k_hist_sums, dim3(tiles), dim3(kBlock), 0, s, (const int32_t*)sa.hist, hn, sums);
@@ -2439,13 +2445,15 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
             hipLaunchKernelGGL(k_hist_apply, dim3(tiles), dim3(kBlock), 0, s, (const int32_t*)sa.hist, offs, hn,
                                (const uint32_t*)sums);
             HIP_TRY(hipGetLastError());
-        } else if (sc_scan_exclusive_i32(sa.hist, offs, hn, ws, s) != SC_OK) {
-            return pt::fail(PT_ERR_HIP, std::string("material scan: ") + sc_last_error());
+        } else {
+            if (sc_scan_exclusive_i32(sa.hist, offs, hn, ws, s) != SC_OK)
+                return pt::fail(PT_ERR_HIP, std::string("material scan: ") + sc_last_error());
+            sx.scan_err = sc_workspace_error_word(ws);
         }
-        hipLaunchKernelGGL(k_sort_scatter, dim3(g64), dim3(kBlock), 0, s, a, sa);
+        hipLaunchKernelGGL(k_sort_scatter, dim3(g64), dim3(kBlock), 0, s, a, sx);
         HIP_TRY(hipGetLastError());
-        if (spp1) hipLaunchKernelGGL(k_sort_shade<true>, dim3(c->grid_bounce[0]), dim3(kBlock), 0, s, a, sa);
-        else hipLaunchKernelGGL(k_sort_shade<false>, dim3(c->grid_bounce[0]), dim3(kBlock), 0, s, a, sa);
+        if (spp1) hipLaunchKernelGGL(k_sort_shade<true>, dim3(c->grid_bounce[0]), dim3(kBlock), 0, s, a, sx);
+        else hipLaunchKernelGGL(k_sort_shade<false>, dim3(c->grid_bounce[0]), dim3(kBlock), 0, s, a, sx);
         HIP_TRY(hipGetLastError());
         return prof_end(ev, s);
     };
@@ -2465,9 +2473,9 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
         L[1].count_pass = 0;
         L[1].hit.uv = c->lsort.uv;
         L[1].ibase = c->lsort.ibase;
-        const SortArgs SL[2] = {{c->keys, c->phys, c->hist, c->offs, c->perm, c->tbase, A.ibase},
+        const SortArgs SL[2] = {{c->keys, c->phys, c->hist, c->offs, c->perm, c->tbase, A.ibase, nullptr},
                                 {c->lsort.keys, c->lsort.phys, c->lsort.hist, c->lsort.offs, c->lsort.perm,
-                                 c->lsort.tbase, c->lsort.ibase}};
+                                 c->lsort.tbase, c->lsort.ibase, nullptr}};
         const int64_t lhn[2] = {c->hist_n, c->lsort.hist_n};
         void* lws[2] = {c->scan_ws, c->lsort.ws};
         const int lt64[2] = {c->max_t64, c->lsort.max_t64};
@@ -2476,6 +2484,15 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
         uint64_t* cnt[2] = {&c->compact_launches, &c->llaunches};
         HIP_TRY(hipEventRecord(c->ev_fork, st));   // after the wait for this colour half above
         HIP_TRY(hipStreamWaitEvent(c->lane_stream, c->ev_fork, 0));
+        // every exit, the error returns included, orders lane 1's queued work before later work on st
+        struct Join {
+            pt_ctx* c;
+            hipStream_t st;
+            ~Join() {
+                (void)hipEventRecord(c->ev_join, c->lane_stream);
+                (void)hipStreamWaitEvent(st, c->ev_join, 0);
+            }
+        } join{c, st};
         int lcur[2] = {0, 0};
         for (int b = 0; b < c->depth; ++b)
             for (int l = 0; l < 2; ++l) {
@@ -2494,8 +2511,6 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
                 ++*cnt[l];
                 lcur[l] ^= 1;
             }
-        HIP_TRY(hipEventRecord(c->ev_join, c->lane_stream));
-        HIP_TRY(hipStreamWaitEvent(st, c->ev_join, 0));
     }
     for (int b = 0; b < c->depth && !laned; ++b) {
         const bool last = b == c->depth - 1;   // every path is dead after the last bounce
@@ -2522,7 +2537,7 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
                 cur ^= 1;
             }
         } else {
-            const SortArgs SA{c->keys, c->phys, c->hist, c->offs, c->perm, c->tbase, A.ibase};
+            const SortArgs SA{c->keys, c->phys, c->hist, c->offs, c->perm, c->tbase, A.ibase, nullptr};
             if ((rc = sort_bounce(A, SA, c->hist_n, c->scan_ws, c->max_t64, st, b))) return rc;
             ++c->compact_launches;
             cur ^= 1;
@@ -2633,7 +2648,10 @@ int pt_stats(pt_ctx* c, pt_stats_t* out) {
     }
     out->device_error = s.err;
     out->bound_mismatch = s.bound_mismatch;
-    return s.err ? pt::fail(PT_ERR_DEVICE, "device-side look-back spin bound was hit") : PT_OK;
+    return s.err ? pt::fail(PT_ERR_DEVICE, (s.err & 2u) ? "material scan hit its look-back spin bound (GPU shared? set "
+                                                         "pt_flags.shared_gpu)"
+                                                       : "device-side look-back spin bound was hit")
+                 : PT_OK;
 }
 
 #ifdef PT_STAMPS

@@ -47,6 +47,14 @@ std::atomic<bool> g_schedule_claimed{[] {
     return v && std::strcmp(v, "claim") == 0;
 }()};
 
+// Test hook (tests/test_scan_gpu.py): PT_AMD_TEST_SCAN_OVERSUB=k launches the look-back kernels on
+// k x the co-resident grid, so the static schedule stalls and must report its spin bound.
+const int g_test_oversub = [] {
+    const char* v = std::getenv("PT_AMD_TEST_SCAN_OVERSUB");
+    const int k = v ? std::atoi(v) : 1;
+    return k >= 1 && k <= 16 ? k : 1;
+}();
+
 int fail(int code, const std::string& msg) { g_err = msg; return code; }
 int hip_fail(hipError_t e, const char* where) {
     return fail(SC_ERR_HIP, std::string(where) + ": " + hipGetErrorString(e));
@@ -540,11 +548,11 @@ int launch(const int32_t* d_in, int32_t* d_out, int64_t n, int64_t* d_count, voi
     const bool aligned = ((reinterpret_cast<uintptr_t>(d_in) | reinterpret_cast<uintptr_t>(d_out)) & 15) == 0;
     const bool claimed = g_schedule_claimed.load(std::memory_order_relaxed);
     if (aligned) {
-        const int g = (int)std::min<int64_t>(tiles, resident_grid((const void*)k_scan_lag<MODE>));
+        const int g = (int)std::min<int64_t>(tiles, resident_grid((const void*)k_scan_lag<MODE>) * g_test_oversub);
         hipLaunchKernelGGL((k_scan_lag<MODE>), dim3(g), dim3(kThreads), 0, stream, d_in, d_out, n, status, ctl,
                            d_count, dead, (int)claimed);
     } else {
-        const int g = (int)std::min<int64_t>(tiles, resident_grid((const void*)k_scan_tiles<MODE>));
+        const int g = (int)std::min<int64_t>(tiles, resident_grid((const void*)k_scan_tiles<MODE>) * g_test_oversub);
         hipLaunchKernelGGL((k_scan_tiles<MODE>), dim3(g), dim3(kThreads), 0, stream, d_in, d_out, n, status, ctl,
                            d_count, dead, (int)claimed);
     }
@@ -557,6 +565,18 @@ int launch(const int32_t* d_in, int32_t* d_out, int64_t n, int64_t* d_count, voi
         e = hipGetLastError();
         if (e != hipSuccess) return hip_fail(e, "k_append_dead launch");
     }
+    return SC_OK;
+}
+
+// The device error word of a workspace (ctl[1]): set by a look-back / window-sum wait that hit its
+// spin bound (lookback.h), i.e. the static schedule's grid was not co-resident.  Each launch
+// re-zeroes it, so it reports the most recent call on that workspace.  Caller has synchronised.
+int read_ws_error(const void* ws) {
+    uint32_t err = 0;
+    hipError_t e = hipMemcpy(&err, static_cast<const uint8_t*>(ws) + sizeof(uint32_t), sizeof err, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return hip_fail(e, "hipMemcpy(workspace error word)");
+    if (err) return fail(SC_ERR_HIP, "look-back spin bound hit: the scan grid was not co-resident (GPU shared? use "
+                                     "sc_set_tile_schedule(1)); results of that call are invalid");
     return SC_OK;
 }
 
@@ -615,6 +635,7 @@ int host_op(int n, int* odata, const int* idata, int* count_out) {
     (void)hipEventRecord(b->ev1, nullptr);
     if ((e = hipEventSynchronize(b->ev1)) != hipSuccess) return hip_fail(e, "hipEventSynchronize");
     (void)hipEventElapsedTime(&g_timer_ms, b->ev0, b->ev1);
+    if ((rc = read_ws_error(ws))) return rc;
     int64_t cnt = n;
     if (MODE != kScan) {
         if ((e = hipMemcpy(&cnt, b->cnt, sizeof cnt, hipMemcpyDeviceToHost)) != hipSuccess)
@@ -662,6 +683,25 @@ int sc_efficient_compact(int n, int* odata, const int* idata, int* count_out) {
 }
 
 float sc_timer_gpu_ms(void) { return g_timer_ms; }
+
+int sc_workspace_check(const void* workspace) {
+    void* ws = const_cast<void*>(workspace);
+    if (!ws) {
+        int dev = 0;
+        hipError_t e = hipGetDevice(&dev);
+        if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
+        std::lock_guard<std::mutex> lk(g_ws_mu);
+        if ((int)g_ws.size() <= dev || !g_ws[dev].ptr) return SC_OK;   // never used
+        ws = g_ws[dev].ptr;
+    }
+    hipError_t e = hipDeviceSynchronize();
+    if (e != hipSuccess) return hip_fail(e, "hipDeviceSynchronize");
+    return read_ws_error(ws);
+}
+
+const uint32_t* sc_workspace_error_word(const void* workspace) {
+    return reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(workspace) + sizeof(uint32_t));
+}
 
 int sc_set_tile_schedule(int32_t claimed) {
     g_schedule_claimed.store(claimed != 0, std::memory_order_relaxed);

@@ -65,10 +65,12 @@ typedef struct pt_flags {
      * unchanged unless rounding moves a triangle's computed t by more than the margin
      * (DESIGN.md §4). */
     int32_t bvh_cull;
-    /* Tile schedule of the look-back kernels (lookback.h): 0 = static co-resident grid (fastest;
-     * a launch that cannot get the whole GPU reports PT_ERR_DEVICE), 1 = tiles claimed in order
-     * from a ticket (correct when other kernels or processes share the GPU; ~2x slower bounce
-     * kernels).  pt_flags_default: 1 if PT_AMD_SCHEDULE=claim is set, else 0. */
+    /* Another context, stream or process shares the GPU (0 = no).  1 makes every inter-workgroup
+     * wait of a render pass safe without co-residency: the split pipeline's look-back compaction
+     * claims tiles in order from a ticket (lookback.h), and the material-sorted pipeline scans its
+     * histogram with the three-kernel reduce/scan/apply path instead of the single-pass library
+     * scan.  With 0, a static-schedule wait that cannot get the whole GPU hits its spin bound and
+     * pt_stats reports PT_ERR_DEVICE.  pt_flags_default: 1 if PT_AMD_SCHEDULE=claim, else 0. */
     int32_t shared_gpu;
     /* Extension (default 0 = the reference): key the shading RNG by the path's global pixel index
      * instead of its position in the compacted path array (pathtrace.cu:315).  The image then

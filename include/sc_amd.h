@@ -73,9 +73,21 @@ int sc_partition_indices(const int32_t* d_flags, int32_t* d_idx, int64_t n, int3
 int sc_efficient_scan(int n, int* odata, const int* idata);
 int sc_efficient_compact(int n, int* odata, const int* idata, int* count_out);
 
+/* The device-pointer entry points are asynchronous, so a look-back stall (static schedule on a
+ * GPU shared with other work: the grid is not co-resident, a wait hits its spin bound and the
+ * grid drains with invalid results) is reported here: synchronises the device and returns
+ * SC_ERR_HIP if the most recent call that used `workspace` (NULL: the cached per-device one) hit
+ * the bound, SC_OK otherwise.  The host-pointer helpers check this themselves. */
+int sc_workspace_check(const void* workspace);
+
+/* Device address of `workspace`'s error word (uint32, non-zero after a stall), for callers that
+ * fold it into their own device-side status without a host round trip (the renderer does). */
+const uint32_t* sc_workspace_error_word(const void* workspace);
+
 /* Tile schedule of the look-back kernels (process-wide).  0 (default, fastest): a static
  * assignment over a grid that must be fully resident — if another kernel or process holds part of
- * the GPU the call fails with SC_ERR_HIP-level "look-back spin bound" instead of hanging.
+ * the GPU the call stalls until a bounded spin gives up (~0.25 s) and sc_workspace_check reports
+ * SC_ERR_HIP ("look-back spin bound") instead of hanging.
  * 1: tiles claimed in order from a ticket — correct whatever else runs on the GPU, ~15% slower.
  * The environment variable PT_AMD_SCHEDULE=claim selects 1 at load time. */
 int sc_set_tile_schedule(int32_t claimed);

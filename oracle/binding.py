@@ -81,6 +81,8 @@ def lib() -> C.CDLL:
         L.oracle_time_scan_ms.restype = C.c_double
         L.oracle_time_compact_ms.argtypes = [I64, P, P, C.c_int, C.POINTER(I64)]
         L.oracle_time_compact_ms.restype = C.c_double
+        L.oracle_time_compact_without_scan_ms.argtypes = [I64, P, P, C.c_int, C.POINTER(I64)]
+        L.oracle_time_compact_without_scan_ms.restype = C.c_double
         L.oracle_sincos.argtypes = [C.c_float, C.POINTER(C.c_float), C.POINTER(C.c_float)]
         L.oracle_u01_sequence.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_float)]
         L.oracle_u01_sequence.restype = C.c_float
@@ -95,6 +97,8 @@ def lib() -> C.CDLL:
                                     P, C.c_int, P, C.c_int, P, C.c_int,
                                     C.POINTER(OCamera), C.c_int, C.POINTER(OFlags), C.c_int, C.c_int, P, P]
         L.oracle_render.restype = C.c_double
+        L.oracle_set_tap.argtypes = [C.c_int, P, P, C.c_int]
+        L.oracle_tap_count.restype = C.c_int
         L.oracle_tonemap.argtypes = [P, C.c_int, C.c_int, C.c_float, P]
         L.oracle_preview.argtypes = [P, C.c_int, C.c_int, C.c_int, P]
         L.oracle_load_obj.argtypes = [C.c_char_p, P, P, C.c_int, P, C.c_int, P, P]
@@ -297,6 +301,22 @@ def render_pass(sc: OracleScene, fl: OFlags, iter_first: int, spp: int = 1, rank
                              C.byref(sc.cam), d, C.byref(fl), iter_first, spp, rank, world,
                              image.ctypes.data, live.ctypes.data)
     return image, [int(x) for x in live[:d]]
+
+
+def bounce_records(sc: OracleScene, fl: OFlags, iteration: int, bounce: int):
+    """Real per-bounce records of a one-iteration render: the material key of every live path as
+    computeIntersections leaves it (before the material sort) and its remainingBounces after
+    shading (before the compaction).  Test input for pinning sort/partition against rocThrust."""
+    cap = sc.cam.res[0] * sc.cam.res[1]
+    keys = np.zeros(cap, np.int32)
+    rem = np.zeros(cap, np.int32)
+    lib().oracle_set_tap(bounce, keys.ctypes.data, rem.ctypes.data, cap)
+    try:
+        render_pass(sc, fl, iteration)
+        n = lib().oracle_tap_count()
+    finally:
+        lib().oracle_set_tap(-1, None, None, 0)
+    return keys[:n].copy(), rem[:n].copy()
 
 
 def render(sc: OracleScene, fl: OFlags, iters: int, iter_first: int = 1):

@@ -695,6 +695,24 @@ void oracle_camera(int resx, int resy, float fovy, const float* eye, const float
 // accumulator (npix_tile x float3, tile-local row-major), updated in place.  `bounce_live`
 // (optional, depth entries) accumulates the live-path count entering each bounce.
 // Per pixel, contributions are added in sample order (as `spp` sequential iterations would).
+// Test tap (tests/test_pin_*.py): the material keys of bounce `bounce` as computeIntersections
+// leaves them (before the sort, pathtrace.cu:470-491) and the survivor flags as shadeMaterials
+// leaves them (remainingBounces > 0, before the compaction, pathtrace.cu:495-505) — real inputs
+// for pinning the sort and partition semantics against rocThrust.
+struct Tap {
+    int bounce = -1, cap = 0, n = 0;
+    int32_t *keys = nullptr, *flags = nullptr;
+};
+static Tap g_tap;
+void oracle_set_tap(int bounce, int32_t* keys, int32_t* flags, int cap) {
+    g_tap = Tap{};
+    g_tap.bounce = bounce;
+    g_tap.keys = keys;
+    g_tap.flags = flags;
+    g_tap.cap = cap;
+}
+int oracle_tap_count() { return g_tap.n; }
+
 int oracle_render_pass(const OGeom* geoms, int ngeoms, const OMaterial* mats, int nmats,
                        const OTriangle* tris, int ntris, const ONode* nodes, int nnodes,
                        const OTexture* texs, int ntexs,
@@ -723,6 +741,11 @@ int oracle_render_pass(const OGeom* geoms, int ngeoms, const OMaterial* mats, in
         if (bounce_live && bounce < depth) bounce_live[bounce] += (uint64_t)N;
         std::memset(isect.data(), 0, sizeof(Isect) * (size_t)P);          // pathtrace.cu:466
         for (int i = 0; i < N; ++i) compute_isect(sc, *fl, paths[i].o, paths[i].d, isect[i]);
+        const bool tap = bounce == g_tap.bounce && N <= g_tap.cap;
+        if (tap) {
+            g_tap.n = N;
+            for (int i = 0; i < N; ++i) g_tap.keys[i] = isect[i].mat;
+        }
         if (fl->sort_by_material) {                                          // pathtrace.cu:479-491
             std::vector<int> ord((size_t)N);
             for (int i = 0; i < N; ++i) ord[i] = i;
@@ -743,6 +766,8 @@ int oracle_render_pass(const OGeom* geoms, int ngeoms, const OMaterial* mats, in
         }
         // relocate_terminated_paths (pathtrace.cu:377-407) == thrust::stable_partition here
         for (int i = 0; i < N; ++i) flags[i] = paths[i].remaining == 0 ? 0 : 1;
+        if (tap)
+            for (int i = 0; i < N; ++i) g_tap.flags[i] = paths[i].remaining;
         int live = 0;
         {
             std::vector<int32_t> keep(flags.begin(), flags.begin() + N), pos((size_t)N);

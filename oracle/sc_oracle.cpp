@@ -79,10 +79,19 @@ double oracle_time_scan_ms(int64_t n, const int32_t* in, int32_t* out, int reps)
     return std::chrono::duration<double, std::milli>(t1 - t0).count();
 }
 
+// CPU::compactWithScan (with_scan != 0) or CPU::compactWithoutScan, timed the same way.
 double oracle_time_compact_ms(int64_t n, const int32_t* in, int32_t* out, int reps, int64_t* count) {
     auto t0 = std::chrono::high_resolution_clock::now();
     int64_t c = 0;
     for (int r = 0; r < reps; ++r) c = oracle_compact_with_scan(n, out, in);
+    auto t1 = std::chrono::high_resolution_clock::now();
+    if (count) *count = c;
+    return std::chrono::duration<double, std::milli>(t1 - t0).count();
+}
+double oracle_time_compact_without_scan_ms(int64_t n, const int32_t* in, int32_t* out, int reps, int64_t* count) {
+    auto t0 = std::chrono::high_resolution_clock::now();
+    int64_t c = 0;
+    for (int r = 0; r < reps; ++r) c = oracle_compact_without_scan(n, out, in);
     auto t1 = std::chrono::high_resolution_clock::now();
     if (count) *count = c;
     return std::chrono::duration<double, std::milli>(t1 - t0).count();

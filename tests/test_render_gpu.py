@@ -360,27 +360,37 @@ def test_config_scenes_bitexact(config_scenes, name, kw):
     assert r.sum() > 0
 
 
-def test_concurrent_contexts_on_two_streams(cornell_path, room_path):
+@pytest.mark.parametrize("spp,kw", [(4, dict()), (1, dict(sortbyMaterial=True)), (1, dict(useThrustPartition=True))])
+def test_concurrent_contexts_on_two_streams(cornell_path, room_path, spp, kw):
     """Two render contexts in flight at once on separate streams (each bounce kernel sized to
-    fill the GPU), in the claimed tile schedule (pt_flags.shared_gpu): both stay bit-exact —
-    claiming tiles in order makes the look-back independent of co-residency."""
+    fill the GPU) with pt_flags.shared_gpu: both stay bit-exact and report no device error.  The
+    split pipeline's look-back claims tiles in order; the sorted pipeline at spp=1 (one lane, which
+    otherwise takes the single-pass library scan that needs its grid co-resident) scans its material
+    histogram with the co-residency-free reduce/scan/apply kernels."""
+    import os
     import torch
     from cuda_pathtracer_amd import PathTracer
-    s1, o1 = _pair(cornell_path, (96, 96))
-    s2, o2 = _room_pair(room_path, (64, 64))
-    p1, p2 = PathTracer(s1, _gui(sharedGPU=True), spp=4), PathTracer(s2, _gui(sharedGPU=True), spp=4)
+    if kw.get("useThrustPartition"):
+        os.environ["PT_PIPELINE"] = "split"
+    try:
+        s1, o1 = _pair(cornell_path, (96, 96))
+        s2, o2 = _room_pair(room_path, (64, 64))
+        p1 = PathTracer(s1, _gui(sharedGPU=True, **kw), spp=spp)
+        p2 = PathTracer(s2, _gui(sharedGPU=True, **kw), spp=spp)
+    finally:
+        os.environ.pop("PT_PIPELINE", None)
     st1, st2 = torch.cuda.Stream(), torch.cuda.Stream()
     for k in range(3):
-        p1.render_pass(1 + 4 * k, st1)
-        p2.render_pass(1 + 4 * k, st2)
+        p1.render_pass(1 + spp * k, st1)
+        p2.render_pass(1 + spp * k, st2)
     torch.cuda.synchronize()
     g1, g2 = p1.image(), p2.image()
-    assert p1.stats()["passes"] == 3 and p2.stats()["passes"] == 3
+    assert p1.stats()["passes"] == 3 and p2.stats()["passes"] == 3   # pt_stats raises on a device error
     p1.free(); p2.free()
     r1 = r2 = None
     for k in range(3):
-        r1, _ = O.render_pass(o1, _oflags(_gui()), 1 + 4 * k, spp=4, image=r1)
-        r2, _ = O.render_pass(o2, _oflags(_gui()), 1 + 4 * k, spp=4, image=r2)
+        r1, _ = O.render_pass(o1, _oflags(_gui(**kw)), 1 + spp * k, spp=spp, image=r1)
+        r2, _ = O.render_pass(o2, _oflags(_gui(**kw)), 1 + spp * k, spp=spp, image=r2)
     _assert_bitexact(g1, r1, "cornell on stream 1")
     _assert_bitexact(g2, r2, "room on stream 2")
 
@@ -529,3 +539,39 @@ def test_two_lanes_equal_one_lane(cornell_path, monkeypatch, spp):
         pt.free()
     _assert_bitexact(out[0][0], out[1][0], f"two lanes vs one, spp {spp}")
     assert out[0][1:] == out[1][1:]
+
+
+@pytest.mark.parametrize("spp", [1, 2])
+def test_config3_full_size_sorted_bitexact(cornell_path, tmp_path, spp):
+    """BASELINE.json config 3 at its full size — cornell geometry at 1920x1080, DEPTH 16,
+    material-sorted shading — GPU == oracle bit for bit over `spp` iterations in one pass.  spp=1
+    takes the one-lane path with the single-pass library scan of the material histogram; spp=2 the
+    two-lane path, whose histogram (5 materials x 32400 tiles per lane) spans ~40 tiles of the
+    reduce/scan/apply kernels, exercising the cross-tile carry."""
+    from cuda_pathtracer_amd import Scene, scenes
+    path = scenes.cornell_hd(tmp_path, res=(1920, 1080), depth=16)
+    g, r, st, live = _run(Scene(path), O.OracleScene.from_json(path), _gui(sortbyMaterial=True), iters=spp, spp=spp)
+    _assert_bitexact(g, r, f"config 3 full size spp={spp}")
+    assert st["bounce_live"] == live and live[0] == spp * 1920 * 1080
+
+
+def test_sorted_multitile_histogram_scan(cornell_path):
+    """Two-lane sorted passes with a histogram of nmats x (P/2)/64 = 5 x 1875 > 4096 entries per lane
+    (several tiles of k_hist_sums / k_hist_scan_sums / k_hist_apply, multi-element threads in the
+    one-workgroup scan of the tile sums): bit-exact over two passes."""
+    s, o = _pair(cornell_path, (200, 150))
+    g, r, st, live = _run(s, o, _gui(sortbyMaterial=True), iters=16, spp=8)
+    _assert_bitexact(g, r, "sorted 200x150 spp=8")
+    assert st["bounce_live"] == live
+
+
+@pytest.mark.parametrize("kw", [dict(), dict(sortbyMaterial=True)])
+def test_config5_100k_triangles_bitexact(tmp_path, kw):
+    """BASELINE.json config 5's geometry at full size — 100k random triangles through OBJ + SAH BVH
+    (depth-22 tree, child-pair layout, LDS stack), DEPTH 32 — at a reduced resolution: GPU == oracle
+    bit for bit (the benchmarked tree itself, not the 3000-triangle parity scene)."""
+    from cuda_pathtracer_amd import Scene, scenes
+    path = scenes.random_triangles(tmp_path, n=100_000, res=(160, 90), depth=32)
+    g, r, st, live = _run(Scene(path), O.OracleScene.from_json(path), _gui(**kw), iters=2, spp=2)
+    _assert_bitexact(g, r, f"config 5 100k triangles {kw}")
+    assert st["bounce_live"] == live and r.sum() > 0
