@@ -139,6 +139,7 @@ SIGNATURES = {
     "pt_save_hdr": (_I, [C.c_char_p, _P, _I, _I, _F]),
     "pt_encode_hdr": (_I, [_P, _I, _I, _F, _P, C.c_int64, _P]),
     "pt_set_accum": (_I, [_P, _P]),
+    "pt_decode_jpeg": (_I, [C.c_char_p, C.c_int64, _IP, _IP, _IP, _P, C.c_int64]),
 }
 
 _lib = None

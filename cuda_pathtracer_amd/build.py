@@ -27,7 +27,7 @@ ARCH = "gfx950"
 # correctly-rounded operations unless the source writes fmaf(); keeps GPU == oracle bitwise.
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall", "-Wno-unused-function"]
 DEVICE_SRCS = ["sc_kernels.hip", "pt_kernels.hip"]
-HOST_SRCS = ["pt_scene.cpp", "pt_mesh.cpp", "pt_image.cpp"]
+HOST_SRCS = ["pt_scene.cpp", "pt_mesh.cpp", "pt_image.cpp", "pt_jpeg.cpp"]
 
 
 def _run(cmd: list[str], verbose: bool) -> None:

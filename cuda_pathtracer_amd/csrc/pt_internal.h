@@ -12,7 +12,7 @@ extern thread_local std::string g_err;
 int fail(int code, const std::string& msg);
 
 struct TextureHost {
-    std::string path;            // set by the JSON loader; pixels filled by pt_scene_set_texture_pixels
+    std::string path;            // TEXTURE_FILE of a JSON scene (decoded by the loader, pt_jpeg.cpp)
     int32_t width = 0, height = 0, components = 0;
     std::vector<uint8_t> pixels;
 };
@@ -42,5 +42,9 @@ int add_mesh(Scene& S, int32_t mat, const float* t, const float* r, const float*
              const float* nrm, int32_t nnrm, const float* uv, int32_t nuv, const int32_t* face_sizes, int32_t nfaces,
              const int32_t* ip, const int32_t* in, const int32_t* it, int32_t* id_out);
 int build_bvh(Scene& S);
+// JPEG textures (pt_jpeg.cpp): stbi_load(path, ..., req_comp = 0) restated
+int decode_jpeg(const uint8_t* data, size_t size, int32_t* width, int32_t* height, int32_t* components,
+                std::vector<uint8_t>* pixels);
+int load_texture_file(TextureHost& t);
 
 }  // namespace pt

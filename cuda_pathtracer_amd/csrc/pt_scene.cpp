@@ -274,7 +274,9 @@ static int load_json(Scene& S, const std::string& path) {
                 m.texture_id = (int)S.textures.size();
                 TextureHost th;
                 th.path = dir + "/Textures/" + p["TEXTURE_FILE"].string();
-                S.textures.push_back(th);
+                // Texture::load (scene.cpp:61-71): decoded here; a failure ends the load
+                if (int rc = load_texture_file(th)) return rc;
+                S.textures.push_back(std::move(th));
             }
             S.materials.push_back(m);
         }

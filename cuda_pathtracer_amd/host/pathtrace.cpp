@@ -43,15 +43,10 @@ pt_flags flags_of(const GuiDataContainer* g) {
 
 Scene::Scene(std::string filename) {
     std::printf("Reading scene from %s ...\n", filename.c_str());
+    // textures are decoded by the loader (pt_decode_jpeg: stb_image 2.06's JPEG path restated)
     check(pt_scene_load_json(filename.c_str(), &h_), "loadFromJSON");
     int32_t ng = 0, nm = 0, nt = 0, nn = 0, ntex = 0;
     check(pt_scene_counts(h_, &ng, &nm, &nt, &nn, &ntex), "counts");
-    if (ntex > 0) {
-        // The reference decodes textures with stb_image; this C++ host has no image decoder, so
-        // textured scenes go through the Python host (PIL) or pt_scene_set_texture_pixels.
-        std::fprintf(stderr, "pathtracer error: %s uses %d texture file(s); decode them and call "
-                             "pt_scene_set_texture_pixels before pathtraceInit\n", filename.c_str(), ntex);
-    }
     geoms.resize(ng);
     materials.resize(nm);
     triangles.resize(nt);

@@ -75,19 +75,21 @@ class RenderState:
     imageName: str
 
 
-def _load_texture_pixels(path: str) -> tuple[int, int, int, bytes]:
-    # The reference decodes with stb_image (scene.cpp:61-71).  Decoding is host-side I/O, not
-    # the hot path; PIL is used when present.
-    from PIL import Image as _PILImage  # noqa: N814
-    im = _PILImage.open(path)
-    if im.mode not in ("RGB", "RGBA", "L"):
-        im = im.convert("RGB")
-    comps = {"RGB": 3, "RGBA": 4, "L": 1}[im.mode]
-    return im.width, im.height, comps, im.tobytes()
+def decode_jpeg(data: bytes) -> np.ndarray:
+    """Texture::load's stbi_load(file, &w, &h, &comp, 0) (sceneStructs.h:171-175) for JPEG bytes,
+    by the native decoder (pt_decode_jpeg): an (h, w, components) uint8 array."""
+    L = lib()
+    w, h, c = C.c_int32(), C.c_int32(), C.c_int32()
+    check_pt(L.pt_decode_jpeg(data, len(data), C.byref(w), C.byref(h), C.byref(c), None, 0))
+    out = np.empty((h.value, w.value, c.value), np.uint8)
+    check_pt(L.pt_decode_jpeg(data, len(data), C.byref(w), C.byref(h), C.byref(c),
+                              out.ctypes.data_as(C.c_void_p), out.size))
+    return out
 
 
 class Scene:
-    """Scene description; `Scene(path)` loads a reference JSON scene file."""
+    """Scene description; `Scene(path)` loads a reference JSON scene file (textures decoded
+    natively, pt_decode_jpeg)."""
 
     def __init__(self, filename: str | os.PathLike | None = None):
         self._h = C.c_void_p()
@@ -96,12 +98,6 @@ class Scene:
             check_pt(L.pt_scene_create(C.byref(self._h)))
             return
         check_pt(L.pt_scene_load_json(str(filename).encode(), C.byref(self._h)))
-        _, _, _, _, ntex = self.counts()
-        buf = C.create_string_buffer(4096)
-        for t in range(ntex):
-            check_pt(L.pt_scene_texture_path(self._h, t, buf, 4096))
-            w, h, comps, data = _load_texture_pixels(buf.value.decode())
-            check_pt(L.pt_scene_set_texture_pixels(self._h, t, w, h, comps, data))
 
     def __del__(self):
         h = getattr(self, "_h", None)

@@ -160,8 +160,9 @@ int pt_scene_add_material(pt_scene* s, const pt_material* m, int32_t* id_out);
 /* Texture pixels (row-major, `components` bytes per texel; only 3 is shaded, like the reference). */
 int pt_scene_add_texture(pt_scene* s, int32_t width, int32_t height, int32_t components,
                          const uint8_t* pixels, int32_t* id_out);
-/* JSON scenes reference textures by file (scene.cpp:61-71, stb_image).  The loader records the
- * path; the host fills the decoded pixels before pt_create (pt_create fails while any is empty). */
+/* JSON scenes reference textures by file (scene.cpp:61-71).  pt_scene_load_json decodes them with
+ * pt_decode_jpeg (below) and fails with PT_ERR_IO where the reference prints "Texture load error!"
+ * and exits.  pt_scene_set_texture_pixels replaces a texture's pixels (hosts with their own decoder). */
 int pt_scene_texture_path(const pt_scene* s, int32_t id, char* buf, int32_t cap);
 int pt_scene_set_texture_pixels(pt_scene* s, int32_t id, int32_t width, int32_t height,
                                 int32_t components, const uint8_t* pixels);
@@ -229,6 +230,15 @@ int pt_profile_read(pt_ctx* c, double ms[4], uint64_t launches[4]);
  * passes of the fused pipeline run two lanes of iterations concurrently (pt_render_pass), so
  * launches of one kind overlap and busy_ms < ms. */
 int pt_profile_read_busy(pt_ctx* c, double ms[4], double busy_ms[4], uint64_t launches[4]);
+
+/* ---- texture input --------------------------------------------------------------------- */
+/* Texture::load (sceneStructs.h:171-175) = stbi_load(file, &w, &h, &comp, 0) for JPEG data:
+ * stb_image 2.06's JPEG decoder restated (baseline + progressive, its integer IDCT, triangle-filter
+ * chroma upsampling and fixed-point YCbCr->RGB), so texels equal the reference's.  Writes width,
+ * height, components (1 or 3); with out != NULL also the w*h*components interleaved bytes (top row
+ * first; cap = size of out).  out == NULL: header only. */
+int pt_decode_jpeg(const uint8_t* data, int64_t size, int32_t* width, int32_t* height, int32_t* components,
+                   uint8_t* out, int64_t cap);
 
 /* ---- image output ---------------------------------------------------------------------- */
 /* saveImage + Image::savePNG pixel math: out[3*(y*W + (W-1-x)) + k] = uchar(clamp(rgb/spp,0,1)*255). */

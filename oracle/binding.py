@@ -159,15 +159,18 @@ def camera(res, fovy, eye, lookat, up) -> OCamera:
     return cam
 
 
+_TEXTURES: dict = {}
+
+
 def load_texture(path):
-    """Decoded texels (the reference decodes with stb_image; both hosts here use PIL, so the
-    oracle and the product shade from the same bytes — JPEG decoding is not on the hot path)."""
-    from PIL import Image
-    im = Image.open(path)
-    if im.mode not in ("RGB", "RGBA", "L"):
-        im = im.convert("RGB")
-    comps = {"RGB": 3, "RGBA": 4, "L": 1}[im.mode]
-    return im.width, im.height, comps, np.frombuffer(im.tobytes(), np.uint8).copy()
+    """Decoded texels by the oracle's own restatement of stb_image 2.06's JPEG decoder
+    (oracle/jpeg_oracle.py; the reference's Texture::load, sceneStructs.h:171-175).  Cached per path."""
+    from oracle import jpeg_oracle
+    key = str(path)
+    if key not in _TEXTURES:
+        px = jpeg_oracle.load(key)
+        _TEXTURES[key] = (px.shape[1], px.shape[0], px.shape[2], np.ascontiguousarray(px).reshape(-1))
+    return _TEXTURES[key]
 
 
 class OracleScene:

@@ -45,6 +45,36 @@ def test_cli_png_matches_oracle(tmp_path, cornell_path):
     assert (np.abs(dec - ref) <= ref.max(axis=2, keepdims=True) * 2 ** -7 + 1e-30).all()
 
 
+def test_cli_room_textures_png_matches_oracle(tmp_path):
+    """The C++ host renders the textured mesh scene (room.json: three OBJ chairs + a wall mesh, two
+    JPEG textures decoded natively by pt_decode_jpeg) and its PNG equals the oracle's render, the
+    oracle shading from its own JPEG restatement's texels (oracle/jpeg_oracle.py).  Resolution
+    reduced to 160x160 so the CPU oracle stays fast; everything else as the bundled file."""
+    import json
+    scenes = ROOT / "tests" / "scenes"
+    spec = json.loads((scenes / "room.json").read_text())
+    spec["Camera"]["RES"] = [160, 160]
+    (tmp_path / "Textures").symlink_to(scenes / "Textures")
+    (tmp_path / "Models").symlink_to(scenes / "Models")
+    path = tmp_path / "room.json"
+    path.write_text(json.dumps(spec))
+    exe = ROOT / "cuda_pathtracer_amd" / "pathtracer_amd"
+    out = tmp_path / "out"
+    out.mkdir()
+    res = subprocess.run([str(exe), str(path), "--iterations", "2", "--out", str(out)], capture_output=True,
+                         text=True, timeout=300)
+    assert res.returncode == 0, res.stdout + res.stderr
+    pngs = list(out.glob("*.2samp.png"))
+    assert len(pngs) == 1, (res.stdout, list(out.iterdir()))
+    from PIL import Image
+    got = np.asarray(Image.open(pngs[0]).convert("RGB"))
+    sc = O.OracleScene.from_json(str(path))
+    img = None
+    for it in (1, 2):
+        img, _ = O.render_pass(sc, O.flags(), it, image=img)
+    np.testing.assert_array_equal(got, O.tonemap(img, 2.0))
+
+
 def test_cli_usage_and_bad_scene(tmp_path):
     exe = ROOT / "cuda_pathtracer_amd" / "pathtracer_amd"
     assert subprocess.run([str(exe)], capture_output=True, timeout=60).returncode == 1
