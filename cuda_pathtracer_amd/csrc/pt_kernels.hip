@@ -115,6 +115,10 @@ struct KArgs {
     unsigned long long* emit_slots;   // [64 bounces][emit_stride]: per-workgroup emissive counts
     int32_t emit_stride;
     int32_t count_pass;    // this launch sequence counts the pass in DevStats::passes (lane 0)
+    v4f* mhit;             // [path capacity] k_traverse -> k_bounce<.., kMeshPre>: (t, idx, bx, by)
+    uint32_t* tticket;     // k_traverse: this bounce's ray ticket (zeroed at the start of the pass)
+    int32_t refill_min;    // k_traverse: idle lanes that trigger a refill (kRefillMin; PT_AMD_REFILL)
+    int32_t stack_rows;    // k_traverse: LDS stack entries per thread (HybStack)
 };
 
 // ------------------------------------------------------------------------------------------
@@ -283,6 +287,18 @@ struct LdsStack {
     __device__ int get(int i) const { return col[i * kBlock]; }
     __device__ void set(int i, int v) const { col[i * kBlock] = v; }
 };
+// k_traverse: the first `rows` entries in LDS (column layout), the rest of the reference's 64 in a
+// private (scratch) array — deep entries are rare, and a short LDS stack keeps more waves resident.
+struct HybStack {
+    int* col;
+    int* priv;   // entries rows .. 63
+    int rows;
+    __device__ int get(int i) const { return i < rows ? col[i * kBlock] : priv[i - rows]; }
+    __device__ void set(int i, int v) const {
+        if (i < rows) col[i * kBlock] = v;
+        else priv[i - rows] = v;
+    }
+};
 struct PrivStack {
     int* a;
     __device__ int get(int i) const { return a[i]; }
@@ -351,6 +367,13 @@ __device__ __forceinline__ MeshHit bvh_walk_pairs(const SceneDev& S, f3 o, f3 d,
     return r;
 }
 
+constexpr int kWalkDone = (int)0x80000000;   // k_traverse: no node left (below every leaf code, first < 2^23)
+constexpr int kWalkNone = (int)0x80000001;   // k_traverse: stay (the leaf has triangles left)
+
+#ifdef PT_TRAV_STATS
+__device__ unsigned long long g_trav[64 * 8];   // [slot][0 rays, 1 pairs, 2 tris, 3 wave steps, 4 waves]
+#endif
+
 __device__ MeshHit bvh_traverse(const SceneDev& S, f3 o, f3 d, bool cull) {
     if (S.nnodes == 0) return MeshHit{false, -1, -1, kFLT_MAX, 0.f, 0.f};
     if (S.bvh_depth < kLdsStack) {
@@ -398,8 +421,10 @@ __device__ float mesh_linear(const SceneDev& S, const G& g, f3 o, f3 d, bool use
     return tmin;
 }
 
-template <bool MESH>
-__device__ __forceinline__ Hit intersect_scene(const SceneDev& S, const FlagsDev& fl, f3 ro, f3 rd) {
+// `pre`: the BVH closest hit of this ray, already computed by k_traverse (nullptr: traverse here).
+template <bool MESH, bool PRE = false>
+__device__ __forceinline__ Hit intersect_scene(const SceneDev& S, const FlagsDev& fl, f3 ro, f3 rd,
+                                               const MeshHit* pre = nullptr) {
     float t_min = kFLT_MAX;
     int hit_geom = -1, best_code = -1;
     f3 best_obj = F3(0, 0, 0), best_n = F3(0, 0, 0);
@@ -421,7 +446,12 @@ __device__ __forceinline__ Hit intersect_scene(const SceneDev& S, const FlagsDev
         } else if (type == PT_GEOM_SPHERE) {
             t = sphere_test(g, ro, rd, obj, outside);
         } else if (MESH && type == PT_GEOM_MESH) {
-            if (fl.bvh) {
+            if constexpr (PRE) {   // (PRE kernels run with fl.bvh set)
+                if (pre->any && pre->id >= g.tri_start && pre->id < g.tri_end) {
+                    t = pre->t;
+                    tri_attrs(S.attrs[pre->idx], pre->bx, pre->by, tmp_n, tmp_u, tmp_v);
+                }
+            } else if (fl.bvh) {
                 if (!traversed) { mh = bvh_traverse(S, ro, rd, fl.bvh_cull != 0); traversed = true; }
                 if (mh.any && mh.id >= g.tri_start && mh.id < g.tri_end) {
                     t = mh.t;
@@ -631,15 +661,25 @@ __device__ __forceinline__ float exact_geom(const LGeom& L, f3 r_o, f3 r_d, int&
     return length(r_o - ip);
 }
 
-template <bool SEL>
+// PRE: scenes with meshes whose BVH closest hit `mh` came from k_traverse.  The owning mesh geom
+// (the first in index order whose triangle range holds the hit, intersect_scene's rule) enters as an
+// exactly evaluated hit before the exact tests; mesh geoms have no bound (bkind 0).
+template <bool SEL, bool PRE = false>
 __device__ __forceinline__ Hit intersect_bounded(const SceneDev& S, const FlagsDev& fl, const LGeom* s_geoms, f3 ro,
-                                                 f3 rd) {
+                                                 f3 rd, const MeshHit* mh = nullptr) {
     const float rl = __builtin_amdgcn_sqrtf(dot(rd, rd));
     bool plain = !(rl > 0.5f && rl < 2.0f);   // NaN / degenerate direction: the plain loop
     float t_min = kFLT_MAX;
     int hit_geom = -1, best_code = -1;
     f3 best_obj = F3(0, 0, 0);
     bool best_outside = true;
+    int mesh_geom = -1;
+    if (PRE && mh->any) {
+        const auto* G = as_const(S.geoms);
+        for (int i = 0; i < S.ngeoms; ++i)
+            if (G[i].type == PT_GEOM_MESH && mh->id >= G[i].tri_start && mh->id < G[i].tri_end) { mesh_geom = i; break; }
+        if (mesh_geom >= 0 && mh->t > 0.0f) { t_min = mh->t; hit_geom = mesh_geom; }
+    }
     if (!plain) {
         // pass 1: the three smallest lower bounds (scene data wave-uniform: scalar loads)
         float lo1 = kInf, lo2 = kInf, lo3 = kInf;
@@ -700,7 +740,7 @@ __device__ __forceinline__ Hit intersect_bounded(const SceneDev& S, const FlagsD
             }
         }
     }
-    if (plain) return intersect_scene<false>(S, fl, ro, rd);
+    if (plain) return intersect_scene<PRE, PRE>(S, fl, ro, rd, mh);
     Hit h;
     if (hit_geom < 0) {
         h.t = -1.0f;
@@ -713,7 +753,8 @@ __device__ __forceinline__ Hit intersect_bounded(const SceneDev& S, const FlagsD
     h.t = t_min;
     h.mat = g.material;
     h.u = h.v = 0.f;
-    h.n = g.type == PT_GEOM_CUBE ? box_normal(g, best_code) : sphere_normal(g, best_obj, best_outside);
+    if (PRE && hit_geom == mesh_geom) tri_attrs(S.attrs[mh->idx], mh->bx, mh->by, h.n, h.u, h.v);
+    else h.n = g.type == PT_GEOM_CUBE ? box_normal(g, best_code) : sphere_normal(g, best_obj, best_outside);
     return h;
 }
 
@@ -1100,13 +1141,230 @@ __device__ __forceinline__ int seg_walk(const int32_t* s_pre, int nseg, int s, i
     return s;
 }
 
+// BVH closest hit of every live path of this bounce, ahead of k_bounce<.., kMeshPre> (which reads it
+// at the path's physical index): the divergent, latency-bound walk runs in a lean persistent kernel
+// with no barriers in its loop and a depth-sized LDS stack, instead of inside the bounce kernel's tile
+// loop (where one wave's walk held its workgroup's other three at every tile barrier, 3 waves/SIMD).
+//   Rays per path vary from zero to hundreds of steps, so a wave that walks 64 fixed rays idles most
+// lanes behind its longest ray (measured on config 5: 25% of lane slots busy).  Here a lane that
+// finishes its ray takes a new one (Aila & Laine 2009, persistent threads + dynamic fetch): when at
+// least kRefillMin lanes are idle, they take the next rays of the wave's chunk (kTravChunk rays from
+// a per-bounce ticket).  A walk is one while-while round per loop trip: descend interior pairs until
+// the lane holds a leaf, test the leaf, pop.  Per ray the sequence of boxes, pushes, pops and
+// triangles is bvh_walk_pairs's, so the hit is the reference's whatever the scheduling.
+//   Rays: first bounce, camera ray k (raygen, as k_bounce<FIRST> makes it), record k; later bounces,
+// the k-th survivor of the previous launch's segments (prefix of the segment words in LDS), record =
+// its physical slot.  Record: (t, BVH-order triangle index or -1, bx, by).
+constexpr int kMeshInline = 1;   // k_bounce MESH modes: 0 no mesh, 1 traversal inside k_bounce,
+constexpr int kMeshPre = 2;      // 2 closest mesh hit precomputed by k_traverse
+constexpr int kTravChunk = 256;  // rays per ticket grab
+constexpr int kRefillMin = 16;   // idle lanes that trigger a refill
+constexpr int kTravLdsRows = 32; // LDS stack entries per thread (HybStack; the rest in scratch)
+
+// Exclusive prefix of the previous launch's segment survivor counts into s_pre[0..nseg]; returns
+// the total.  All threads of the block call it (barriers).
+__device__ __forceinline__ int seg_prefix(const uint32_t* __restrict__ words, int nseg, int32_t* s_pre, uint32_t* s_wsum) {
+    constexpr int kPer = kMaxSeg / kBlock;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    uint32_t w[kPer], sum = 0;
+    const int s0 = tid * kPer;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        w[k] = s0 + k < nseg ? (words[s0 + k] & kSegCountMask) : 0u;
+        sum += w[k];
+    }
+    const uint32_t incl = lb::wave_inclusive_scan(sum);
+    if (lane == 63) s_wsum[wave] = incl;
+    __syncthreads();
+    uint32_t run = incl - sum;
+    for (int q = 0; q < wave; ++q) run += s_wsum[q];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        if (s0 + k <= nseg) s_pre[s0 + k] = (int32_t)run;
+        run += w[k];
+    }
+    if (tid == kBlock - 1) s_pre[kMaxSeg] = (int32_t)run;
+    __syncthreads();
+    return __builtin_amdgcn_readfirstlane(s_pre[nseg]);
+}
+
+template <bool FIRST>
+__global__ __launch_bounds__(kBlock) void k_traverse(const KArgs A) {
+    extern __shared__ int s_tstack[];   // stack_rows entries per thread, column layout
+    __shared__ int32_t s_pre[FIRST ? 1 : kMaxSeg + 1];
+    __shared__ uint32_t s_wsum[4];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const SceneDev& S = A.S;
+    int N, nseg = 0, chunk = 0;
+    if (FIRST) {
+        N = A.tile.P;
+    } else {
+        const int par = A.parity;
+        nseg = (int)A.ctl[par].nseg;
+        chunk = (int)A.ctl[par].chunk;
+        N = seg_prefix(reinterpret_cast<const uint32_t*>(A.seg) + (size_t)par * kMaxSeg, nseg, s_pre, s_wsum);
+    }
+    // ray k -> (origin, direction, record slot)
+    auto ray = [&](int k, f3& o, f3& d) -> int {
+        if (FIRST) {
+            PathReg p;
+            raygen(A.cam, A.fl, A.tile, k, p);
+            o = p.o;
+            d = p.d;
+            return k;
+        }
+        int lo = 0, hi = nseg - 1;   // segment holding survivor k: the last s with s_pre[s] <= k
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (s_pre[mid] <= k) lo = mid; else hi = mid - 1;
+        }
+        const int q = lo * chunk + (k - s_pre[lo]);
+        const v4f a = A.in.a[q], b = A.in.b[q];
+        o = F3(a[0], a[1], a[2]);
+        d = F3(a[3], b[0], b[1]);
+        return q;
+    };
+    int spill[64];   // stack entries past the LDS rows (HybStack)
+    const HybStack st{s_tstack + tid, spill, A.stack_rows};
+    // the pair walk pushes only passing children: exact while its stack never reaches the reference's
+    // 64 entries (occupancy <= bvh_depth + 1); else, and under bvh_cull, the node-at-a-time walk
+    if (!(S.pairs && !A.fl.bvh_cull && S.bvh_depth + 2 <= 64)) {
+        for (int k = (int)blockIdx.x * kBlock + tid; k < N; k += (int)gridDim.x * kBlock) {
+            f3 o, d;
+            const int q = ray(k, o, d);
+            const MeshHit r = bvh_walk(S, o, d, A.fl.bvh_cull != 0, st);
+            A.mhit[q] = v4f{r.t, __int_as_float(r.any ? r.idx : -1), r.bx, r.by};
+        }
+        return;
+    }
+    uint32_t* ticket = A.tticket;
+    // chunk size: kTravChunk, smaller when the bounce has few rays (>= 2 chunks per resident wave)
+    const int csz = min(kTravChunk, max(64, (N / (int)(gridDim.x * (kBlock / 64) * 2)) & ~63));
+    int cnext = 0, cend = 0;   // the wave's chunk of rays (wave-uniform)
+    bool exhausted = false;
+    bool have = false;         // this lane holds a ray
+    // walk state: an interior pair (cur >= 0) or a leaf's triangle range [ti, te) (leaf)
+    int q = 0, cur = 0, top = 0, ti = 0, te = 0;
+    bool leaf = false;
+    f3 o = F3(0, 0, 0), d = F3(0, 0, 0), inv = F3(0, 0, 0);
+    uint32_t negm = 0;         // bit a: d[a] < 0
+    MeshHit r{false, -1, -1, kFLT_MAX, 0.f, 0.f};
+    auto enter = [&](int code) {   // code: interior (>= 0) or leaf (< 0, != kWalkDone)
+        leaf = code < 0;
+        if (leaf) {
+            const int c = -code - 1;
+            ti = c >> 8;
+            te = ti + (c & 255);
+        } else {
+            cur = code;
+        }
+    };
+#ifdef PT_TRAV_STATS
+    uint32_t n_rays = 0, n_pairs = 0, n_tris = 0, w_trips = 0;
+#endif
+    for (;;) {
+        const uint64_t idle = __ballot(!have);
+        const int nidle = __popcll(idle);
+        if (nidle >= A.refill_min && !exhausted) {
+            if (cnext >= cend) {
+                int base = 0;
+                if (lane == 0) base = (int)atomicAdd(ticket, (uint32_t)csz);
+                base = __shfl(base, 0);
+                if (base >= N) exhausted = true;
+                else { cnext = base; cend = min(base + csz, N); }
+            }
+            if (!exhausted) {
+                const uint32_t rank =
+                    __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+                if (!have && cnext + (int)rank < cend) {
+                    q = ray(cnext + (int)rank, o, d);
+                    negm = (d.x < 0.0f ? 1u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 4u : 0u);
+                    inv = F3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+                    const float bmin[3] = {S.root_lo[0], S.root_lo[1], S.root_lo[2]};
+                    const float bmax[3] = {S.root_hi[0], S.root_hi[1], S.root_hi[2]};
+                    top = 0;
+                    r = MeshHit{false, -1, -1, kFLT_MAX, 0.f, 0.f};
+                    if (aabb_hit(bmin, bmax, o, inv)) {
+                        enter(S.root_code);
+                        have = true;
+                    } else {   // misses the whole tree
+                        A.mhit[q] = v4f{r.t, __int_as_float(-1), r.bx, r.by};
+                    }
+#ifdef PT_TRAV_STATS
+                    ++n_rays;
+#endif
+                }
+                cnext = min(cnext + nidle, cend);
+            }
+        }
+        if (__ballot(have) == 0) {   // every lane idle: done, or (rays that missed the root) refill
+            if (exhausted) break;
+            continue;
+        }
+#ifdef PT_TRAV_STATS
+        w_trips += lane == 0 ? 1u : 0u;
+#endif
+        if (have) {
+            // one memory round trip per trip for every lane: a pair (interior) or a triangle (leaf)
+            const v4f* src = leaf ? reinterpret_cast<const v4f*>(S.tris + ti) : reinterpret_cast<const v4f*>(S.pairs + (cur >> 2));
+            const v4f x0 = src[0], x1 = src[1], x2 = src[2];
+            v4f x3 = v4f{0.f, 0.f, 0.f, 0.f};
+            if (!leaf) x3 = src[3];
+            int next = kWalkNone;
+            if (leaf) {
+#ifdef PT_TRAV_STATS
+                ++n_tris;
+#endif
+                const DTri tr{x0, x1, x2};
+                float bx, by, bz;
+                if (ray_tri(tr, o, d, bx, by, bz)) {
+                    r.any = true;
+                    if (r.t == -1.0f || bz < r.t) {
+                        r.t = bz; r.bx = bx; r.by = by; r.idx = ti;
+                    }
+                }
+                if (++ti == te) next = top == 0 ? kWalkDone : st.get(--top);
+            } else {
+#ifdef PT_TRAV_STATS
+                ++n_pairs;
+#endif
+                float lo;
+                const float lmn[3] = {x0[0], x0[1], x0[2]}, lmx[3] = {x1[0], x1[1], x1[2]};
+                const float rmn[3] = {x2[0], x2[1], x2[2]}, rmx[3] = {x3[0], x3[1], x3[2]};
+                const bool hl = aabb_hit(lmn, lmx, o, inv, lo), hr = aabb_hit(rmn, rmx, o, inv, lo);
+                const int cl = __float_as_int(x0[3]), cr = __float_as_int(x2[3]);
+                const bool ng = (negm >> (cur & 3)) & 1u;   // split axis: right child first
+                const bool h1 = ng ? hr : hl, h2 = ng ? hl : hr;
+                const int c1 = ng ? cr : cl, c2 = ng ? cl : cr;
+                if (h1 && h2) st.set(top++, c2);
+                next = (h1 || h2) ? (h1 ? c1 : c2) : (top == 0 ? kWalkDone : st.get(--top));
+            }
+            if (next == kWalkDone) {
+                A.mhit[q] = v4f{r.t, __int_as_float(r.any ? r.idx : -1), r.bx, r.by};
+                have = false;
+            } else if (next != kWalkNone) {
+                enter(next);
+            }
+        }
+    }
+#ifdef PT_TRAV_STATS
+    unsigned long long* g = g_trav + (blockIdx.x & 63) * 8;
+    atomicAdd(&g[0], (unsigned long long)n_rays);
+    atomicAdd(&g[1], (unsigned long long)n_pairs);
+    atomicAdd(&g[2], (unsigned long long)n_tris);
+    atomicAdd(&g[3], (unsigned long long)w_trips);
+    atomicAdd(&g[4], lane == 0 ? 1ull : 0ull);
+#endif
+}
+
 // [raygen] -> intersect -> shade -> segmented compaction (above).
-template <bool FIRST, bool SPP1, bool MESH>
+template <bool FIRST, bool SPP1, int MESH>
 __global__ __launch_bounds__(kBlock) void k_bounce(const KArgs A) {
     // scene tables sized to the scene (dynamic LDS, bounce_lds_bytes): geom rows, then materials
     extern __shared__ __align__(16) uint8_t s_dyn[];
     LGeom* s_geoms = reinterpret_cast<LGeom*>(s_dyn);
-    DMaterial* s_mats = reinterpret_cast<DMaterial*>(s_dyn + (MESH || A.S.ngeoms > kLdsGeoms ? 0 : A.S.ngeoms) * sizeof(LGeom));
+    DMaterial* s_mats =
+        reinterpret_cast<DMaterial*>(s_dyn + (MESH == kMeshInline || A.S.ngeoms > kLdsGeoms ? 0 : A.S.ngeoms) * sizeof(LGeom));
     __shared__ int32_t s_pre[FIRST ? 1 : kMaxSeg + 1];
     __shared__ int32_t s_ib[kMaxSpp + 1];
     __shared__ uint32_t s_wc[2][4];
@@ -1144,7 +1402,7 @@ __global__ __launch_bounds__(kBlock) void k_bounce(const KArgs A) {
         A.ctl[par ^ 1].chunk = (uint32_t)chunk;
     }
     if (my_it < 0) return;
-    if (!MESH) stage_geoms(A.S, s_geoms);
+    if (MESH != kMeshInline) stage_geoms(A.S, s_geoms);
     stage_materials(A, s_mats);
     const bool lds_mats = A.S.nmats <= kLdsMats;
     count_bounce(A, N);
@@ -1172,14 +1430,29 @@ __global__ __launch_bounds__(kBlock) void k_bounce(const KArgs A) {
         PathReg p;
         STAMP(t0);
         if (i < last) {
+            int q = i;   // physical index of the path (and of its k_traverse record)
             if (FIRST) {
                 raygen_at(A.cam, A.fl, A.tile, i, my_it, i - it_base, p);   // (a workgroup holds one iteration)
             } else {
                 const int s = seg_walk(s_pre, nseg_in, seg, i);
-                load_path(A.in, s * chunk_in + (i - s_pre[s]), p);
+                q = s * chunk_in + (i - s_pre[s]);
+                load_path(A.in, q, p);
             }
             STAMP(t1);
-            const Hit h = closest_hit<MESH, false, !FIRST>(A.S, A.fl, s_geoms, p.o, p.d, &A.stats->bound_mismatch);
+            Hit h;
+            if constexpr (MESH == kMeshPre) {
+                const v4f m = A.mhit[q];
+                MeshHit mh;
+                mh.t = m[0];
+                mh.idx = __float_as_int(m[1]);
+                mh.bx = m[2];
+                mh.by = m[3];
+                mh.any = mh.idx >= 0;
+                mh.id = mh.any ? __float_as_int(A.S.tris[mh.idx].a[3]) : -1;
+                h = intersect_bounded<!FIRST, true>(A.S, A.fl, s_geoms, p.o, p.d, &mh);
+            } else {
+                h = closest_hit<MESH == kMeshInline, false, !FIRST>(A.S, A.fl, s_geoms, p.o, p.d, &A.stats->bound_mismatch);
+            }
             STAMP(t2);
             const int key = A.fl.rng_pixel ? slot_pixel(A.cam, A.tile, p.slot) : i - it_base;
             // every path entering bounce b has b bounces behind it: a wave-uniform value, so the
@@ -1766,6 +2039,13 @@ struct pt_ctx {
         int64_t hist_n = 0;
         int max_t64 = 0;
     } lsort;
+    // Mesh scenes: the BVH walk runs in k_traverse ahead of k_bounce<.., kMeshPre> (mesh_mode 2) when
+    // the BVH is on and the geom table fits LDS; otherwise inside k_bounce (kMeshInline).
+    v4f* mhit[2] = {nullptr, nullptr};   // per lane, indexed by physical path slot
+    size_t lcap[2] = {0, 0};             // path capacity of each lane's buffers
+    bool mesh_inline = false;            // PT_AMD_MESH_INLINE=1 at pt_create: always kMeshInline
+    uint32_t* tq = nullptr;              // k_traverse ray tickets: [lane][bounce], zeroed per pass
+    int grid_traverse = 0;               // k_traverse: one resident wave of workgroups
     hipStream_t fin_stream = nullptr;
     hipEvent_t ev_pass[2] = {}, ev_fin[2] = {};
     bool fin_out[2] = {false, false};
@@ -1994,19 +2274,28 @@ int resident_per_cu(const void* kernel) {
 
 // Dynamic LDS of k_bounce: the scene's geom rows (analytic scenes of <= kLdsGeoms geoms) and
 // materials (<= kLdsMats); Cornell needs 1.6 KiB instead of a fixed 12 KiB.
-size_t bounce_lds_bytes(const SceneDev& S) {
-    const int g = (S.ntris > 0 || S.ngeoms > kLdsGeoms) ? 0 : S.ngeoms;
+size_t bounce_lds_bytes(const SceneDev& S, int mesh) {
+    const int g = (mesh == kMeshInline || S.ngeoms > kLdsGeoms) ? 0 : S.ngeoms;
     const int m = std::min(S.nmats, kLdsMats);
     return (size_t)g * sizeof(LGeom) + (size_t)m * sizeof(DMaterial);
 }
 
+// k_bounce's mesh mode for the current flags (see pt_ctx::mhit).
+int mesh_mode(const pt_ctx* c) {
+    const SceneDev& S = c->args.S;
+    if (S.ntris == 0) return 0;
+    return (c->args.fl.bvh && S.nnodes > 0 && S.ngeoms <= kLdsGeoms && c->mhit[0] && !c->mesh_inline) ? kMeshPre
+                                                                                                     : kMeshInline;
+}
+
 using KernelFn = void (*)(const KArgs);
-KernelFn bounce_kernel(bool first, bool spp1, bool mesh) {
-    static const KernelFn table[8] = {
-        k_bounce<false, false, false>, k_bounce<false, false, true>, k_bounce<false, true, false>,
-        k_bounce<false, true, true>,   k_bounce<true, false, false>, k_bounce<true, false, true>,
-        k_bounce<true, true, false>,   k_bounce<true, true, true>};
-    return table[(first ? 4 : 0) + (spp1 ? 2 : 0) + (mesh ? 1 : 0)];
+KernelFn bounce_kernel(bool first, bool spp1, int mesh) {   // mesh: 0, kMeshInline, kMeshPre
+    static const KernelFn table[12] = {
+        k_bounce<false, false, 0>, k_bounce<false, false, 1>, k_bounce<false, false, 2>,
+        k_bounce<false, true, 0>,  k_bounce<false, true, 1>,  k_bounce<false, true, 2>,
+        k_bounce<true, false, 0>,  k_bounce<true, false, 1>,  k_bounce<true, false, 2>,
+        k_bounce<true, true, 0>,   k_bounce<true, true, 1>,   k_bounce<true, true, 2>};
+    return table[(first ? 6 : 0) + (spp1 ? 3 : 0) + mesh];
 }
 KernelFn trace_kernel(bool first, bool spp1, bool mesh) {
     static const KernelFn table[8] = {
@@ -2021,6 +2310,24 @@ int launch_k(pt_ctx* c, K kernel, int grid, hipStream_t st, int kind, const KArg
     ProfEv* ev;
     if (int rc = prof_begin(c, st, kind, &ev)) return rc;
     hipLaunchKernelGGL(kernel, dim3(grid), dim3(kBlock), lds, st, a);
+    HIP_TRY(hipGetLastError());
+    return prof_end(ev, st);
+}
+
+// One bounce of the fused pipeline: [k_traverse (mesh mode 2)] + k_bounce, profiled as one launch.
+// `cap`: path capacity of the lane's buffers (k_traverse's later-bounce grid covers every slot).
+int launch_bounce(pt_ctx* c, bool first, bool spp1, int mesh, hipStream_t st, const KArgs& a, size_t cap) {
+    ProfEv* ev;
+    if (int rc = prof_begin(c, st, first ? PT_KIND_FIRST_BOUNCE : PT_KIND_BOUNCE, &ev)) return rc;
+    (void)cap;
+    if (mesh == kMeshPre) {
+        const size_t lds = (size_t)a.stack_rows * kBlock * sizeof(int);
+        if (first) hipLaunchKernelGGL(k_traverse<true>, dim3(c->grid_traverse), dim3(kBlock), lds, st, a);
+        else hipLaunchKernelGGL(k_traverse<false>, dim3(c->grid_traverse), dim3(kBlock), lds, st, a);
+        HIP_TRY(hipGetLastError());
+    }
+    hipLaunchKernelGGL(bounce_kernel(first, spp1, mesh), dim3(c->grid_bounce[first]), dim3(kBlock),
+                       bounce_lds_bytes(a.S, mesh), st, a);
     HIP_TRY(hipGetLastError());
     return prof_end(ev, st);
 }
@@ -2261,8 +2568,9 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
     c->grid_compact = std::max(1, std::min((int)((P + kCompactTile - 1) / kCompactTile), cus * resident_per_cu((const void*)k_compact_paths)));
     for (int f = 0; f < 2; ++f) {   // k_bounce: any grid is correct; one full wave of equal-work
         int per_cu = 0;              // workgroups avoids a half-empty second wave
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bounce_kernel(f, sh.spp == 1, A.S.ntris > 0), kBlock,
-                                                         bounce_lds_bytes(A.S)) != hipSuccess || per_cu <= 0)
+        const int mm = A.S.ntris > 0 ? kMeshPre : 0;   // (any grid is correct for either mesh mode)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bounce_kernel(f, sh.spp == 1, mm), kBlock,
+                                                         bounce_lds_bytes(A.S, mm)) != hipSuccess || per_cu <= 0)
             per_cu = 4;
         // > 2 spp workgroups: the per-iteration layout of k_bounce needs grid - spp >= spp
         // the first bounce (raygen, 5 waves/SIMD) balances better over two waves of workgroups
@@ -2285,6 +2593,22 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
     if (int rc = path_cap(P, sh.spp, &c->path_cap)) return bail(rc);
     for (int b = 0; b < 2; ++b)
         if (int rc = alloc_paths(c, c->buf[b], c->path_cap)) return bail(rc);
+    c->lcap[0] = c->path_cap;
+    if (const char* mi = std::getenv("PT_AMD_MESH_INLINE")) c->mesh_inline = std::strcmp(mi, "1") == 0;
+    if (A.S.nnodes > 0) {   // k_traverse records (mesh mode 2), tickets, stack depth and grid
+        if (int rc = c->alloc(&c->mhit[0], c->path_cap)) return bail(rc);
+        if (int rc = c->alloc(&c->tq, 2 * 64)) return bail(rc);
+        A.stack_rows = std::min(A.S.bvh_depth + 2, kTravLdsRows);
+        if (const char* sr = std::getenv("PT_AMD_STACK_ROWS")) A.stack_rows = std::max(1, std::min(64, std::atoi(sr)));
+        int per_cu = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_traverse<false>, kBlock,
+                                                         (size_t)A.stack_rows * kBlock * sizeof(int)) != hipSuccess ||
+            per_cu <= 0)
+            per_cu = 4;
+        c->grid_traverse = cus * per_cu;
+        A.refill_min = kRefillMin;
+        if (const char* rf = std::getenv("PT_AMD_REFILL")) A.refill_min = std::max(1, std::min(64, std::atoi(rf)));
+    }
     if (int rc = c->alloc(&A.image, (size_t)npix * 3)) return bail(rc);
     if (sh.spp > 1) {
         if (int rc = c->alloc(&c->colbuf, 2 * (size_t)P)) return bail(rc);
@@ -2317,6 +2641,9 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
             if (int rc = path_cap((long long)n1 * (long long)npix, n1, &cap1)) return bail(rc);
             for (int b = 0; b < 2; ++b)
                 if (int rc = alloc_paths(c, c->lbuf[b], cap1)) return bail(rc);
+            c->lcap[1] = cap1;
+            if (c->mhit[0])
+                if (int rc = c->alloc(&c->mhit[1], cap1)) return bail(rc);
             if (int rc = c->alloc(&c->lctl, 2)) return bail(rc);
             if (int rc = c->alloc(&c->lseg, (size_t)2 * kMaxSeg)) return bail(rc);
             if (int rc = c->alloc(&c->lemit, (size_t)64 * A.emit_stride)) return bail(rc);
@@ -2414,6 +2741,7 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
     const bool spp1 = A.tile.spp == 1;
     const bool sorted = c->flags.sort_by_material != 0;
     const bool mesh = A.S.ntris > 0;
+    const int mmode = mesh_mode(c);   // k_bounce's mesh mode (fused pipeline)
     int cur = 0;   // paths start in buf[0]
     const int h = c->col_half;
     if (!spp1) {
@@ -2457,6 +2785,8 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
         HIP_TRY(hipGetLastError());
         return prof_end(ev, s);
     };
+    if (!sorted && c->fused && mmode == kMeshPre)   // k_traverse's per-bounce ray tickets (both lanes)
+        HIP_TRY(hipMemsetAsync(c->tq, 0, 2 * 64 * sizeof(uint32_t), st));
     if (laned) {
         const int npix = A.tile.npix;
         const int n1 = A.tile.spp / 2, n0 = A.tile.spp - n1;
@@ -2504,9 +2834,10 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
                 a.out = bufs[l][lcur[l] ^ 1];
                 if (sorted) {
                     if (int rc = sort_bounce(a, SL[l], lhn[l], lws[l], lt64[l], ls[l], b)) return rc;
-                } else if (int rc = launch_k(c, bounce_kernel(b == 0, false, mesh), c->grid_bounce[b == 0], ls[l],
-                                             b == 0 ? PT_KIND_FIRST_BOUNCE : PT_KIND_BOUNCE, a, bounce_lds_bytes(a.S))) {
-                    return rc;
+                } else {
+                    a.mhit = c->mhit[l];
+                    a.tticket = c->tq ? c->tq + 64 * l + b : nullptr;
+                    if (int rc = launch_bounce(c, b == 0, false, mmode, ls[l], a, c->lcap[l])) return rc;
                 }
                 ++*cnt[l];
                 lcur[l] ^= 1;
@@ -2521,8 +2852,9 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
         A.out = c->buf[cur ^ 1];
         int rc;
         if (!sorted && c->fused) {
-            rc = launch_k(c, bounce_kernel(b == 0, spp1, mesh), c->grid_bounce[b == 0], st,
-                          b == 0 ? PT_KIND_FIRST_BOUNCE : PT_KIND_BOUNCE, A, bounce_lds_bytes(A.S));
+            A.mhit = c->mhit[0];
+            A.tticket = c->tq ? c->tq + b : nullptr;
+            rc = launch_bounce(c, b == 0, spp1, mmode, st, A, c->lcap[0]);
             if (rc) return rc;
             ++c->compact_launches;
             cur ^= 1;
@@ -2661,6 +2993,26 @@ int pt_debug_stamps(unsigned long long* out8, int32_t reset) {
     if (reset) {
         unsigned long long z[16] = {};
         HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof z));
+    }
+    return PT_OK;
+}
+#endif
+
+#ifdef PT_TRAV_STATS
+// Diagnostic build only (scripts/trav_stats.py): k_traverse's counters summed over their slots:
+// out[0] rays, [1] pair fetches, [2] triangle tests, [3] sum over waves of the longest lane's
+// steps (pairs + triangles), [4] waves.
+int pt_debug_trav(unsigned long long* out5, int32_t reset) {
+    HIP_TRY(hipDeviceSynchronize());
+    static unsigned long long h[64 * 8];
+    HIP_TRY(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_trav), sizeof h));
+    for (int k = 0; k < 5; ++k) {
+        out5[k] = 0;
+        for (int q = 0; q < 64; ++q) out5[k] += h[q * 8 + k];
+    }
+    if (reset) {
+        std::memset(h, 0, sizeof h);
+        HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_trav), h, sizeof h));
     }
     return PT_OK;
 }

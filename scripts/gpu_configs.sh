@@ -1,5 +1,5 @@
 # Bench lines for BASELINE.json configs 3-5 (1 GPU), each under its own time limit.
-# Iterations per pass: 16 (bench default) for configs 3 and 4, 4 for the 100k-triangle config 5.
+# Iterations per pass: the bench default (32) for configs 3 and 4, 8 for the 100k-triangle config 5.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"; mkdir -p gpurun_out
@@ -11,8 +11,8 @@ run() {   # name, extra args
 }
 run cornell_hd_sorted --steps 10 || exit 1
 run multi_object_4k --steps 5 || exit 1
-run random_triangles_100k --steps 3 --spp 4 || exit 1
-run random_triangles_100k --steps 3 --spp 4 --bvh-cull || exit 1
+run random_triangles_100k --steps 3 --spp 8 --samples 8 || exit 1
+run random_triangles_100k --steps 3 --spp 8 --samples 8 --bvh-cull || exit 1
 python3 - <<'PY'
 import json
 for line in open("gpurun_out/configs.jsonl"):

@@ -360,6 +360,44 @@ def test_config_scenes_bitexact(config_scenes, name, kw):
     assert r.sum() > 0
 
 
+@pytest.mark.parametrize("inline", [False, True])
+@pytest.mark.parametrize("name,spp,kw", [
+    ("room", 1, dict()),
+    ("room", 3, dict()),                        # two lanes, each with its own k_traverse records
+    ("room", 3, dict(bvhCull=True)),
+    ("random_triangles", 2, dict()),
+    ("random_triangles", 1, dict(SSAA=False, russianRoulette=False)),
+])
+def test_mesh_traversal_modes_bitexact(room_path, config_scenes, monkeypatch, inline, name, spp, kw):
+    """Mesh scenes with the BVH on: the walk runs in k_traverse ahead of the bounce kernel, whose
+    bounded closest hit takes the mesh hit as an evaluated candidate (default), or inside the bounce
+    kernel (PT_AMD_MESH_INLINE=1).  Both equal the oracle bit for bit, one lane and two."""
+    from cuda_pathtracer_amd import Scene
+    if inline:
+        monkeypatch.setenv("PT_AMD_MESH_INLINE", "1")
+    if name == "room":
+        s, o = _room_pair(room_path, (48, 36))
+    else:
+        s, o = Scene(config_scenes[name]), O.OracleScene.from_json(config_scenes[name])
+    g, r, st, live = _run(s, o, _gui(**kw), iters=2, spp=spp)
+    _assert_bitexact(g, r, f"{name} spp={spp} inline={inline} {kw}")
+    assert r.sum() > 0
+
+
+@pytest.mark.parametrize("rows", ["1", "3"])
+def test_mesh_traversal_stack_spill_bitexact(room_path, config_scenes, monkeypatch, rows):
+    """k_traverse keeps the first PT_AMD_STACK_ROWS stack entries per lane in LDS and the rest in
+    scratch (HybStack): with 1 or 3 LDS rows nearly every push spills, and the images stay exact."""
+    from cuda_pathtracer_amd import Scene
+    monkeypatch.setenv("PT_AMD_STACK_ROWS", rows)
+    s, o = _room_pair(room_path, (40, 30))
+    g, r, _, _ = _run(s, o, _gui(), iters=2, spp=2)
+    _assert_bitexact(g, r, f"room stack rows {rows}")
+    path = config_scenes["random_triangles"]
+    g, r, _, _ = _run(Scene(path), O.OracleScene.from_json(path), _gui(), iters=2, spp=2)
+    _assert_bitexact(g, r, f"random triangles stack rows {rows}")
+
+
 @pytest.mark.parametrize("spp,kw", [(4, dict()), (1, dict(sortbyMaterial=True)), (1, dict(useThrustPartition=True))])
 def test_concurrent_contexts_on_two_streams(cornell_path, room_path, spp, kw):
     """Two render contexts in flight at once on separate streams (each bounce kernel sized to
