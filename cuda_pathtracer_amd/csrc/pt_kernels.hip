@@ -118,6 +118,7 @@ struct KArgs {
     v4f* mhit;             // [path capacity] k_traverse -> k_bounce<.., kMeshPre>: (t, idx, bx, by)
     uint32_t* tticket;     // k_traverse: this bounce's ray ticket (zeroed at the start of the pass)
     int32_t refill_min;    // k_traverse: idle lanes that trigger a refill (kRefillMin; PT_AMD_REFILL)
+    int32_t tchunk;        // k_traverse: largest ray chunk per ticket grab (kTravChunk; PT_AMD_TCHUNK)
     int32_t stack_rows;    // k_traverse: LDS stack entries per thread (HybStack)
 };
 
@@ -224,6 +225,18 @@ __device__ __forceinline__ bool aabb_hit(const float* bmin, const float* bmax, f
 __device__ __forceinline__ bool aabb_hit(const float* bmin, const float* bmax, f3 o, f3 inv) {
     float lo;
     return aabb_hit(bmin, bmax, o, inv, lo);
+}
+
+// The same test for a ray whose o and 1/d are finite: then no slab parameter is NaN (no 0 * inf), and
+// fminf/fmaxf (v_min/v_max) give glm's ternary min/max up to the sign of a zero, which neither
+// comparison below sees — the same outcome in about 12 fewer instructions.
+__device__ __forceinline__ bool aabb_hit_finite(const float* bmin, const float* bmax, f3 o, f3 inv) {
+    const float mx = (bmin[0] - o.x) * inv.x, Mx = (bmax[0] - o.x) * inv.x;
+    const float my = (bmin[1] - o.y) * inv.y, My = (bmax[1] - o.y) * inv.y;
+    const float mz = (bmin[2] - o.z) * inv.z, Mz = (bmax[2] - o.z) * inv.z;
+    const float lo = fmaxf(fmaxf(fminf(mx, Mx), fminf(my, My)), fminf(mz, Mz));
+    const float hi = fminf(fminf(fmaxf(mx, Mx), fmaxf(my, My)), fmaxf(mz, Mz));
+    return !(hi < 0) && !(lo > hi);
 }
 
 struct MeshHit {
@@ -1239,13 +1252,13 @@ __global__ __launch_bounds__(kBlock) void k_traverse(const KArgs A) {
     }
     uint32_t* ticket = A.tticket;
     // chunk size: kTravChunk, smaller when the bounce has few rays (>= 2 chunks per resident wave)
-    const int csz = min(kTravChunk, max(64, (N / (int)(gridDim.x * (kBlock / 64) * 2)) & ~63));
+    const int csz = min(A.tchunk, max(64, (N / (int)(gridDim.x * (kBlock / 64) * 2)) & ~63));
     int cnext = 0, cend = 0;   // the wave's chunk of rays (wave-uniform)
     bool exhausted = false;
     bool have = false;         // this lane holds a ray
     // walk state: an interior pair (cur >= 0) or a leaf's triangle range [ti, te) (leaf)
     int q = 0, cur = 0, top = 0, ti = 0, te = 0;
-    bool leaf = false;
+    bool leaf = false, finite = true;   // finite: o and 1/d are finite (aabb_hit_finite)
     f3 o = F3(0, 0, 0), d = F3(0, 0, 0), inv = F3(0, 0, 0);
     uint32_t negm = 0;         // bit a: d[a] < 0
     MeshHit r{false, -1, -1, kFLT_MAX, 0.f, 0.f};
@@ -1280,6 +1293,8 @@ __global__ __launch_bounds__(kBlock) void k_traverse(const KArgs A) {
                     q = ray(cnext + (int)rank, o, d);
                     negm = (d.x < 0.0f ? 1u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 4u : 0u);
                     inv = F3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+                    finite = __builtin_isfinite(inv.x) && __builtin_isfinite(inv.y) && __builtin_isfinite(inv.z) &&
+                             __builtin_isfinite(o.x) && __builtin_isfinite(o.y) && __builtin_isfinite(o.z);
                     const float bmin[3] = {S.root_lo[0], S.root_lo[1], S.root_lo[2]};
                     const float bmax[3] = {S.root_hi[0], S.root_hi[1], S.root_hi[2]};
                     top = 0;
@@ -1328,10 +1343,16 @@ __global__ __launch_bounds__(kBlock) void k_traverse(const KArgs A) {
 #ifdef PT_TRAV_STATS
                 ++n_pairs;
 #endif
-                float lo;
                 const float lmn[3] = {x0[0], x0[1], x0[2]}, lmx[3] = {x1[0], x1[1], x1[2]};
                 const float rmn[3] = {x2[0], x2[1], x2[2]}, rmx[3] = {x3[0], x3[1], x3[2]};
-                const bool hl = aabb_hit(lmn, lmx, o, inv, lo), hr = aabb_hit(rmn, rmx, o, inv, lo);
+                bool hl, hr;
+                if (__ballot(!finite) == 0) {   // (wave-uniform)
+                    hl = aabb_hit_finite(lmn, lmx, o, inv);
+                    hr = aabb_hit_finite(rmn, rmx, o, inv);
+                } else {
+                    hl = aabb_hit(lmn, lmx, o, inv);
+                    hr = aabb_hit(rmn, rmx, o, inv);
+                }
                 const int cl = __float_as_int(x0[3]), cr = __float_as_int(x2[3]);
                 const bool ng = (negm >> (cur & 3)) & 1u;   // split axis: right child first
                 const bool h1 = ng ? hr : hl, h2 = ng ? hl : hr;
@@ -2607,6 +2628,8 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
             per_cu = 4;
         c->grid_traverse = cus * per_cu;
         A.refill_min = kRefillMin;
+        A.tchunk = kTravChunk;
+        if (const char* tc = std::getenv("PT_AMD_TCHUNK")) A.tchunk = std::max(64, std::min(4096, std::atoi(tc)));
         if (const char* rf = std::getenv("PT_AMD_REFILL")) A.refill_min = std::max(1, std::min(64, std::atoi(rf)));
     }
     if (int rc = c->alloc(&A.image, (size_t)npix * 3)) return bail(rc);
