@@ -52,7 +52,7 @@ struct Ctl {            // per-parity control block (32 B)
     uint32_t ticket;       // claimed tile schedule (look-back kernels)
     uint32_t live;         // path count: after k_compact_paths (split), of this bounce (sorted)
     uint32_t chunk, nseg;  // segment layout written by k_bounce / k_sort_shade
-    uint32_t hist_t64;     // sorted pipeline: histogram tiles of the launch (an upper bound for the next)
+    uint32_t hist_live;    // sorted pipeline: live histogram entries (+1) written by k_sort_produce
     uint32_t pad[3];
 };
 struct DevStats {
@@ -1079,7 +1079,7 @@ constexpr uint32_t kSegCountMask = (1u << kSegItShift) - 1u;
 // by the whole workgroup (thread t owns iteration t; spp <= kBlock): s_lay = {tpb, nseg, iteration
 // of this workgroup (-1: idle), its chunk index in that iteration}.  s_ib must be visible on entry.
 __device__ __forceinline__ void plan_layout(const int32_t* s_ib, int spp, int grid, int b, int32_t* s_lay,
-                                            uint32_t* s_tmp) {
+                                            uint32_t* s_tmp, int32_t* s_first = nullptr) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t tl = tid < spp ? (uint32_t)(s_ib[tid + 1] - s_ib[tid] + kBlock - 1) / kBlock : 0u;
     const uint32_t i1 = lb::wave_inclusive_scan(tl);
@@ -1096,6 +1096,10 @@ __device__ __forceinline__ void plan_layout(const int32_t* s_ib, int spp, int gr
     for (int q = 0; q < wave; ++q) pre += s_tmp[4 + q];
     if (tid < spp && b >= (int)pre && b < (int)(pre + g)) { s_lay[2] = tid; s_lay[3] = b - (int)pre; }
     if (tid == 0) { s_lay[0] = tpb; s_lay[1] = (int)(s_tmp[4] + s_tmp[5] + s_tmp[6] + s_tmp[7]); }
+    if (s_first) {   // first workgroup (= output segment) of every iteration, s_first[spp] = nseg
+        if (tid < spp) s_first[tid] = (int32_t)pre;
+        if (tid == 0) s_first[spp] = (int32_t)(s_tmp[4] + s_tmp[5] + s_tmp[6] + s_tmp[7]);
+    }
     __syncthreads();
 }
 
@@ -1599,280 +1603,206 @@ __global__ __launch_bounds__(kBlock) void k_compact_paths(const KArgs A) {
 }
 
 // ---- material-sorted mode (pathtrace.cu:479-491: stable sort_by_key on materialId) ---------
-// Material-sorted pipeline (sortbyMaterial), three kernels and one library scan per bounce:
-//   k_sort_isect  [raygen] + closest hit of the logical input (read through the previous
-//                 k_sort_shade's segments), hit record and material key per path, and a
-//                 per-64-path material histogram;
-//   scan          of the histogram: every path's stable sorted position base;
-//   k_sort_scatter  perm[sorted position] = physical path index (and re-zeroes the histogram);
-//   k_sort_shade  shades in sorted order (RNG key = sorted index within the iteration,
-//                 pathtrace.cu:315) and compacts the survivors into per-iteration segments
-//                 exactly like k_bounce — no separate compaction launch or path copy.
+// Material-sorted pipeline (sortbyMaterial): per bounce one producer launch, a histogram scan and
+// one scatter.
+//   k_sort_produce  shades the paths of bounce b in sorted order (gathered through perm; RNG key =
+//                   sorted index within the iteration, pathtrace.cu:315), compacts the survivors into
+//                   per-iteration segments exactly like k_bounce, and INTERSECTS each survivor's new
+//                   ray right away (the sort key of bounce b + 1): the survivor's 64-byte record is
+//                   written once, with its hit.  The first bounce's producer generates the camera
+//                   rays instead of shading.  Sort keys are counted per PRODUCER TILE (the 256 input
+//                   paths one workgroup step handles, whose survivors are a contiguous run of the
+//                   output): hist[iteration][material][tile of that iteration], and every survivor
+//                   gets its rank among the same-material survivors of its tile;
+//   scan            of the histogram (k_hist_sums / k_hist_scan_sums / k_hist_apply, no co-residency
+//                   needed): tiles are in logical order, so hist's flat exclusive scan + the in-tile
+//                   rank IS the survivor's position in the stable sort by (iteration, material);
+//   k_sort_scatter  perm[sorted position] = physical slot.
 // Batched passes sort every iteration on its own (stable sort by (iteration, material), as `spp`
-// sequential pathtrace() calls would).  Each iteration's paths start on a fresh 64-path tile and
-// the histogram is laid out [iteration][material][tile of that iteration]: its flat exclusive
-// scan IS the (iteration, material) sorted position, at nmats * (tiles + spp) entries, whatever spp.
-// Hits are stored at the PHYSICAL path index so k_sort_shade needs only perm.
-// Path j of the sorted pipeline: state and hit record as ONE 64-byte record, so k_sort_shade's
-// gather in sorted order reads one 64-byte span per path (the 16-byte planes of the fused layout
-// plus two hit planes put five cache lines behind every gathered path):
+// sequential pathtrace() calls would): an iteration's tiles form one block of the histogram.
+// Compared with a separate intersect launch that re-reads every record and writes its hit back,
+// this moves each record across HBM twice per bounce (one gathered read, one write) instead of four
+// times, and the histogram has one entry per 256 paths and material instead of one per 64.
+// Path j of the sorted pipeline is ONE 64-byte record, so the gather reads one 64-byte span:
 //   r0 = (o.xyz, d.x)   r1 = (d.yz, c.rg)   r2 = (c.b, slot, t, material)   r3 = (n.xyz, 0)
 // `bounces` is not stored: every path entering bounce b has b bounces behind it.  Texture
-// coordinates (textured scenes only) go to HitSoA::uv.
+// coordinates (textured scenes only) go to a side array, double-buffered like the records.
 __device__ __forceinline__ v4f* srec(const PathSoA& B, int j) { return B.a + ((size_t)(uint32_t)j << 2); }
 
 struct SortArgs {
-    int32_t* keys;     // [P] material key of logical path i
-    int32_t* phys;     // [P] physical index of logical path i
-    int32_t* hist;     // [nmats * (max_t64 + spp) + 1], all zero between bounces
-    const int32_t* offs;
-    int32_t* perm;     // [P] sorted position -> physical index
-    int32_t* tbase;    // [spp + 1] first histogram tile of each iteration (this bounce)
-    int32_t* ibase;    // [spp + 1] first logical path of each iteration (this bounce)
-    const uint32_t* scan_err;   // the library scan's error word (sc_workspace_error_word), or null
+    int32_t* kr;        // [cap] per output slot: material << 24 | producer tile << 8 | rank in (tile, material)
+    int32_t* hist;      // per (iteration, material, producer tile) survivor counts (sort_hidx)
+    int32_t* offs;      // its exclusive scan
+    int32_t* perm;      // [P] sorted position -> physical slot
+    int32_t* iseg0;     // [2][kMaxSpp + 1] per parity: first segment of each iteration ([spp] = nseg)
+    float* uv_out;      // textured scenes: (u, v) of the output records ([2 * cap])
 };
+constexpr int kSortMaxMats = 64;   // one lane per material in the per-tile counts (else: no sorting)
 
-// Thread t < spp: s_tb = exclusive scan of the iterations' 64-path tile counts (s_tb[spp] = all).
-__device__ __forceinline__ void iteration_tiles(const int32_t* s_ib, int spp, int32_t* s_tb, uint32_t* s_tmp) {
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint32_t n = tid < spp ? (uint32_t)(s_ib[tid + 1] - s_ib[tid] + 63) / 64u : 0u;
-    const uint32_t incl = lb::wave_inclusive_scan(n);
-    if (lane == 63) s_tmp[wave] = incl;
-    __syncthreads();
-    uint32_t pre = incl - n;
-    for (int q = 0; q < wave; ++q) pre += s_tmp[q];
-    if (tid < spp) s_tb[tid] = (int32_t)pre;
-    if (tid == 0) s_tb[spp] = (int32_t)(s_tmp[0] + s_tmp[1] + s_tmp[2] + s_tmp[3]);
-    __syncthreads();
-}
-// Iteration owning histogram tile g (the last one starting at or before g: empty ones own none).
-__device__ __forceinline__ int tile_iteration(const int32_t* s_tb, int spp, int g) {
-    int lo = 0, hi = spp - 1;
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (s_tb[mid] <= g) lo = mid; else hi = mid - 1;
-    }
-    return lo;
+// Histogram entry of producer tile k of segment s for material m, the iteration's segments being
+// [s0, s1) of tpb tiles each: [iteration block][material][tile of the iteration].
+__device__ __forceinline__ size_t sort_hidx(int s0, int s1, int tpb, int nmats, int s, int k, int m) {
+    return (size_t)s0 * tpb * nmats + (size_t)m * (size_t)(s1 - s0) * tpb + (size_t)(s - s0) * tpb + k;
 }
 
-template <bool FIRST, bool MESH>
-__global__ __launch_bounds__(kBlock) void k_sort_isect(const KArgs A, const SortArgs SA) {
+template <bool FIRST, bool SPP1, bool MESH>
+__global__ __launch_bounds__(kBlock) void k_sort_produce(const KArgs A, const SortArgs SA) {
+    __shared__ DMaterial s_mats[kLdsMats];
     __shared__ LGeom s_geoms[MESH ? 1 : kLdsGeoms];
-    __shared__ int32_t s_pre[FIRST ? 1 : kMaxSeg + 1];
-    __shared__ int32_t s_ib[kMaxSpp + 1], s_tb[kMaxSpp + 1];
+    __shared__ int32_t s_sb[kMaxSpp + 1];      // input: sorted start of every iteration (first: j * npix)
+    __shared__ int32_t s_first[kMaxSpp + 1];   // output: first segment of every iteration ([spp] = nseg)
     __shared__ int32_t s_lay[4];
     __shared__ uint32_t s_tmp[12];
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int par = A.parity;
-    const int spp = A.tile.spp;
-    // tiles never grow within a pass: a workgroup past the previous bounce's tiles has no work
-    if (!FIRST && (int)blockIdx.x * (kBlock / 64) >= (int)A.ctl[par].hist_t64 && blockIdx.x != 0) return;
-    int N, nseg_in = 0, chunk_in = 0;
-    if (FIRST) {
-        N = A.n_fixed;
-        for (int j = tid; j <= spp; j += kBlock) s_ib[j] = j * A.tile.npix;   // spp + 1 entries (spp <= kBlock)
-        __syncthreads();
-    } else {
-        for (int j = tid; j <= spp; j += kBlock) s_ib[j] = -1;
-        nseg_in = (int)A.ctl[par].nseg;
-        chunk_in = (int)A.ctl[par].chunk;
-        N = scan_segments(reinterpret_cast<const uint32_t*>(A.seg) + (size_t)par * kMaxSeg, nseg_in, spp, s_pre, s_ib,
-                          s_lay, s_tmp);
-    }
-    iteration_tiles(s_ib, spp, s_tb, s_tmp + 4);
-    if (!MESH) stage_geoms(A.S, s_geoms);
-    __syncthreads();
-    const int T = s_tb[spp];
-    if (blockIdx.x == 0) {
-        for (int j = tid; j <= spp; j += kBlock) { SA.tbase[j] = s_tb[j]; SA.ibase[j] = s_ib[j]; }
-        if (tid == 0) {
-            A.ctl[par ^ 1].hist_t64 = (uint32_t)T;
-            A.ctl[par].live = (uint32_t)N;   // for k_sort_scatter / k_sort_shade of this bounce
-        }
-        count_bounce(A, N);
-    }
-    const int nmats = A.S.nmats;
-    const int waves = gridDim.x * (blockDim.x >> 6);
-    for (int g = blockIdx.x * (blockDim.x >> 6) + (tid >> 6); g < T; g += waves) {
-        const int it = tile_iteration(s_tb, spp, g);
-        const int t = g - s_tb[it];
-        const int i = s_ib[it] + 64 * t + lane;
-        int key = -1;
-        if (i < s_ib[it + 1]) {
-            int j = i;
-            PathReg p;
-            if (FIRST) {
-                raygen(A.cam, A.fl, A.tile, i, p);
-            } else {
-                int lo = 0, hi = nseg_in - 1;   // segment of the tile's first path, then walk
-                const int f = s_ib[it] + 64 * t;
-                while (lo < hi) {
-                    const int mid = (lo + hi + 1) >> 1;
-                    if (s_pre[mid] <= f) lo = mid; else hi = mid - 1;
-                }
-                const int sg = seg_walk(s_pre, nseg_in, lo, i);
-                j = sg * chunk_in + (i - s_pre[sg]);
-                const v4f* r = srec(A.in, j);
-                const v4f pa = r[0], pb = r[1];
-                p.o = F3(pa[0], pa[1], pa[2]);
-                p.d = F3(pa[3], pb[0], pb[1]);
-            }
-            const Hit h = closest_hit<MESH, true, !FIRST>(A.S, A.fl, s_geoms, p.o, p.d, &A.stats->bound_mismatch);
-            key = h.t == -1.0f ? 0 : h.mat;     // misses keep the memset materialId 0 (pathtrace.cu:466)
-            v4f* r = srec(A.in, j);
-            if (FIRST) {
-                r[0] = v4f{p.o.x, p.o.y, p.o.z, p.d.x};
-                r[1] = v4f{p.d.y, p.d.z, p.c.x, p.c.y};
-                r[2] = v4f{p.c.z, __int_as_float(p.slot), h.t, __int_as_float(key)};
-            } else {   // (c.b, slot) were written by the previous k_sort_shade
-                *reinterpret_cast<v2f*>(reinterpret_cast<float*>(r + 2) + 2) = v2f{h.t, __int_as_float(key)};
-            }
-            r[3] = v4f{h.n.x, h.n.y, h.n.z, 0.0f};
-            if (A.S.texs) {
-                A.hit.uv[2 * (size_t)j] = h.u;
-                A.hit.uv[2 * (size_t)j + 1] = h.v;
-            }
-            SA.keys[i] = key;
-            SA.phys[i] = j;
-        }
-        // this tile's count of every material present: one ballot per distinct key in the wave
-        // (the histogram is all zero on entry; k_sort_scatter re-zeroes exactly these entries)
-        const size_t h0 = (size_t)nmats * s_tb[it] + t;
-        const size_t tiles_it = (size_t)(s_tb[it + 1] - s_tb[it]);
-        uint64_t rem = __ballot(key >= 0);
-        while (rem) {
-            const int src = __builtin_ctzll(rem);
-            const int kk = __builtin_amdgcn_readlane(key, src);
-            const uint64_t m = __ballot(key == kk);
-            if (lane == src) SA.hist[h0 + (size_t)kk * tiles_it] = (int32_t)__popcll(m);
-            rem &= ~m;
-        }
-    }
-}
-
-__global__ __launch_bounds__(kBlock) void k_sort_scatter(const KArgs A, const SortArgs SA) {
-    __shared__ int32_t s_ib[kMaxSpp + 1], s_tb[kMaxSpp + 1];
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int spp = A.tile.spp;
-    for (int j = tid; j <= spp; j += kBlock) { s_ib[j] = SA.ibase[j]; s_tb[j] = SA.tbase[j]; }
-    // a stalled library scan (static schedule on a shared GPU) left invalid offsets: report it
-    // through DevStats::err, which pt_stats turns into PT_ERR_DEVICE
-    if (SA.scan_err && blockIdx.x == 0 && tid == 0 && *SA.scan_err) atomicOr(&A.stats->err, 2u);
-    __syncthreads();
-    const int T = s_tb[spp];
-    const int nmats = A.S.nmats;
-    const int waves = gridDim.x * (blockDim.x >> 6);
-    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    for (int g = blockIdx.x * (blockDim.x >> 6) + (tid >> 6); g < T; g += waves) {
-        const int it = tile_iteration(s_tb, spp, g);
-        const int t = g - s_tb[it];
-        const int tiles_it = s_tb[it + 1] - s_tb[it];
-        const int i = s_ib[it] + 64 * t + lane;
-        const bool valid = i < s_ib[it + 1];
-        const int key = valid ? SA.keys[i] : -1;
-        const size_t h0 = (size_t)nmats * s_tb[it] + t;
-        // rank among the tile's lanes with the same key: one ballot per distinct key in the wave;
-        // the histogram entries k_sort_isect set are zeroed again for the next bounce
-        uint32_t rank = 0;
-        uint64_t rem = __ballot(valid);
-        while (rem) {
-            const int src = __builtin_ctzll(rem);
-            const int kk = __builtin_amdgcn_readlane(key, src);
-            const uint64_t m = __ballot(key == kk);
-            if (key == kk) rank = (uint32_t)__popcll(m & lt);
-            if (lane == src) SA.hist[h0 + (size_t)kk * tiles_it] = 0;
-            rem &= ~m;
-        }
-        if (valid) SA.perm[SA.offs[h0 + (size_t)key * tiles_it] + rank] = SA.phys[i];
-    }
-}
-
-template <bool SPP1>
-__global__ __launch_bounds__(kBlock) void k_sort_shade(const KArgs A, const SortArgs SA) {
-    __shared__ DMaterial s_mats[kLdsMats];
-    __shared__ int32_t s_sb[kMaxSpp + 1];
-    __shared__ int32_t s_lay[4];
-    __shared__ uint32_t s_tmp[8];
     __shared__ uint32_t s_wc[2][4];
+    __shared__ uint32_t s_kc[2][4][kSortMaxMats];   // per wave: survivors of each material in the tile
     __shared__ uint32_t s_cnt;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int par = A.parity;
     const int spp = A.tile.spp;
     const int nmats = A.S.nmats;
-    // sorted start of every iteration: the scanned histogram at its first tile
-    for (int j = tid; j <= spp; j += kBlock) s_sb[j] = SA.offs[(size_t)nmats * SA.tbase[j]];
+    if (FIRST) {
+        for (int j = tid; j <= spp; j += kBlock) s_sb[j] = j * A.tile.npix;
+    } else {   // the scanned histogram at each iteration's first entry
+        const int tpb_in = (int)(A.ctl[par].chunk / kBlock);
+        const int32_t* is0 = SA.iseg0 + (size_t)par * (kMaxSpp + 1);
+        for (int j = tid; j <= spp; j += kBlock) s_sb[j] = SA.offs[(size_t)is0[j] * tpb_in * nmats];
+    }
     __syncthreads();
-    plan_layout(s_sb, spp, (int)gridDim.x, (int)blockIdx.x, s_lay, s_tmp);
+    plan_layout(s_sb, spp, (int)gridDim.x, (int)blockIdx.x, s_lay, s_tmp, s_first);
     const int tpb = __builtin_amdgcn_readfirstlane(s_lay[0]);
     const int nseg = __builtin_amdgcn_readfirstlane(s_lay[1]);
     const int my_it = __builtin_amdgcn_readfirstlane(s_lay[2]);
     const int my_c = __builtin_amdgcn_readfirstlane(s_lay[3]);
     const int chunk = tpb * kBlock;
-    if (blockIdx.x == 0 && tid == 0) {
-        A.ctl[par ^ 1].nseg = (uint32_t)nseg;
-        A.ctl[par ^ 1].chunk = (uint32_t)chunk;
+    if (blockIdx.x == 0) {
+        if (tid == 0) {
+            A.ctl[par ^ 1].nseg = (uint32_t)nseg;
+            A.ctl[par ^ 1].chunk = (uint32_t)chunk;
+            A.ctl[par ^ 1].hist_live = (uint32_t)(nseg * tpb * nmats + 1);   // entries + the end offset
+        }
+        int32_t* os0 = SA.iseg0 + (size_t)(par ^ 1) * (kMaxSpp + 1);
+        for (int j = tid; j <= spp; j += kBlock) os0[j] = s_first[j];
+        if (!FIRST) count_bounce(A, s_sb[spp]);   // the live paths of bounce b, shaded here
     }
     if (my_it < 0) return;
+    if (!MESH) stage_geoms(A.S, s_geoms);
     stage_materials(A, s_mats);
-    const bool lds_mats = A.S.nmats <= kLdsMats;
+    const bool lds_mats = nmats <= kLdsMats;
     const int it_base = __builtin_amdgcn_readfirstlane(s_sb[my_it]);
     const int first = it_base + my_c * chunk;
     const int last = min(__builtin_amdgcn_readfirstlane(s_sb[my_it + 1]), first + chunk);
     const int iter = A.tile.iter_first + my_it;
+    const int s0 = __builtin_amdgcn_readfirstlane(s_first[my_it]);
+    const int s1 = __builtin_amdgcn_readfirstlane(s_first[my_it + 1]);
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     uint32_t kept = 0, emit_cnt = 0;
     int k = 0;
     for (int base = first; base < last; base += kBlock, ++k) {
         const int idx = base + tid;
         bool alive = false, emitted = false;
         PathReg p;
+        Hit h;
         if (idx < last) {
-            const int j = SA.perm[idx];
-            const v4f* r = srec(A.in, j);
-            const v4f r0 = r[0], r1 = r[1], r2 = r[2], r3 = r[3];
-            p.o = F3(r0[0], r0[1], r0[2]);
-            p.d = F3(r0[3], r1[0], r1[1]);
-            p.c = F3(r1[2], r1[3], r2[0]);
-            p.slot = __float_as_int(r2[1]);
-            p.bounces = A.bounce;
-            Hit h;
-            h.t = r2[2];
-            h.mat = __float_as_int(r2[3]);
-            h.n = F3(r3[0], r3[1], r3[2]);
-            h.u = h.v = 0.0f;
-            if (A.S.texs && h.t > 0.0f) {
-                const bool tex = lds_mats ? s_mats[h.mat].texture_id != -1 : A.S.mats[h.mat].texture_id != -1;
-                if (tex) {
-                    h.u = A.hit.uv[2 * (size_t)j];
-                    h.v = A.hit.uv[2 * (size_t)j + 1];
+            if (FIRST) {
+                raygen(A.cam, A.fl, A.tile, idx, p);
+                alive = true;
+            } else {
+                const int j = SA.perm[idx];
+                const v4f* r = srec(A.in, j);
+                const v4f r0 = r[0], r1 = r[1], r2 = r[2], r3 = r[3];
+                p.o = F3(r0[0], r0[1], r0[2]);
+                p.d = F3(r0[3], r1[0], r1[1]);
+                p.c = F3(r1[2], r1[3], r2[0]);
+                p.slot = __float_as_int(r2[1]);
+                p.bounces = A.bounce;
+                h.t = r2[2];
+                h.mat = __float_as_int(r2[3]);
+                h.n = F3(r3[0], r3[1], r3[2]);
+                h.u = h.v = 0.0f;
+                if (A.S.texs && h.t > 0.0f) {
+                    const bool tex = lds_mats ? s_mats[h.mat].texture_id != -1 : A.S.mats[h.mat].texture_id != -1;
+                    if (tex) {
+                        h.u = A.hit.uv[2 * (size_t)j];
+                        h.v = A.hit.uv[2 * (size_t)j + 1];
+                    }
+                }
+                // key: sorted index within the path's own iteration
+                const int key = A.fl.rng_pixel ? slot_pixel(A.cam, A.tile, p.slot) : idx - it_base;
+                alive = lds_mats ? shade(A.S, A.fl, A.tile.depth, iter, key, p, h, s_mats)
+                                 : shade(A.S, A.fl, A.tile.depth, iter, key, p, h, A.S.mats);
+                if (!alive) {
+                    emitted = p.c.x != 0.0f || p.c.y != 0.0f || p.c.z != 0.0f;
+                    retire<SPP1>(A, p);
                 }
             }
-            // key: sorted index within the path's own iteration
-            const int key = A.fl.rng_pixel ? slot_pixel(A.cam, A.tile, p.slot) : idx - it_base;
-            alive = lds_mats ? shade(A.S, A.fl, A.tile.depth, iter, key, p, h, s_mats)
-                             : shade(A.S, A.fl, A.tile.depth, iter, key, p, h, A.S.mats);
-            if (!alive) {
-                emitted = p.c.x != 0.0f || p.c.y != 0.0f || p.c.z != 0.0f;
-                retire<SPP1>(A, p);
-            }
+            if (alive) h = closest_hit<MESH, true, !FIRST>(A.S, A.fl, s_geoms, p.o, p.d, &A.stats->bound_mismatch);
         }
+        const int key = alive ? (h.t == -1.0f ? 0 : h.mat) : -1;   // misses keep materialId 0 (pathtrace.cu:466)
         emit_cnt += (uint32_t)__popcll(__ballot(emitted));
         const uint64_t m = __ballot(alive);
         const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        // per material present: one ballot -> in-wave rank (lanes of that key) and count (lane == key)
+        uint32_t krank = 0, kcnt = 0;
+        uint64_t rem = m;
+        while (rem) {
+            const int src = __builtin_ctzll(rem);
+            const int kk = __builtin_amdgcn_readlane(key, src);
+            const uint64_t mk = __ballot(key == kk);
+            if (key == kk) krank = (uint32_t)__popcll(mk & lt);
+            if (lane == kk) kcnt = (uint32_t)__popcll(mk);
+            rem &= ~mk;
+        }
+        if (lane < nmats) s_kc[k & 1][wave][lane] = kcnt;
         if (lane == 0) s_wc[k & 1][wave] = (uint32_t)__popcll(m);
         __syncthreads();
         const uint32_t w0 = s_wc[k & 1][0], w1 = s_wc[k & 1][1], w2 = s_wc[k & 1][2], w3 = s_wc[k & 1][3];
         const uint32_t before = (wave > 0 ? w0 : 0u) + (wave > 1 ? w1 : 0u) + (wave > 2 ? w2 : 0u);
-        if (alive) {   // the whole 64-byte record (k_sort_isect fills in t, material and n)
-            v4f* r = srec(A.out, (int)blockIdx.x * chunk + (int)(kept + before + rank));
+        if (alive) {
+            uint32_t kb = krank;
+            for (int w = 0; w < wave; ++w) kb += s_kc[k & 1][w][key];
+            const int q = (int)blockIdx.x * chunk + (int)(kept + before + rank);
+            v4f* r = srec(A.out, q);
             r[0] = v4f{p.o.x, p.o.y, p.o.z, p.d.x};
             r[1] = v4f{p.d.y, p.d.z, p.c.x, p.c.y};
-            r[2] = v4f{p.c.z, __int_as_float(p.slot), 0.0f, 0.0f};
-            r[3] = v4f{0.0f, 0.0f, 0.0f, 0.0f};
+            r[2] = v4f{p.c.z, __int_as_float(p.slot), h.t, __int_as_float(key)};
+            r[3] = v4f{h.n.x, h.n.y, h.n.z, 0.0f};
+            if (A.S.texs) {
+                SA.uv_out[2 * (size_t)q] = h.u;
+                SA.uv_out[2 * (size_t)q + 1] = h.v;
+            }
+            SA.kr[q] = (int32_t)(((uint32_t)key << 24) | ((uint32_t)k << 8) | kb);
         }
+        if (wave == 0 && lane < nmats)
+            SA.hist[sort_hidx(s0, s1, tpb, nmats, (int)blockIdx.x, k, lane)] =
+                (int32_t)((s_kc[k & 1][0][lane] + s_kc[k & 1][1][lane]) + (s_kc[k & 1][2][lane] + s_kc[k & 1][3][lane]));
         kept += (w0 + w1) + (w2 + w3);
     }
+    for (int e = tid; e < (tpb - k) * nmats; e += kBlock)   // this segment's tiles past its last: empty
+        SA.hist[sort_hidx(s0, s1, tpb, nmats, (int)blockIdx.x, k + e / nmats, e % nmats)] = 0;
     if (tid == 0) A.seg[(size_t)(par ^ 1) * kMaxSeg + blockIdx.x] = (int32_t)(kept | ((uint32_t)my_it << kSegItShift));
     flush_emissive(A, emit_cnt, &s_cnt);
+}
+
+// perm[sorted position] = physical slot, for every survivor in the producer's segments (256-slot
+// blocks of the segments, grid-stride; blocks past a segment's count are empty).
+__global__ __launch_bounds__(kBlock) void k_sort_scatter(const KArgs A, const SortArgs SA) {
+    const int par = A.parity;
+    const int nmats = A.S.nmats;
+    const int nseg = (int)A.ctl[par].nseg, chunk = (int)A.ctl[par].chunk;
+    const int tpb = chunk / kBlock;
+    const int32_t* is0 = SA.iseg0 + (size_t)par * (kMaxSpp + 1);
+    const uint32_t* words = reinterpret_cast<const uint32_t*>(A.seg) + (size_t)par * kMaxSeg;
+    for (int blk = (int)blockIdx.x; blk < nseg * tpb; blk += (int)gridDim.x) {
+        const int s = blk / tpb;
+        const uint32_t w = words[s];
+        const int cnt = (int)(w & kSegCountMask), it = (int)(w >> kSegItShift);
+        const int j = (blk - s * tpb) * kBlock + (int)threadIdx.x;
+        if (j >= cnt) continue;
+        const int q = s * chunk + j;
+        const uint32_t kr = (uint32_t)SA.kr[q];
+        const int key = (int)(kr >> 24), kt = (int)((kr >> 8) & 0xffffu), r = (int)(kr & 255u);
+        SA.perm[SA.offs[sort_hidx(is0[it], is0[it + 1], tpb, nmats, s, kt, key)] + r] = q;
+    }
 }
 
 // Exclusive scan of the sorted pipeline's histogram when two lanes share the GPU: reduce, scan of
@@ -1910,9 +1840,14 @@ __device__ __forceinline__ void hist_load(const int32_t* __restrict__ in, int64_
     }
 }
 
-__global__ __launch_bounds__(kBlock) void k_hist_sums(const int32_t* __restrict__ in, int64_t n,
+// n: capacity; *nlive (if given): the live entry count (<= n), written by the producer.
+__device__ __forceinline__ int64_t hist_n(int64_t n, const uint32_t* nlive) {
+    return nlive ? (int64_t)min((uint64_t)n, (uint64_t)*nlive) : n;
+}
+__global__ __launch_bounds__(kBlock) void k_hist_sums(const int32_t* __restrict__ in, int64_t n, const uint32_t* nlive,
                                                       uint32_t* __restrict__ sums) {
     __shared__ uint32_t s_w[4];
+    n = hist_n(n, nlive);
     const int64_t base = (int64_t)blockIdx.x * kHistTile + (int64_t)threadIdx.x * kHistPer;
     uint32_t x[kHistPer], v = 0;
     hist_load(in, n, base, x);
@@ -1923,8 +1858,9 @@ __global__ __launch_bounds__(kBlock) void k_hist_sums(const int32_t* __restrict_
     if (threadIdx.x == 0) sums[blockIdx.x] = total;
 }
 
-__global__ __launch_bounds__(kBlock) void k_hist_scan_sums(uint32_t* __restrict__ sums, int tiles) {
+__global__ __launch_bounds__(kBlock) void k_hist_scan_sums(uint32_t* __restrict__ sums, int64_t n, const uint32_t* nlive) {
     __shared__ uint32_t s_w[4];
+    const int tiles = (int)((hist_n(n, nlive) + kHistTile - 1) / kHistTile);
     const int per = (tiles + kBlock - 1) / kBlock;
     const int j0 = (int)threadIdx.x * per;
     uint32_t v = 0;
@@ -1939,8 +1875,9 @@ __global__ __launch_bounds__(kBlock) void k_hist_scan_sums(uint32_t* __restrict_
 }
 
 __global__ __launch_bounds__(kBlock) void k_hist_apply(const int32_t* __restrict__ in, int32_t* __restrict__ out,
-                                                       int64_t n, const uint32_t* __restrict__ sums) {
+                                                       int64_t n, const uint32_t* nlive, const uint32_t* __restrict__ sums) {
     __shared__ uint32_t s_w[4];
+    n = hist_n(n, nlive);
     const int64_t base = (int64_t)blockIdx.x * kHistTile + (int64_t)threadIdx.x * kHistPer;
     uint32_t x[kHistPer], v = 0;
     hist_load(in, n, base, x);
@@ -2022,9 +1959,6 @@ struct pt_ctx {
     std::vector<void*> allocs;
     PathSoA buf[2]{};
     int cur = 0;
-    int32_t *keys = nullptr, *hist = nullptr, *offs = nullptr, *perm = nullptr, *phys = nullptr, *tbase = nullptr;
-    int64_t hist_n = 0;
-    void* scan_ws = nullptr;
     DevStats* stats = nullptr;
     bool profiling = false;
     std::vector<ProfEv> events;   // pool; the first `ev_used` are recorded and unread
@@ -2052,14 +1986,12 @@ struct pt_ctx {
     uint64_t llaunches = 0;
     hipStream_t lane_stream = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-    struct SortSet {   // lane 1's material-sort buffers (lane 0 uses the context's own)
-        int32_t *keys = nullptr, *phys = nullptr, *hist = nullptr, *offs = nullptr, *perm = nullptr;
-        int32_t *tbase = nullptr, *ibase = nullptr;
-        float* uv = nullptr;
-        void* ws = nullptr;
-        int64_t hist_n = 0;
-        int max_t64 = 0;
-    } lsort;
+    struct SortSet {   // material-sort buffers of one lane (k_sort_produce / k_sort_scatter)
+        int32_t *kr = nullptr, *hist = nullptr, *offs = nullptr, *perm = nullptr, *iseg0 = nullptr;
+        float* uv[2] = {nullptr, nullptr};   // (u, v) of the records in buf[0] / buf[1]
+        uint32_t* sums = nullptr;            // histogram scan: tile sums
+        int64_t hist_cap = 0;                // histogram entries allocated (+ the end offset)
+    } sset[2];
     // Mesh scenes: the BVH walk runs in k_traverse ahead of k_bounce<.., kMeshPre> (mesh_mode 2) when
     // the BVH is on and the geom table fits LDS; otherwise inside k_bounce (kMeshInline).
     v4f* mhit[2] = {nullptr, nullptr};   // per lane, indexed by physical path slot
@@ -2323,6 +2255,15 @@ KernelFn trace_kernel(bool first, bool spp1, bool mesh) {
         k_trace<false, false, false>, k_trace<false, false, true>, k_trace<false, true, false>,
         k_trace<false, true, true>,   k_trace<true, false, false>, k_trace<true, false, true>,
         k_trace<true, true, false>,   k_trace<true, true, true>};
+    return table[(first ? 4 : 0) + (spp1 ? 2 : 0) + (mesh ? 1 : 0)];
+}
+
+using SortKernelFn = void (*)(const KArgs, const SortArgs);
+SortKernelFn produce_kernel(bool first, bool spp1, bool mesh) {
+    static const SortKernelFn table[8] = {
+        k_sort_produce<false, false, false>, k_sort_produce<false, false, true>, k_sort_produce<false, true, false>,
+        k_sort_produce<false, true, true>,   k_sort_produce<true, false, false>, k_sort_produce<true, false, true>,
+        k_sort_produce<true, true, false>,   k_sort_produce<true, true, true>};
     return table[(first ? 4 : 0) + (spp1 ? 2 : 0) + (mesh ? 1 : 0)];
 }
 
@@ -2686,48 +2627,23 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
         (e = hipMemset(A.status, 0, (size_t)2 * c->max_tiles * sizeof(uint64_t))) != hipSuccess ||
         (e = hipMemset(c->stats, 0, sizeof(DevStats))) != hipSuccess)
         return bail(pt::fail(PT_ERR_HIP, std::string("hipMemset: ") + hipGetErrorString(e)));
-    // hit SoA + sort buffers (material-sorted mode)
-    {
-        // indexed by physical path index (< path_cap)
-        if (int rc = c->alloc(&A.hit.uv, 2 * (size_t)c->path_cap)) return bail(rc);
-        if (int rc = c->alloc(&c->phys, (size_t)P)) return bail(rc);
-        c->max_t64 = (int)((P + 63) / 64);
-        // [iteration][material][tile]: each iteration starts a fresh tile (+1: the end offset)
-        const size_t hn = (size_t)c->nmats * ((size_t)c->max_t64 + sh.spp) + 1;
-        c->hist_n = (int64_t)hn;
-        if (int rc = c->alloc(&c->tbase, (size_t)kMaxSpp + 1)) return bail(rc);
-        if (int rc = c->alloc(&c->keys, (size_t)P)) return bail(rc);
-        if (int rc = c->alloc(&c->hist, hn)) return bail(rc);
-        if (int rc = c->alloc(&c->offs, hn)) return bail(rc);
-        if ((e = hipMemset(c->hist, 0, hn * sizeof(int32_t))) != hipSuccess)   // k_sort_isect's invariant
-            return bail(pt::fail(PT_ERR_HIP, std::string("hipMemset: ") + hipGetErrorString(e)));
-        if (int rc = c->alloc(&c->perm, (size_t)P)) return bail(rc);
-        uint8_t* ws;
-        if (int rc = c->alloc(&ws, sc_workspace_bytes((int64_t)hn))) return bail(rc);
-        c->scan_ws = ws;
-    }
-    if (c->lanes == 2) {   // lane 1's sort buffers, sized for its floor(spp / 2) iterations
-        auto& L = c->lsort;
-        const int n1 = sh.spp / 2;
-        const long long P1 = (long long)n1 * (long long)npix;
-        size_t cap1 = 0;
-        if (int rc = path_cap(P1, n1, &cap1)) return bail(rc);
-        L.max_t64 = (int)((P1 + 63) / 64);
-        const size_t hn = (size_t)c->nmats * ((size_t)L.max_t64 + n1) + 1;
-        L.hist_n = (int64_t)hn;
-        uint8_t* ws;
-        if (int rc = c->alloc(&L.uv, 2 * cap1)) return bail(rc);
-        if (int rc = c->alloc(&L.phys, (size_t)P1)) return bail(rc);
-        if (int rc = c->alloc(&L.keys, (size_t)P1)) return bail(rc);
-        if (int rc = c->alloc(&L.perm, (size_t)P1)) return bail(rc);
-        if (int rc = c->alloc(&L.tbase, (size_t)kMaxSpp + 1)) return bail(rc);
-        if (int rc = c->alloc(&L.ibase, (size_t)kMaxSpp + 1)) return bail(rc);
-        if (int rc = c->alloc(&L.hist, hn)) return bail(rc);
-        if (int rc = c->alloc(&L.offs, hn)) return bail(rc);
-        if (int rc = c->alloc(&ws, sc_workspace_bytes((int64_t)hn))) return bail(rc);
-        L.ws = ws;
-        if ((e = hipMemset(L.hist, 0, hn * sizeof(int32_t))) != hipSuccess)
-            return bail(pt::fail(PT_ERR_HIP, std::string("hipMemset: ") + hipGetErrorString(e)));
+    // material-sort buffers, per lane: kr and uv by physical slot (< cap), perm by sorted position
+    // (< the lane's paths), the histogram by (producer tile, material) (cap / 256 tiles at most)
+    for (int l = 0; l < c->lanes; ++l) {
+        auto& ss = c->sset[l];
+        const int n_l = l == 0 ? (c->lanes == 2 ? sh.spp - sh.spp / 2 : sh.spp) : sh.spp / 2;
+        const size_t paths = (size_t)n_l * (size_t)npix, cap = c->lcap[l];
+        ss.hist_cap = (int64_t)((size_t)c->nmats * (cap / kBlock + 1) + 2);
+        const size_t tiles = ((size_t)ss.hist_cap + kHistTile - 1) / kHistTile;
+        if (int rc = c->alloc(&ss.kr, cap)) return bail(rc);
+        if (int rc = c->alloc(&ss.perm, paths)) return bail(rc);
+        if (int rc = c->alloc(&ss.hist, (size_t)ss.hist_cap)) return bail(rc);
+        if (int rc = c->alloc(&ss.offs, (size_t)ss.hist_cap)) return bail(rc);
+        if (int rc = c->alloc(&ss.iseg0, 2 * ((size_t)kMaxSpp + 1))) return bail(rc);
+        if (int rc = c->alloc(&ss.sums, tiles)) return bail(rc);
+        if (!S.textures.empty())
+            for (int h = 0; h < 2; ++h)
+                if (int rc = c->alloc(&ss.uv[h], 2 * cap)) return bail(rc);
     }
     if (const char* pl = std::getenv("PT_PIPELINE")) c->fused = std::string(pl) != "split";
     *out = c;
@@ -2772,42 +2688,42 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
         if (c->fin_out[h]) HIP_TRY(hipStreamWaitEvent(st, c->ev_fin[h], 0));   // pass p-2's finalize
     }
     const bool laned = (sorted || c->fused) && c->lanes == 2 && !spp1;
-    // One bounce of the material-sorted pipeline on stream s.  With two lanes the histogram scan
-    // is k_hist_sums / k_hist_scan_sums / k_hist_apply (no co-residency needed: the other lane's
-    // scan may run at the same time); alone, the library's single-pass scan.
-    auto sort_bounce = [&](const KArgs& a, const SortArgs& sa, int64_t hn, void* ws, int max_t64, hipStream_t s,
-                           int b) -> int {
-        const int g64 = std::min((max_t64 + 3) / 4, c->grid_trace);   // grid-stride beyond
+    // One bounce b of the material-sorted pipeline on stream s, for the lane whose buffers are `bufs`
+    // (current one: lcur), launch counter `lc` and sort buffers `ss`: [the first bounce's producer],
+    // histogram scan, scatter, producer (shade b + intersect b + 1).  Every producer flips the buffers.
+    auto sort_bounce = [&](KArgs& a, pt_ctx::SortSet& ss, hipStream_t s, int b, int& lcur, uint64_t& lc,
+                           const PathSoA* bufs) -> int {
         ProfEv* ev;
         if (int rc = prof_begin(c, s, PT_KIND_SORT, &ev)) return rc;
-        if (b == 0 && mesh) hipLaunchKernelGGL((k_sort_isect<true, true>), dim3(g64), dim3(kBlock), 0, s, a, sa);
-        else if (b == 0) hipLaunchKernelGGL((k_sort_isect<true, false>), dim3(g64), dim3(kBlock), 0, s, a, sa);
-        else if (mesh) hipLaunchKernelGGL((k_sort_isect<false, true>), dim3(g64), dim3(kBlock), 0, s, a, sa);
-        else hipLaunchKernelGGL((k_sort_isect<false, false>), dim3(g64), dim3(kBlock), 0, s, a, sa);
-        HIP_TRY(hipGetLastError());
-        int32_t* offs = const_cast<int32_t*>(sa.offs);
-        SortArgs sx = sa;
-        sx.scan_err = nullptr;
-        if (laned || c->flags.shared_gpu) {   // no co-residency needed (another lane or process may hold CUs)
-            const int tiles = (int)((hn + kHistTile - 1) / kHistTile);
-            uint32_t* sums = static_cast<uint32_t*>(ws);   // tiles words (the workspace holds >= hn)
-            hipLaunchKernelGGL(k_hist_sums, dim3(tiles), dim3(kBlock), 0, s, (const int32_t*)sa.hist, hn, sums);
-            hipLaunchKernelGGL(k_hist_scan_sums, dim3(1), dim3(kBlock), 0, s, sums, tiles);
-            hipLaunchKernelGGL(k_hist_apply, dim3(tiles), dim3(kBlock), 0, s, (const int32_t*)sa.hist, offs, hn,
-                               (const uint32_t*)sums);
+        auto produce = [&](bool first) -> int {
+            a.parity = (int)(lc & 1);
+            a.in = bufs[lcur];
+            a.out = bufs[lcur ^ 1];
+            a.hit.uv = ss.uv[lcur];
+            const SortArgs sa{ss.kr, ss.hist, ss.offs, ss.perm, ss.iseg0, ss.uv[lcur ^ 1]};
+            hipLaunchKernelGGL(produce_kernel(first, spp1, mesh), dim3(c->grid_bounce[0]), dim3(kBlock), 0, s, a, sa);
             HIP_TRY(hipGetLastError());
-        } else {
-            if (sc_scan_exclusive_i32(sa.hist, offs, hn, ws, s) != SC_OK)
-                return pt::fail(PT_ERR_HIP, std::string("material scan: ") + sc_last_error());
-            sx.scan_err = sc_workspace_error_word(ws);
-        }
-        hipLaunchKernelGGL(k_sort_scatter, dim3(g64), dim3(kBlock), 0, s, a, sx);
+            ++lc;
+            lcur ^= 1;
+            return PT_OK;
+        };
+        if (b == 0)
+            if (int rc = produce(true)) return rc;
+        a.parity = (int)(lc & 1);
+        const uint32_t* nlive = &a.ctl[a.parity].hist_live;
+        const int tiles = (int)((ss.hist_cap + kHistTile - 1) / kHistTile);
+        hipLaunchKernelGGL(k_hist_sums, dim3(tiles), dim3(kBlock), 0, s, (const int32_t*)ss.hist, ss.hist_cap, nlive, ss.sums);
+        hipLaunchKernelGGL(k_hist_scan_sums, dim3(1), dim3(kBlock), 0, s, ss.sums, ss.hist_cap, nlive);
+        hipLaunchKernelGGL(k_hist_apply, dim3(tiles), dim3(kBlock), 0, s, (const int32_t*)ss.hist, ss.offs, ss.hist_cap,
+                           nlive, (const uint32_t*)ss.sums);
+        const SortArgs sa{ss.kr, ss.hist, ss.offs, ss.perm, ss.iseg0, nullptr};
+        hipLaunchKernelGGL(k_sort_scatter, dim3(c->grid_trace), dim3(kBlock), 0, s, a, sa);
         HIP_TRY(hipGetLastError());
-        if (spp1) hipLaunchKernelGGL(k_sort_shade<true>, dim3(c->grid_bounce[0]), dim3(kBlock), 0, s, a, sx);
-        else hipLaunchKernelGGL(k_sort_shade<false>, dim3(c->grid_bounce[0]), dim3(kBlock), 0, s, a, sx);
-        HIP_TRY(hipGetLastError());
+        if (int rc = produce(false)) return rc;
         return prof_end(ev, s);
     };
+    if (sorted && c->nmats > kSortMaxMats)
+        return pt::fail(PT_ERR_ARG, "material-sorted shading supports at most 64 materials");
     if (!sorted && c->fused && mmode == kMeshPre)   // k_traverse's per-bounce ray tickets (both lanes)
         HIP_TRY(hipMemsetAsync(c->tq, 0, 2 * 64 * sizeof(uint32_t), st));
     if (laned) {
@@ -2824,14 +2740,6 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
         L[1].seg = c->lseg;
         L[1].emit_slots = c->lemit;
         L[1].count_pass = 0;
-        L[1].hit.uv = c->lsort.uv;
-        L[1].ibase = c->lsort.ibase;
-        const SortArgs SL[2] = {{c->keys, c->phys, c->hist, c->offs, c->perm, c->tbase, A.ibase, nullptr},
-                                {c->lsort.keys, c->lsort.phys, c->lsort.hist, c->lsort.offs, c->lsort.perm,
-                                 c->lsort.tbase, c->lsort.ibase, nullptr}};
-        const int64_t lhn[2] = {c->hist_n, c->lsort.hist_n};
-        void* lws[2] = {c->scan_ws, c->lsort.ws};
-        const int lt64[2] = {c->max_t64, c->lsort.max_t64};
         const hipStream_t ls[2] = {st, c->lane_stream};
         const PathSoA* bufs[2] = {c->buf, c->lbuf};
         uint64_t* cnt[2] = {&c->compact_launches, &c->llaunches};
@@ -2850,18 +2758,18 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
         for (int b = 0; b < c->depth; ++b)
             for (int l = 0; l < 2; ++l) {
                 KArgs& a = L[l];
-                a.parity = (int)(*cnt[l] & 1);
                 a.bounce = b;
+                if (sorted) {
+                    if (int rc = sort_bounce(a, c->sset[l], ls[l], b, lcur[l], *cnt[l], bufs[l])) return rc;
+                    continue;
+                }
+                a.parity = (int)(*cnt[l] & 1);
                 a.n_fixed = b == 0 ? a.tile.P : -1;
                 a.in = bufs[l][lcur[l]];
                 a.out = bufs[l][lcur[l] ^ 1];
-                if (sorted) {
-                    if (int rc = sort_bounce(a, SL[l], lhn[l], lws[l], lt64[l], ls[l], b)) return rc;
-                } else {
-                    a.mhit = c->mhit[l];
-                    a.tticket = c->tq ? c->tq + 64 * l + b : nullptr;
-                    if (int rc = launch_bounce(c, b == 0, false, mmode, ls[l], a, c->lcap[l])) return rc;
-                }
+                a.mhit = c->mhit[l];
+                a.tticket = c->tq ? c->tq + 64 * l + b : nullptr;
+                if (int rc = launch_bounce(c, b == 0, false, mmode, ls[l], a, c->lcap[l])) return rc;
                 ++*cnt[l];
                 lcur[l] ^= 1;
             }
@@ -2891,11 +2799,8 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
                 ++c->compact_launches;
                 cur ^= 1;
             }
-        } else {
-            const SortArgs SA{c->keys, c->phys, c->hist, c->offs, c->perm, c->tbase, A.ibase, nullptr};
-            if ((rc = sort_bounce(A, SA, c->hist_n, c->scan_ws, c->max_t64, st, b))) return rc;
-            ++c->compact_launches;
-            cur ^= 1;
+        } else if ((rc = sort_bounce(A, c->sset[0], st, b, cur, c->compact_launches, c->buf))) {
+            return rc;
         }
     }
 
