@@ -1792,16 +1792,40 @@ __global__ __launch_bounds__(kBlock) void k_sort_scatter(const KArgs A, const So
     const int tpb = chunk / kBlock;
     const int32_t* is0 = SA.iseg0 + (size_t)par * (kMaxSpp + 1);
     const uint32_t* words = reinterpret_cast<const uint32_t*>(A.seg) + (size_t)par * kMaxSeg;
-    for (int blk = (int)blockIdx.x; blk < nseg * tpb; blk += (int)gridDim.x) {
-        const int s = blk / tpb;
-        const uint32_t w = words[s];
-        const int cnt = (int)(w & kSegCountMask), it = (int)(w >> kSegItShift);
-        const int j = (blk - s * tpb) * kBlock + (int)threadIdx.x;
-        if (j >= cnt) continue;
-        const int q = s * chunk + j;
-        const uint32_t kr = (uint32_t)SA.kr[q];
-        const int key = (int)(kr >> 24), kt = (int)((kr >> 8) & 0xffffu), r = (int)(kr & 255u);
-        SA.perm[SA.offs[sort_hidx(is0[it], is0[it + 1], tpb, nmats, s, kt, key)] + r] = q;
+    // kU blocks per step, their loads issued together (each slot is kr -> offs -> store, dependent)
+    constexpr int kU = 4;
+    const int nblk = nseg * tpb, G = (int)gridDim.x;
+    for (int blk0 = (int)blockIdx.x; blk0 < nblk; blk0 += kU * G) {
+        int q[kU], nt[kU];
+        size_t hb[kU];
+        uint32_t kr[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const int blk = blk0 + u * G;
+            q[u] = -1;
+            if (blk < nblk) {
+                const int s = blk / tpb;
+                const uint32_t w = words[s];
+                const int cnt = (int)(w & kSegCountMask), it = (int)(w >> kSegItShift);
+                const int j = (blk - s * tpb) * kBlock + (int)threadIdx.x;
+                if (j < cnt) {
+                    q[u] = s * chunk + j;
+                    hb[u] = sort_hidx(is0[it], is0[it + 1], tpb, nmats, s, 0, 0);   // + key * nt + tile
+                    nt[u] = (is0[it + 1] - is0[it]) * tpb;
+                    kr[u] = (uint32_t)SA.kr[q[u]];
+                }
+            }
+        }
+        int dst[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u)
+            if (q[u] >= 0) {
+                const int key = (int)(kr[u] >> 24), kt = (int)((kr[u] >> 8) & 0xffffu);
+                dst[u] = SA.offs[hb[u] + (size_t)key * (size_t)nt[u] + kt] + (int)(kr[u] & 255u);
+            }
+#pragma unroll
+        for (int u = 0; u < kU; ++u)
+            if (q[u] >= 0) SA.perm[dst[u]] = q[u];
     }
 }
 
