@@ -132,6 +132,7 @@ SIGNATURES = {
     "pt_reset_image": (_I, [_P, _P]),
     "pt_stats": (_I, [_P, C.POINTER(Stats)]),
     "pt_profile_enable": (_I, [_P, _I]),
+    "pt_selftest_math": (_I, [C.c_uint64, C.c_uint32, C.POINTER(C.c_uint64)]),
     "pt_profile_read": (_I, [_P, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
     "pt_profile_read_busy": (_I, [_P, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
     "pt_tonemap": (_I, [_P, _I, _I, _F, _P]),
@@ -155,6 +156,9 @@ def _preload_torch() -> None:
             pass
 
 
+_OPTIONAL = {"pt_selftest_math"}
+
+
 def lib() -> C.CDLL:
     global _lib
     if _lib is not None:
@@ -170,6 +174,8 @@ def lib() -> C.CDLL:
     except OSError as e:
         raise NativeLibraryError(f"failed to load {LIB_PATH}: {e}") from e
     for name, (res, args) in SIGNATURES.items():
+        if name in _OPTIONAL and not hasattr(L, name):   # (an older build timed beside this one)
+            continue
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args

@@ -31,8 +31,72 @@ __device__ __forceinline__ float dot(f3 a, f3 b) { return (a.x * b.x + a.y * b.y
 __device__ __forceinline__ f3 cross(f3 a, f3 b) {
     return F3(a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y);
 }
-__device__ __forceinline__ f3 normalize(f3 v) { return v * (1.0f / sqrtf(dot(v, v))); }
-__device__ __forceinline__ float length(f3 v) { return sqrtf(dot(v, v)); }
+
+// ---- correctly rounded sqrt and division, range-gated --------------------------------------
+// hipcc expands sqrtf into v_sqrt + two neighbour corrections, wrapped in a scaling step for tiny
+// inputs and a zero/inf fix-up (16 instructions), and '/' into v_div_scale x2, v_rcp, a Newton
+// step, two residual corrections (v_div_fmas) and v_div_fixup (11 instructions + hazard nops).
+// For operands in a safe range the wrapping steps are identities, so the cores below — the same
+// operations in the same order — return the same bits; outside it (or for 0, NaN, inf, denormal
+// intermediates) the library form runs instead (a divergent branch, skipped when no lane needs it).
+//   sqrt:  x in [2^-96, FLT_MAX]: no scaling, not zero/inf.
+//   n / d: |n|, |d| in [2^-40, 2^40]: exponent gap < 96, no denormal 1/d or quotient, no tiny n,
+//          no zero (a zero numerator's sign would not survive the residual steps).
+// pt_selftest_math checks cores == library ops on the device over random and edge operands.
+__device__ __forceinline__ float sqrt_core(float x) {
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float sm = __uint_as_float(__float_as_uint(s) - 1u);
+    const float sp = __uint_as_float(__float_as_uint(s) + 1u);
+    const float r1 = fmaf(-sm, s, x);
+    const float s1 = r1 <= 0.0f ? sm : s;
+    const float r2 = fmaf(-sp, s, x);
+    return r2 > 0.0f ? sp : s1;
+}
+__device__ __forceinline__ bool sqrt_ok(float x) { return x >= 0x1p-96f && x <= 3.402823466e+38f; }
+__device__ __forceinline__ float recip_core(float d) {   // v_rcp + one Newton step (the divisor's part)
+    const float r = __builtin_amdgcn_rcpf(d);
+    return fmaf(fmaf(-d, r, 1.0f), r, r);
+}
+__device__ __forceinline__ float div_core(float n, float d, float r) {
+    float q = n * r;
+    float e = fmaf(-d, q, n);
+    q = fmaf(e, r, q);
+    e = fmaf(-d, q, n);
+    return fmaf(e, r, q);
+}
+__device__ __forceinline__ bool div_ok(float v) {
+    const float a = fabsf(v);
+    return a >= 0x1p-40f && a <= 0x1p+40f;
+}
+__device__ __forceinline__ float sqrt_cr(float x) {
+    float s = sqrt_core(x);
+    if (__builtin_expect(!sqrt_ok(x), 0)) s = sqrtf(x);
+    return s;
+}
+__device__ __forceinline__ float div_cr(float n, float d) {
+    float q = div_core(n, d, recip_core(d));
+    if (__builtin_expect(!(div_ok(n) && div_ok(d)), 0)) q = n / d;
+    return q;
+}
+// n1 / d and n2 / d sharing the divisor's reciprocal step
+__device__ __forceinline__ void div2_cr(float n1, float n2, float d, float& q1, float& q2) {
+    const float r = recip_core(d);
+    q1 = div_core(n1, d, r);
+    q2 = div_core(n2, d, r);
+    if (__builtin_expect(!(div_ok(n1) && div_ok(n2) && div_ok(d)), 0)) {
+        q1 = n1 / d;
+        q2 = n2 / d;
+    }
+}
+// glm normalize: v * (1 / sqrt(dot(v, v))); dot in [2^-80, 2^80] keeps sqrt and 1/sqrt in range
+__device__ __forceinline__ f3 normalize(f3 v) {
+    const float x = dot(v, v);
+    const float s = sqrt_core(x);
+    float inv = div_core(1.0f, s, recip_core(s));
+    if (__builtin_expect(!(x >= 0x1p-80f && x <= 0x1p+80f), 0)) inv = 1.0f / sqrtf(x);
+    return v * inv;
+}
+__device__ __forceinline__ float length(f3 v) { return sqrt_cr(dot(v, v)); }
 __device__ __forceinline__ float gmin(float a, float b) { return a < b ? a : b; }
 __device__ __forceinline__ float gmax(float a, float b) { return a > b ? a : b; }
 __device__ __forceinline__ float at(f3 v, int i) { return i == 0 ? v.x : (i == 1 ? v.y : v.z); }

@@ -143,8 +143,8 @@ __device__ __forceinline__ float box_test(const G& g, f3 ro, f3 rd, int& ncode) 
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
         const float qa = at(qd, a), oa = at(qo, a);
-        const float t1 = (-0.5f - oa) / qa;
-        const float t2 = (+0.5f - oa) / qa;
+        float t1, t2;
+        div2_cr(-0.5f - oa, +0.5f - oa, qa, t1, t2);
         const float ta = gmin(t1, t2), tb = gmax(t1, t2);
         const int code = 2 * a + (t2 < t1 ? 0 : 1);
         if (ta > 0 && ta > tmin) { tmin = ta; nmin = code; }
@@ -177,7 +177,7 @@ __device__ __forceinline__ float sphere_test(const G& g, f3 r_o, f3 r_d, f3& obj
     const float vdd = dot(ro, rd);
     const float radicand = vdd * vdd - (dot(ro, ro) - 0.25f);   // powf(0.5f, 2) == 0.25f
     if (radicand < 0) return -1.0f;
-    const float sq = sqrtf(radicand);
+    const float sq = sqrt_cr(radicand);
     const float first = -vdd;
     const float t1 = first + sq, t2 = first - sq;
     float t;
@@ -202,7 +202,7 @@ __device__ __forceinline__ bool ray_tri(const DTri& tr, f3 o, f3 d, float& bx, f
     const f3 p = cross(d, e2);
     const float a = dot(e1, p);
     if (a < kFLT_EPS) return false;
-    const float f = 1.0f / a;
+    const float f = div_cr(1.0f, a);
     const f3 s = o - v0;
     bx = f * dot(s, p);
     if (bx < 0.0f || bx > 1.0f) return false;
@@ -648,8 +648,8 @@ __device__ __forceinline__ float exact_geom(const LGeom& L, f3 r_o, f3 r_d, int&
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
             const float qa = at(qd, a), oa = at(qo, a);
-            const float t1 = (-0.5f - oa) / qa;
-            const float t2 = (+0.5f - oa) / qa;
+            float t1, t2;
+            div2_cr(-0.5f - oa, +0.5f - oa, qa, t1, t2);
             const float ta = gmin(t1, t2), tb = gmax(t1, t2);
             const int c = 2 * a + (t2 < t1 ? 0 : 1);
             if (ta > 0 && ta > tmin) { tmin = ta; nmin = c; }
@@ -662,7 +662,7 @@ __device__ __forceinline__ float exact_geom(const LGeom& L, f3 r_o, f3 r_d, int&
     } else {
         const float vdd = dot(qo, qd);
         const float radicand = vdd * vdd - (dot(qo, qo) - 0.25f);
-        const float sq = sqrtf(radicand);
+        const float sq = sqrt_cr(radicand);
         const float t1 = -vdd + sq, t2 = -vdd - sq;
         hit = !(radicand < 0) && !(t1 < 0 && t2 < 0);
         if (t1 > 0 && t2 > 0) { t = gmin(t1, t2); outside = true; }
@@ -811,8 +811,8 @@ __device__ __forceinline__ f3 tex_color(const DTexture& tx, float u, float v) { 
 }
 
 __device__ __forceinline__ f3 hemisphere(f3 n, Rng& rng) {   // interactions.cu:3-41
-    const float up = sqrtf(rng.u01());
-    const float over = sqrtf(1 - up * up);
+    const float up = sqrt_cr(rng.u01());
+    const float over = sqrt_cr(1 - up * up);
     const float around = rng.u01() * kTWO_PI;
     f3 dnn;
     if (fabsf(n.x) < kSQRT_1_3) dnn = F3(1, 0, 0);
@@ -829,7 +829,7 @@ __device__ __forceinline__ f3 reflect(f3 I, f3 N) { return I - hadamard(N * dot(
 __device__ __forceinline__ f3 refract(f3 I, f3 N, float eta) {   // glm 0.9.6.3: NaN when k < 0
     const float dv = dot(N, I);
     const float k = 1.0f - eta * eta * (1.0f - dv * dv);
-    return (eta * I - (eta * dv + sqrtf(k)) * N) * (float)(k >= 0.0f);
+    return (eta * I - (eta * dv + sqrt_cr(k)) * N) * (float)(k >= 0.0f);
 }
 
 // Global pixel index of tile slot `slot` (the raygen mapping below): the shading RNG key under
@@ -883,7 +883,11 @@ __device__ __forceinline__ bool shade(const SceneDev& S, const FlagsDev& fl, int
         const float l = dot(p.c, luma);
         const float q = gmax(0.05f, 1 - l);
         if (rng.u01() < q) { p.c = F3(0, 0, 0); return false; }
-        p.c = p.c / (1.0f - q);
+        const float dq = 1.0f - q;   // three divisions by one divisor: its reciprocal step shared
+        const float rq = recip_core(dq);
+        f3 cq = F3(div_core(p.c.x, dq, rq), div_core(p.c.y, dq, rq), div_core(p.c.z, dq, rq));
+        if (__builtin_expect(!(div_ok(dq) && div_ok(p.c.x) && div_ok(p.c.y) && div_ok(p.c.z)), 0)) cq = p.c / dq;
+        p.c = cq;
     }
     return true;
 }
@@ -1951,6 +1955,40 @@ __global__ void k_preview(const float* __restrict__ image, uint8_t* __restrict__
     }
 }
 
+// pt_selftest_math: the range-gated cores of pt_device.h against the library sqrtf and '/'.
+__device__ __forceinline__ bool same_bits(float a, float b) {
+    return __float_as_uint(a) == __float_as_uint(b) || (a != a && b != b);
+}
+__device__ __forceinline__ float selftest_operand(uint32_t h, uint64_t i, int slot) {
+    const uint32_t kind = (uint32_t)(i >> 2) % 16u;
+    if ((i & 3) == 0) return __uint_as_float((h & 0x807fffffu) | ((0x70u + ((h >> 23) & 0x1fu)) << 23));   // |x| in [2^-15, 2^17)
+    if (kind == 0 && slot == 0) {   // edge operands
+        const float e[8] = {0.0f, -0.0f, 1e-45f, -3e-39f, __builtin_inff(), -__builtin_inff(), __builtin_nanf(""), 0x1p-40f};
+        return e[(h >> 3) & 7];
+    }
+    return __uint_as_float(h);
+}
+__global__ void k_selftest_math(uint64_t n, uint32_t seed, unsigned long long* bad) {
+    unsigned long long e = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t h1 = utilhash((uint32_t)i ^ seed ^ (uint32_t)(i >> 32) * 0x9e3779b9u);
+        const uint32_t h2 = utilhash(h1 + 0x7f4a7c15u), h3 = utilhash(h2 ^ 0x85ebca6bu);
+        const float x = selftest_operand(h1, i, 0), y = selftest_operand(h2, i, 1), z = selftest_operand(h3, i, 2);
+        e += same_bits(sqrt_cr(fabsf(x)), sqrtf(fabsf(x))) ? 0 : 1;
+        e += same_bits(sqrt_cr(x), sqrtf(x)) ? 0 : 1;
+        e += same_bits(div_cr(x, y), x / y) ? 0 : 1;
+        e += same_bits(div_cr(1.0f, y), 1.0f / y) ? 0 : 1;
+        float q1, q2;
+        div2_cr(x, z, y, q1, q2);
+        e += same_bits(q1, x / y) ? 0 : 1;
+        e += same_bits(q2, z / y) ? 0 : 1;
+        const f3 v = F3(x, y, z), nv = normalize(v), rv = v * (1.0f / sqrtf(dot(v, v)));
+        e += (same_bits(nv.x, rv.x) && same_bits(nv.y, rv.y) && same_bits(nv.z, rv.z)) ? 0 : 1;
+        e += same_bits(length(v), sqrtf(dot(v, v))) ? 0 : 1;
+    }
+    if (e) atomicAdd(bad, e);
+}
+
 // ------------------------------------------------------------------------------------------
 // Host context
 // ------------------------------------------------------------------------------------------
@@ -2969,6 +3007,23 @@ int pt_debug_trav(unsigned long long* out5, int32_t reset) {
     return PT_OK;
 }
 #endif
+
+int pt_selftest_math(uint64_t n, uint32_t seed, uint64_t* mismatches) {
+    if (!mismatches) return pt::fail(PT_ERR_ARG, "null argument");
+    unsigned long long* d = nullptr;
+    HIP_TRY(hipMalloc(&d, sizeof *d));
+    hipError_t e = hipMemset(d, 0, sizeof *d);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_selftest_math, dim3(2048), dim3(256), 0, nullptr, n, seed, d);
+        e = hipGetLastError();
+    }
+    unsigned long long h = 0;
+    if (e == hipSuccess) e = hipMemcpy(&h, d, sizeof h, hipMemcpyDeviceToHost);   // (synchronises)
+    (void)hipFree(d);
+    if (e != hipSuccess) return pt::fail(PT_ERR_HIP, std::string("selftest: ") + hipGetErrorString(e));
+    *mismatches = h;
+    return PT_OK;
+}
 
 int pt_profile_enable(pt_ctx* c, int32_t on) {
     if (!c) return pt::fail(PT_ERR_ARG, "null context");

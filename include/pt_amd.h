@@ -231,6 +231,12 @@ int pt_profile_read(pt_ctx* c, double ms[4], uint64_t launches[4]);
  * launches of one kind overlap and busy_ms < ms. */
 int pt_profile_read_busy(pt_ctx* c, double ms[4], double busy_ms[4], uint64_t launches[4]);
 
+/* Device self-check of the range-gated correctly rounded sqrt / division cores the kernels use
+ * (pt_device.h) against hipcc's library sqrtf and '/': n operand sets from `seed` (random bit
+ * patterns over every exponent, a quarter near 1, plus zeros, denormals, infinities and NaNs).
+ * *mismatches = operations whose bits differ (NaN == NaN).  Synchronous. */
+int pt_selftest_math(uint64_t n, uint32_t seed, uint64_t* mismatches);
+
 /* ---- texture input --------------------------------------------------------------------- */
 /* Texture::load (sceneStructs.h:171-175) = stbi_load(file, &w, &h, &comp, 0) for JPEG data:
  * stb_image 2.06's JPEG decoder restated (baseline + progressive, its integer IDCT, triangle-filter
