@@ -241,6 +241,11 @@ def _pmc_leg(args, scene_path, spp_pass, sorted_, avg_ms, kernel_prefix, seg_per
         out["limiter"] = (f"VALU issue + latency, not bandwidth: waves issue {act:.0%} of their cycles, wait on "
                           f"dependencies/arbitration {wi:.0%}, on memory/LDS/barriers {wa:.0%}; fabric traffic "
                           f"{out['traffic_frac']:.0%} of the HBM peak")
+        # the bound, from the counters: the measured fabric traffic is far below the HBM peak while
+        # the waves spend their cycles issuing or waiting to issue -> issue/latency-bound (`frac`
+        # stays the prescribed 184 B / launch time / HBM peak)
+        if out["traffic_frac"] < 0.5:
+            out["bound"] = "issue"
     return out
 
 
@@ -395,7 +400,8 @@ def main() -> None:
     pemit = [b - a for a, b in zip(sp0["bounce_emit"], sp1["bounce_emit"])]
     seg_bounce = sum(plive[1:depth])
     mesh = scene.counts()[2] > 0
-    kprefix = f"k_bounce<false, {'true' if spp == 1 else 'false'}, {'true' if mesh else 'false'}>"
+    # k_bounce<FIRST, SPP1, MESH mode>: mesh scenes run mode 2 (closest mesh hit from k_traverse)
+    kprefix = f"k_bounce<false, {'true' if spp == 1 else 'false'}, {2 if mesh else 0}>"
     kernel_name = ("material-sorted pipeline (isect+hist / scan / scatter / shade+compact)" if sorted_ else kprefix)
     kernel_min = 0
     for b in range(1, depth):
