@@ -4,7 +4,7 @@ set -e
 R=$(cd "$(dirname "$0")/.." && pwd)
 B=$R/cuda_pathtracer_amd/build
 python -c "import sys; sys.path.insert(0, '$R'); from cuda_pathtracer_amd import build; build.build_native()"
-/opt/rocm/bin/hipcc -x hip --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -DPT_STAMPS ${STAMP_DEFS:-} -I $R/include \
+/opt/rocm/bin/hipcc -x hip --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-slp-vectorize -DPT_STAMPS ${STAMP_DEFS:-} -I $R/include \
     -c $R/cuda_pathtracer_amd/csrc/pt_kernels.hip -o $B/pt_kernels_stamps.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $B/libpt_amd_stamps.so $B/pt_kernels_stamps.o \
     $B/sc_kernels.hip.o $B/pt_scene.cpp.o $B/pt_mesh.cpp.o $B/pt_image.cpp.o $B/pt_jpeg.cpp.o -lz
