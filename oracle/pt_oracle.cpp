@@ -19,11 +19,20 @@
 // Under this contract the product's GPU output is bit-identical to this oracle
 // (tests/test_render_gpu.py).
 //
+// Pinned pieces (tests/test_pin_thrust.py, against rocThrust 7.2 from the system ROCm headers —
+// the third-party library the reference calls through the same Thrust API, not reference code —
+// under thrust::host and thrust::device):
+//   * oracle_u01_sequence (makeSeededRandomEngine + thrust::default_random_engine +
+//     uniform_real_distribution<float>(0,1), pathtrace.cu:57-62,197,314; interactions.cu:7,58):
+//     bit for bit over 3,900 (iteration, index, depth) keys x 8 draws;
+//   * the material order of the sort (thrust::sort_by_key with material_compare,
+//     pathtrace.cu:410-414,479-491): this file's std::stable_sort order on real per-bounce keys;
+//   * relocate_terminated_paths (thrust::stable_partition, pathtrace.cu:416-420,498-503).
 // Parity caveat ("parity unpinned" for radiance): the reference ships no renderer test or
-// golden vector that can pin these numbers; its CUDA build cannot run
-// here and compiling/running reference sources was denied.  This restatement
-// is pinned only by reading the reference source; thrust's RNG semantics are pinned by the
-// rocThrust 7.2 headers.
+// golden vector that can pin per-pixel radiance; its CUDA build cannot run
+// here and compiling/running reference sources was denied.  The geometry,
+// shading and accumulation arithmetic is pinned by reading the reference source, and the
+// radiance statistically by the reference's course render.
 #include <cfloat>
 #include <cmath>
 #include <cstdint>
