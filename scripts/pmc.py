@@ -27,6 +27,8 @@ GROUPS = {
     "write": ["WRITE_SIZE"],
     "sq": ["SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_ANY",
            "SQ_WAIT_ANY", "SQ_ACTIVE_INST_VALU", "GRBM_GUI_ACTIVE"],
+    "l2": ["TCC_HIT_sum", "TCC_MISS_sum"],                       # L2 hit rate (per-XCD L2s summed)
+    "vmem": ["SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR", "SQ_INSTS_LDS", "SQ_INSTS_BRANCH"],
 }
 
 
