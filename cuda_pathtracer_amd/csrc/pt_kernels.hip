@@ -1610,23 +1610,28 @@ __global__ __launch_bounds__(kBlock) void k_compact_paths(const KArgs A) {
 // Material-sorted pipeline (sortbyMaterial): per bounce one producer launch, a histogram scan and
 // one scatter.
 //   k_sort_produce  shades the paths of bounce b in sorted order (gathered through perm; RNG key =
-//                   sorted index within the iteration, pathtrace.cu:315), compacts the survivors into
-//                   per-iteration segments exactly like k_bounce, and INTERSECTS each survivor's new
-//                   ray right away (the sort key of bounce b + 1): the survivor's 64-byte record is
-//                   written once, with its hit.  The first bounce's producer generates the camera
-//                   rays instead of shading.  Sort keys are counted per PRODUCER TILE (the 256 input
-//                   paths one workgroup step handles, whose survivors are a contiguous run of the
-//                   output): hist[iteration][material][tile of that iteration], and every survivor
-//                   gets its rank among the same-material survivors of its tile;
+//                   sorted index within the iteration, pathtrace.cu:315) and INTERSECTS each
+//                   survivor's new ray right away (the sort key of bounce b + 1): the survivor's
+//                   64-byte record is written once, with its hit.  The first bounce's producer
+//                   generates the camera rays instead of shading.
+//                   Work unit = TILE: 256 consecutive positions of one iteration's sorted range.
+//                   Tile t's survivors go, in order, to slots [256 t, 256 t + count_t) (tcnt[t]), so
+//                   the survivors' logical order is the tile order — stable.  Workgroups take
+//                   tiles t = b, b + G, b + 2G, ... (G = grid): every workgroup walks the sorted
+//                   order in step with the others, so the records being gathered at any moment
+//                   belong to one or two iterations (one iteration's records at bounce 1: 20 k tiles
+//                   x 16 KiB = 133 MB at 1920x1080, within the 256 MiB Infinity Cache) instead of
+//                   every iteration of the pass at once.
+//                   Sort keys are counted per tile: hist[iteration][material][tile of that
+//                   iteration], and every survivor gets its rank among the same-material survivors
+//                   of its tile (one ballot per material present in the wave);
 //   scan            of the histogram (k_hist_sums / k_hist_scan_sums / k_hist_apply, no co-residency
 //                   needed): tiles are in logical order, so hist's flat exclusive scan + the in-tile
 //                   rank IS the survivor's position in the stable sort by (iteration, material);
 //   k_sort_scatter  perm[sorted position] = physical slot.
 // Batched passes sort every iteration on its own (stable sort by (iteration, material), as `spp`
-// sequential pathtrace() calls would): an iteration's tiles form one block of the histogram.
-// Compared with a separate intersect launch that re-reads every record and writes its hit back,
-// this moves each record across HBM twice per bounce (one gathered read, one write) instead of four
-// times, and the histogram has one entry per 256 paths and material instead of one per 64.
+// sequential pathtrace() calls would): tiles never span two iterations, and an iteration's tiles
+// form one block of the histogram.
 // Path j of the sorted pipeline is ONE 64-byte record, so the gather reads one 64-byte span:
 //   r0 = (o.xyz, d.x)   r1 = (d.yz, c.rg)   r2 = (c.b, slot, t, material)   r3 = (n.xyz, 0)
 // `bounces` is not stored: every path entering bounce b has b bounces behind it.  Texture
@@ -1634,29 +1639,40 @@ __global__ __launch_bounds__(kBlock) void k_compact_paths(const KArgs A) {
 __device__ __forceinline__ v4f* srec(const PathSoA& B, int j) { return B.a + ((size_t)(uint32_t)j << 2); }
 
 struct SortArgs {
-    int32_t* kr;        // [cap] per output slot: material << 24 | producer tile << 8 | rank in (tile, material)
-    int32_t* hist;      // per (iteration, material, producer tile) survivor counts (sort_hidx)
+    int32_t* kr;        // [cap] per output slot: material << 24 | rank in (tile, material)
+    int32_t* tcnt;      // [cap / 256] survivors of each tile
+    int32_t* hist;      // per (iteration, material, tile) survivor counts (sort_hidx)
     int32_t* offs;      // its exclusive scan
     int32_t* perm;      // [P] sorted position -> physical slot
-    int32_t* iseg0;     // [2][kMaxSpp + 1] per parity: first segment of each iteration ([spp] = nseg)
+    int32_t* itb;       // [2][kMaxSpp + 1] per parity: first tile of each iteration ([spp] = tiles)
     float* uv_out;      // textured scenes: (u, v) of the output records ([2 * cap])
 };
 constexpr int kSortMaxMats = 64;   // one lane per material in the per-tile counts (else: no sorting)
 
-// Histogram entry of producer tile k of segment s for material m, the iteration's segments being
-// [s0, s1) of tpb tiles each: [iteration block][material][tile of the iteration].
-__device__ __forceinline__ size_t sort_hidx(int s0, int s1, int tpb, int nmats, int s, int k, int m) {
-    return (size_t)s0 * tpb * nmats + (size_t)m * (size_t)(s1 - s0) * tpb + (size_t)(s - s0) * tpb + k;
+// Histogram entry of tile t (iteration tiles [t0, t1)) for material m: [iteration block][material][tile].
+__device__ __forceinline__ size_t sort_hidx(int t0, int t1, int nmats, int t, int m) {
+    return (size_t)t0 * nmats + (size_t)m * (size_t)(t1 - t0) + (size_t)(t - t0);
+}
+// Iteration owning tile t: the last it with s_tb[it] <= t (empty iterations own no tile).
+__device__ __forceinline__ int tile_iteration(const int32_t* s_tb, int spp, int t) {
+    int lo = 0, hi = spp - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (s_tb[mid] <= t) lo = mid; else hi = mid - 1;
+    }
+    return lo;
 }
 
+#ifndef PT_PRODUCE_WAVES
+#define PT_PRODUCE_WAVES 1   // (A/B knob: minimum waves per SIMD of the analytic producer)
+#endif
 template <bool FIRST, bool SPP1, bool MESH>
-__global__ __launch_bounds__(kBlock) void k_sort_produce(const KArgs A, const SortArgs SA) {
+__global__ __launch_bounds__(kBlock, MESH ? 1 : PT_PRODUCE_WAVES) void k_sort_produce(const KArgs A, const SortArgs SA) {
     __shared__ DMaterial s_mats[kLdsMats];
     __shared__ LGeom s_geoms[MESH ? 1 : kLdsGeoms];
-    __shared__ int32_t s_sb[kMaxSpp + 1];      // input: sorted start of every iteration (first: j * npix)
-    __shared__ int32_t s_first[kMaxSpp + 1];   // output: first segment of every iteration ([spp] = nseg)
-    __shared__ int32_t s_lay[4];
-    __shared__ uint32_t s_tmp[12];
+    __shared__ int32_t s_sb[kMaxSpp + 1];      // sorted start of every iteration (first bounce: j * npix)
+    __shared__ int32_t s_tb[kMaxSpp + 1];      // first tile of every iteration ([spp] = all tiles)
+    __shared__ uint32_t s_tmp[8];
     __shared__ uint32_t s_wc[2][4];
     __shared__ uint32_t s_kc[2][4][kSortMaxMats];   // per wave: survivors of each material in the tile
     __shared__ uint32_t s_cnt;
@@ -1666,47 +1682,50 @@ __global__ __launch_bounds__(kBlock) void k_sort_produce(const KArgs A, const So
     const int nmats = A.S.nmats;
     if (FIRST) {
         for (int j = tid; j <= spp; j += kBlock) s_sb[j] = j * A.tile.npix;
-    } else {   // the scanned histogram at each iteration's first entry
-        const int tpb_in = (int)(A.ctl[par].chunk / kBlock);
-        const int32_t* is0 = SA.iseg0 + (size_t)par * (kMaxSpp + 1);
-        for (int j = tid; j <= spp; j += kBlock) s_sb[j] = SA.offs[(size_t)is0[j] * tpb_in * nmats];
+    } else {   // the scanned histogram at each iteration's first entry (the previous producer's tiles)
+        const int32_t* tb_in = SA.itb + (size_t)par * (kMaxSpp + 1);
+        for (int j = tid; j <= spp; j += kBlock) s_sb[j] = SA.offs[(size_t)tb_in[j] * nmats];
     }
     __syncthreads();
-    plan_layout(s_sb, spp, (int)gridDim.x, (int)blockIdx.x, s_lay, s_tmp, s_first);
-    const int tpb = __builtin_amdgcn_readfirstlane(s_lay[0]);
-    const int nseg = __builtin_amdgcn_readfirstlane(s_lay[1]);
-    const int my_it = __builtin_amdgcn_readfirstlane(s_lay[2]);
-    const int my_c = __builtin_amdgcn_readfirstlane(s_lay[3]);
-    const int chunk = tpb * kBlock;
+    {   // this launch's tiles: iteration it owns ceil(n_it / 256) of them, from s_tb[it]
+        const uint32_t n = tid < spp ? (uint32_t)(s_sb[tid + 1] - s_sb[tid] + kBlock - 1) / kBlock : 0u;
+        const uint32_t incl = lb::wave_inclusive_scan(n);
+        if (lane == 63) s_tmp[wave] = incl;
+        __syncthreads();
+        uint32_t pre = incl - n;
+        for (int q = 0; q < wave; ++q) pre += s_tmp[q];
+        if (tid < spp) s_tb[tid] = (int32_t)pre;
+        if (tid == 0) s_tb[spp] = (int32_t)(s_tmp[0] + s_tmp[1] + s_tmp[2] + s_tmp[3]);
+        __syncthreads();
+    }
+    const int T = __builtin_amdgcn_readfirstlane(s_tb[spp]);
     if (blockIdx.x == 0) {
         if (tid == 0) {
-            A.ctl[par ^ 1].nseg = (uint32_t)nseg;
-            A.ctl[par ^ 1].chunk = (uint32_t)chunk;
-            A.ctl[par ^ 1].hist_live = (uint32_t)(nseg * tpb * nmats + 1);   // entries + the end offset
+            A.ctl[par ^ 1].nseg = (uint32_t)T;   // tiles of the output
+            A.ctl[par ^ 1].chunk = (uint32_t)kBlock;
+            A.ctl[par ^ 1].hist_live = (uint32_t)(T * nmats + 1);   // entries + the end offset
         }
-        int32_t* os0 = SA.iseg0 + (size_t)(par ^ 1) * (kMaxSpp + 1);
-        for (int j = tid; j <= spp; j += kBlock) os0[j] = s_first[j];
+        int32_t* tb_out = SA.itb + (size_t)(par ^ 1) * (kMaxSpp + 1);
+        for (int j = tid; j <= spp; j += kBlock) tb_out[j] = s_tb[j];
         if (!FIRST) count_bounce(A, s_sb[spp]);   // the live paths of bounce b, shaded here
     }
-    if (my_it < 0) return;
+    if ((int)blockIdx.x >= T) return;
     if (!MESH) stage_geoms(A.S, s_geoms);
     stage_materials(A, s_mats);
     const bool lds_mats = nmats <= kLdsMats;
-    const int it_base = __builtin_amdgcn_readfirstlane(s_sb[my_it]);
-    const int first = it_base + my_c * chunk;
-    const int last = min(__builtin_amdgcn_readfirstlane(s_sb[my_it + 1]), first + chunk);
-    const int iter = A.tile.iter_first + my_it;
-    const int s0 = __builtin_amdgcn_readfirstlane(s_first[my_it]);
-    const int s1 = __builtin_amdgcn_readfirstlane(s_first[my_it + 1]);
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    uint32_t kept = 0, emit_cnt = 0;
+    uint32_t emit_cnt = 0;
     int k = 0;
-    for (int base = first; base < last; base += kBlock, ++k) {
-        const int idx = base + tid;
+    for (int t = (int)blockIdx.x; t < T; t += (int)gridDim.x, ++k) {
+        const int it = tile_iteration(s_tb, spp, t);
+        const int t0 = s_tb[it], t1 = s_tb[it + 1];
+        const int it_base = s_sb[it];
+        const int idx = it_base + (t - t0) * kBlock + tid;   // sorted position
+        const int iter = A.tile.iter_first + it;
         bool alive = false, emitted = false;
         PathReg p;
         Hit h;
-        if (idx < last) {
+        if (idx < s_sb[it + 1]) {
             if (FIRST) {
                 raygen(A.cam, A.fl, A.tile, idx, p);
                 alive = true;
@@ -1764,7 +1783,7 @@ __global__ __launch_bounds__(kBlock) void k_sort_produce(const KArgs A, const So
         if (alive) {
             uint32_t kb = krank;
             for (int w = 0; w < wave; ++w) kb += s_kc[k & 1][w][key];
-            const int q = (int)blockIdx.x * chunk + (int)(kept + before + rank);
+            const int q = t * kBlock + (int)(before + rank);
             v4f* r = srec(A.out, q);
             r[0] = v4f{p.o.x, p.o.y, p.o.z, p.d.x};
             r[1] = v4f{p.d.y, p.d.z, p.c.x, p.c.y};
@@ -1774,59 +1793,53 @@ __global__ __launch_bounds__(kBlock) void k_sort_produce(const KArgs A, const So
                 SA.uv_out[2 * (size_t)q] = h.u;
                 SA.uv_out[2 * (size_t)q + 1] = h.v;
             }
-            SA.kr[q] = (int32_t)(((uint32_t)key << 24) | ((uint32_t)k << 8) | kb);
+            SA.kr[q] = (int32_t)(((uint32_t)key << 24) | kb);
         }
-        if (wave == 0 && lane < nmats)
-            SA.hist[sort_hidx(s0, s1, tpb, nmats, (int)blockIdx.x, k, lane)] =
-                (int32_t)((s_kc[k & 1][0][lane] + s_kc[k & 1][1][lane]) + (s_kc[k & 1][2][lane] + s_kc[k & 1][3][lane]));
-        kept += (w0 + w1) + (w2 + w3);
+        if (wave == 0) {
+            if (lane < nmats)
+                SA.hist[sort_hidx(t0, t1, nmats, t, lane)] =
+                    (int32_t)((s_kc[k & 1][0][lane] + s_kc[k & 1][1][lane]) + (s_kc[k & 1][2][lane] + s_kc[k & 1][3][lane]));
+            if (lane == 0) SA.tcnt[t] = (int32_t)((w0 + w1) + (w2 + w3));
+        }
     }
-    for (int e = tid; e < (tpb - k) * nmats; e += kBlock)   // this segment's tiles past its last: empty
-        SA.hist[sort_hidx(s0, s1, tpb, nmats, (int)blockIdx.x, k + e / nmats, e % nmats)] = 0;
-    if (tid == 0) A.seg[(size_t)(par ^ 1) * kMaxSeg + blockIdx.x] = (int32_t)(kept | ((uint32_t)my_it << kSegItShift));
     flush_emissive(A, emit_cnt, &s_cnt);
 }
 
-// perm[sorted position] = physical slot, for every survivor in the producer's segments (256-slot
-// blocks of the segments, grid-stride; blocks past a segment's count are empty).
+// perm[sorted position] = physical slot, for every survivor in the producer's tiles (grid-stride
+// over the tiles; a tile's slots past its survivor count are empty).
 __global__ __launch_bounds__(kBlock) void k_sort_scatter(const KArgs A, const SortArgs SA) {
+    __shared__ int32_t s_tb[kMaxSpp + 1];
     const int par = A.parity;
     const int nmats = A.S.nmats;
-    const int nseg = (int)A.ctl[par].nseg, chunk = (int)A.ctl[par].chunk;
-    const int tpb = chunk / kBlock;
-    const int32_t* is0 = SA.iseg0 + (size_t)par * (kMaxSpp + 1);
-    const uint32_t* words = reinterpret_cast<const uint32_t*>(A.seg) + (size_t)par * kMaxSeg;
-    // kU blocks per step, their loads issued together (each slot is kr -> offs -> store, dependent)
+    const int spp = A.tile.spp;
+    const int T = (int)A.ctl[par].nseg;
+    const int32_t* tb = SA.itb + (size_t)par * (kMaxSpp + 1);
+    for (int j = threadIdx.x; j <= spp; j += kBlock) s_tb[j] = tb[j];
+    __syncthreads();
+    // kU tiles per step, their loads issued together (each slot is kr -> offs -> store, dependent)
     constexpr int kU = 4;
-    const int nblk = nseg * tpb, G = (int)gridDim.x;
-    for (int blk0 = (int)blockIdx.x; blk0 < nblk; blk0 += kU * G) {
-        int q[kU], nt[kU];
+    const int G = (int)gridDim.x;
+    for (int t0 = (int)blockIdx.x; t0 < T; t0 += kU * G) {
+        int q[kU];
         size_t hb[kU];
+        int nt[kU];
         uint32_t kr[kU];
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
-            const int blk = blk0 + u * G;
+            const int t = t0 + u * G;
             q[u] = -1;
-            if (blk < nblk) {
-                const int s = blk / tpb;
-                const uint32_t w = words[s];
-                const int cnt = (int)(w & kSegCountMask), it = (int)(w >> kSegItShift);
-                const int j = (blk - s * tpb) * kBlock + (int)threadIdx.x;
-                if (j < cnt) {
-                    q[u] = s * chunk + j;
-                    hb[u] = sort_hidx(is0[it], is0[it + 1], tpb, nmats, s, 0, 0);   // + key * nt + tile
-                    nt[u] = (is0[it + 1] - is0[it]) * tpb;
-                    kr[u] = (uint32_t)SA.kr[q[u]];
-                }
+            if (t < T && (int)threadIdx.x < SA.tcnt[t]) {
+                const int it = tile_iteration(s_tb, spp, t);
+                q[u] = t * kBlock + (int)threadIdx.x;
+                hb[u] = sort_hidx(s_tb[it], s_tb[it + 1], nmats, t, 0);   // + key * nt
+                nt[u] = s_tb[it + 1] - s_tb[it];
+                kr[u] = (uint32_t)SA.kr[q[u]];
             }
         }
         int dst[kU];
 #pragma unroll
         for (int u = 0; u < kU; ++u)
-            if (q[u] >= 0) {
-                const int key = (int)(kr[u] >> 24), kt = (int)((kr[u] >> 8) & 0xffffu);
-                dst[u] = SA.offs[hb[u] + (size_t)key * (size_t)nt[u] + kt] + (int)(kr[u] & 255u);
-            }
+            if (q[u] >= 0) dst[u] = SA.offs[hb[u] + (size_t)(kr[u] >> 24) * (size_t)nt[u]] + (int)(kr[u] & 0xffffffu);
 #pragma unroll
         for (int u = 0; u < kU; ++u)
             if (q[u] >= 0) SA.perm[dst[u]] = q[u];
@@ -2049,7 +2062,7 @@ struct pt_ctx {
     hipStream_t lane_stream = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     struct SortSet {   // material-sort buffers of one lane (k_sort_produce / k_sort_scatter)
-        int32_t *kr = nullptr, *hist = nullptr, *offs = nullptr, *perm = nullptr, *iseg0 = nullptr;
+        int32_t *kr = nullptr, *tcnt = nullptr, *hist = nullptr, *offs = nullptr, *perm = nullptr, *itb = nullptr;
         float* uv[2] = {nullptr, nullptr};   // (u, v) of the records in buf[0] / buf[1]
         uint32_t* sums = nullptr;            // histogram scan: tile sums
         int64_t hist_cap = 0;                // histogram entries allocated (+ the end offset)
@@ -2701,7 +2714,8 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
         if (int rc = c->alloc(&ss.perm, paths)) return bail(rc);
         if (int rc = c->alloc(&ss.hist, (size_t)ss.hist_cap)) return bail(rc);
         if (int rc = c->alloc(&ss.offs, (size_t)ss.hist_cap)) return bail(rc);
-        if (int rc = c->alloc(&ss.iseg0, 2 * ((size_t)kMaxSpp + 1))) return bail(rc);
+        if (int rc = c->alloc(&ss.itb, 2 * ((size_t)kMaxSpp + 1))) return bail(rc);
+        if (int rc = c->alloc(&ss.tcnt, cap / kBlock + 1)) return bail(rc);
         if (int rc = c->alloc(&ss.sums, tiles)) return bail(rc);
         if (!S.textures.empty())
             for (int h = 0; h < 2; ++h)
@@ -2762,7 +2776,7 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
             a.in = bufs[lcur];
             a.out = bufs[lcur ^ 1];
             a.hit.uv = ss.uv[lcur];
-            const SortArgs sa{ss.kr, ss.hist, ss.offs, ss.perm, ss.iseg0, ss.uv[lcur ^ 1]};
+            const SortArgs sa{ss.kr, ss.tcnt, ss.hist, ss.offs, ss.perm, ss.itb, ss.uv[lcur ^ 1]};
             hipLaunchKernelGGL(produce_kernel(first, spp1, mesh), dim3(c->grid_bounce[0]), dim3(kBlock), 0, s, a, sa);
             HIP_TRY(hipGetLastError());
             ++lc;
@@ -2778,7 +2792,7 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
         hipLaunchKernelGGL(k_hist_scan_sums, dim3(1), dim3(kBlock), 0, s, ss.sums, ss.hist_cap, nlive);
         hipLaunchKernelGGL(k_hist_apply, dim3(tiles), dim3(kBlock), 0, s, (const int32_t*)ss.hist, ss.offs, ss.hist_cap,
                            nlive, (const uint32_t*)ss.sums);
-        const SortArgs sa{ss.kr, ss.hist, ss.offs, ss.perm, ss.iseg0, nullptr};
+        const SortArgs sa{ss.kr, ss.tcnt, ss.hist, ss.offs, ss.perm, ss.itb, nullptr};
         hipLaunchKernelGGL(k_sort_scatter, dim3(c->grid_trace), dim3(kBlock), 0, s, a, sa);
         HIP_TRY(hipGetLastError());
         if (int rc = produce(false)) return rc;
