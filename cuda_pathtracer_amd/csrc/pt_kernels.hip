@@ -1647,7 +1647,7 @@ struct SortArgs {
     int32_t* itb;       // [2][kMaxSpp + 1] per parity: first tile of each iteration ([spp] = tiles)
     float* uv_out;      // textured scenes: (u, v) of the output records ([2 * cap])
 };
-constexpr int kSortMaxMats = 64;   // one lane per material in the per-tile counts (else: no sorting)
+constexpr int kSortMaxMats = 256;  // per-tile material counts in LDS; the material is 8 bits of kr
 
 // Histogram entry of tile t (iteration tiles [t0, t1)) for material m: [iteration block][material][tile].
 __device__ __forceinline__ size_t sort_hidx(int t0, int t1, int nmats, int t, int m) {
@@ -1674,7 +1674,8 @@ __global__ __launch_bounds__(kBlock, MESH ? 1 : PT_PRODUCE_WAVES) void k_sort_pr
     __shared__ int32_t s_tb[kMaxSpp + 1];      // first tile of every iteration ([spp] = all tiles)
     __shared__ uint32_t s_tmp[8];
     __shared__ uint32_t s_wc[2][4];
-    __shared__ uint32_t s_kc[2][4][kSortMaxMats];   // per wave: survivors of each material in the tile
+    extern __shared__ uint32_t s_kc[];   // [2][4][nmats] (dynamic): per wave, survivors of each material in the tile
+#define KC(buf, w, m) s_kc[((buf) * 4 + (w)) * nmats + (m)]
     __shared__ uint32_t s_cnt;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int par = A.parity;
@@ -1764,25 +1765,30 @@ __global__ __launch_bounds__(kBlock, MESH ? 1 : PT_PRODUCE_WAVES) void k_sort_pr
         emit_cnt += (uint32_t)__popcll(__ballot(emitted));
         const uint64_t m = __ballot(alive);
         const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        // per material present: one ballot -> in-wave rank (lanes of that key) and count (lane == key)
-        uint32_t krank = 0, kcnt = 0;
+        // this wave's row of per-material counts: cleared, then one ballot per material present ->
+        // in-wave rank (lanes of that key) and the count (written by the first lane of the key).
+        // Buffer k&1 was last read two tiles ago, before the previous barrier; a wave's LDS
+        // writes land in order.
+#pragma unroll
+        for (int q = 0; q < kSortMaxMats / 64; ++q)   // (fixed trip count: a dynamic loop here cost 34 VGPRs)
+            if (lane + 64 * q < nmats) KC(k & 1, wave, lane + 64 * q) = 0u;
+        uint32_t krank = 0;
         uint64_t rem = m;
         while (rem) {
             const int src = __builtin_ctzll(rem);
             const int kk = __builtin_amdgcn_readlane(key, src);
             const uint64_t mk = __ballot(key == kk);
             if (key == kk) krank = (uint32_t)__popcll(mk & lt);
-            if (lane == kk) kcnt = (uint32_t)__popcll(mk);
+            if (lane == src) KC(k & 1, wave, kk) = (uint32_t)__popcll(mk);
             rem &= ~mk;
         }
-        if (lane < nmats) s_kc[k & 1][wave][lane] = kcnt;
         if (lane == 0) s_wc[k & 1][wave] = (uint32_t)__popcll(m);
         __syncthreads();
         const uint32_t w0 = s_wc[k & 1][0], w1 = s_wc[k & 1][1], w2 = s_wc[k & 1][2], w3 = s_wc[k & 1][3];
         const uint32_t before = (wave > 0 ? w0 : 0u) + (wave > 1 ? w1 : 0u) + (wave > 2 ? w2 : 0u);
         if (alive) {
             uint32_t kb = krank;
-            for (int w = 0; w < wave; ++w) kb += s_kc[k & 1][w][key];
+            for (int w = 0; w < wave; ++w) kb += KC(k & 1, w, key);
             const int q = t * kBlock + (int)(before + rank);
             v4f* r = srec(A.out, q);
             r[0] = v4f{p.o.x, p.o.y, p.o.z, p.d.x};
@@ -1795,14 +1801,16 @@ __global__ __launch_bounds__(kBlock, MESH ? 1 : PT_PRODUCE_WAVES) void k_sort_pr
             }
             SA.kr[q] = (int32_t)(((uint32_t)key << 24) | kb);
         }
-        if (wave == 0) {
-            if (lane < nmats)
-                SA.hist[sort_hidx(t0, t1, nmats, t, lane)] =
-                    (int32_t)((s_kc[k & 1][0][lane] + s_kc[k & 1][1][lane]) + (s_kc[k & 1][2][lane] + s_kc[k & 1][3][lane]));
-            if (lane == 0) SA.tcnt[t] = (int32_t)((w0 + w1) + (w2 + w3));
+        {   // the tile's histogram entries: wave w writes materials 64 w .. 64 w + 63
+            const int mm = wave * 64 + lane;
+            if (mm < nmats)
+                SA.hist[sort_hidx(t0, t1, nmats, t, mm)] =
+                    (int32_t)((KC(k & 1, 0, mm) + KC(k & 1, 1, mm)) + (KC(k & 1, 2, mm) + KC(k & 1, 3, mm)));
+            if (tid == 0) SA.tcnt[t] = (int32_t)((w0 + w1) + (w2 + w3));
         }
     }
     flush_emissive(A, emit_cnt, &s_cnt);
+#undef KC
 }
 
 // perm[sorted position] = physical slot, for every survivor in the producer's tiles (grid-stride
@@ -2777,7 +2785,8 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
             a.out = bufs[lcur ^ 1];
             a.hit.uv = ss.uv[lcur];
             const SortArgs sa{ss.kr, ss.tcnt, ss.hist, ss.offs, ss.perm, ss.itb, ss.uv[lcur ^ 1]};
-            hipLaunchKernelGGL(produce_kernel(first, spp1, mesh), dim3(c->grid_bounce[0]), dim3(kBlock), 0, s, a, sa);
+            hipLaunchKernelGGL(produce_kernel(first, spp1, mesh), dim3(c->grid_bounce[0]), dim3(kBlock),
+                               (size_t)8 * c->nmats * sizeof(uint32_t), s, a, sa);
             HIP_TRY(hipGetLastError());
             ++lc;
             lcur ^= 1;
@@ -2799,7 +2808,7 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
         return prof_end(ev, s);
     };
     if (sorted && c->nmats > kSortMaxMats)
-        return pt::fail(PT_ERR_ARG, "material-sorted shading supports at most 64 materials");
+        return pt::fail(PT_ERR_ARG, "material-sorted shading supports at most 256 materials");
     if (!sorted && c->fused && mmode == kMeshPre)   // k_traverse's per-bounce ray tickets (both lanes)
         HIP_TRY(hipMemsetAsync(c->tq, 0, 2 * 64 * sizeof(uint32_t), st));
     if (laned) {

@@ -120,15 +120,22 @@ def random_triangles(out_dir, n=100_000, res=(3840, 2160), depth=32, seed=5) -> 
     return _write(out_dir, name, scene)
 
 
-def random_primitives(out_dir, n=24, res=(640, 480), depth=8, seed=7) -> str:
+def random_primitives(out_dir, n=24, res=(640, 480), depth=8, seed=7, extra_materials=0) -> str:
     """Stress scene for the bounded closest-hit pass (not a BASELINE workload): the Cornell shell
     plus n cubes and spheres with random rotations and strongly non-uniform scales (thin slabs,
-    needles), overlapping each other and the walls; diffuse, mirror and glass materials."""
+    needles), overlapping each other and the walls; diffuse, mirror and glass materials.
+    `extra_materials` adds that many diffuse/mirror materials used round-robin (material-sort width)."""
     rng = np.random.default_rng(seed)
     mats = dict(CORNELL_MATERIALS)
     mats["glass"] = {"TYPE": "Refractive", "RGB": [0.98, 0.98, 0.98], "SPECRGB": [0.98, 0.98, 0.98],
                      "REFRACTIVE": 1.0, "IOR": 1.5}
     cycle = ["diffuse_white", "specular_white", "glass", "diffuse_red", "diffuse_green"]
+    for k in range(extra_materials):
+        c = [float(v) for v in rng.uniform(0.2, 0.95, 3)]
+        mats[f"m{k:03d}"] = ({"TYPE": "Diffuse", "RGB": c} if k % 3 else
+                             {"TYPE": "Specular", "RGB": c, "SPECRGB": c, "REFLECTIVE": 0.5})
+    if extra_materials:
+        cycle = [f"m{k:03d}" for k in range(extra_materials)] + cycle
     objs = _room()
     for k in range(n):
         scale = np.exp(rng.uniform(np.log(0.02), np.log(4.0), 3))
@@ -139,7 +146,7 @@ def random_primitives(out_dir, n=24, res=(640, 480), depth=8, seed=7) -> str:
                      "ROTAT": [float(v) for v in rng.uniform(0.0, 360.0, 3)],
                      "SCALE": [float(v) for v in scale]})
     scene = {"Materials": mats, "Camera": _camera(res, depth, 5000, "random_primitives"), "Objects": objs}
-    return _write(out_dir, f"random_primitives_{seed}", scene)
+    return _write(out_dir, f"random_primitives_{seed}" + (f"_m{extra_materials}" if extra_materials else ""), scene)
 
 
 CONFIGS = {

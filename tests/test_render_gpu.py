@@ -384,6 +384,19 @@ def test_mesh_traversal_modes_bitexact(room_path, config_scenes, monkeypatch, in
     assert r.sum() > 0
 
 
+@pytest.mark.parametrize("nmat", [70, 200])
+def test_sorted_many_materials_bitexact(tmp_path, nmat):
+    """Material-sorted shading with more materials than a wave has lanes (the per-tile counts live
+    in LDS rows of nmats entries): 70 and 200 materials over 120 objects, spp 1 and 3 (two lanes),
+    bit-exact against the oracle's stable sort."""
+    from cuda_pathtracer_amd import Scene, scenes
+    path = scenes.random_primitives(tmp_path, n=120, res=(48, 36), seed=3, extra_materials=nmat)
+    for spp in (1, 3):
+        g, r, _, _ = _run(Scene(path), O.OracleScene.from_json(path), _gui(sortbyMaterial=True), iters=3, spp=spp)
+        _assert_bitexact(g, r, f"{nmat} materials spp={spp}")
+        assert r.sum() > 0
+
+
 @pytest.mark.parametrize("rows", ["1", "3"])
 def test_mesh_traversal_stack_spill_bitexact(room_path, config_scenes, monkeypatch, rows):
     """k_traverse keeps the first PT_AMD_STACK_ROWS stack entries per lane in LDS and the rest in
