@@ -1074,6 +1074,10 @@ __global__ __launch_bounds__(kBlock) void k_iter_bases(const KArgs A) {
 // need not be co-resident and shared GPUs need no claimed schedule.
 constexpr int kMaxSeg = 2048;
 constexpr int kMaxSpp = kBlock;   // batch iterations per pass (pt_shard.spp): one thread each
+constexpr int kMaxLanes = 4;      // lanes of a batched pass (pt_ctx::lanes; PT_AMD_LANES)
+constexpr int kDefaultLanes = 2;
+// Iterations of lane l when `spp` are split over `lanes`: the first spp % lanes lanes take one more.
+inline int lane_iters(int spp, int lanes, int l) { return spp / lanes + (l < spp % lanes ? 1 : 0); }
 
 // Segment words of k_bounce: survivor count | batch iteration << 24 (pt_create bounds chunk < 2^24).
 constexpr int kSegItShift = 24;
@@ -2061,24 +2065,24 @@ struct pt_ctx {
     // lane_stream with its own path buffers and control words.  The lanes are independent (every
     // path's RNG keys and colour slot depend only on its iteration), so one lane's first bounce,
     // short tail bounces and launch gaps overlap the other's work.  PT_AMD_LANES=1 disables.
-    int lanes = 1;
-    PathSoA lbuf[2]{};
-    Ctl* lctl = nullptr;
-    int32_t* lseg = nullptr;
-    unsigned long long* lemit = nullptr;
-    uint64_t llaunches = 0;
-    hipStream_t lane_stream = nullptr;
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    int lanes = 1;                       // lanes 1.. use the arrays below; lane 0 the context's own
+    PathSoA lbuf[kMaxLanes][2]{};
+    Ctl* lctl[kMaxLanes] = {};
+    int32_t* lseg[kMaxLanes] = {};
+    unsigned long long* lemit[kMaxLanes] = {};
+    uint64_t llaunches[kMaxLanes] = {};
+    hipStream_t lane_stream[kMaxLanes] = {};
+    hipEvent_t ev_fork = nullptr, ev_join[kMaxLanes] = {};
     struct SortSet {   // material-sort buffers of one lane (k_sort_produce / k_sort_scatter)
         int32_t *kr = nullptr, *tcnt = nullptr, *hist = nullptr, *offs = nullptr, *perm = nullptr, *itb = nullptr;
         float* uv[2] = {nullptr, nullptr};   // (u, v) of the records in buf[0] / buf[1]
         uint32_t* sums = nullptr;            // histogram scan: tile sums
         int64_t hist_cap = 0;                // histogram entries allocated (+ the end offset)
-    } sset[2];
+    } sset[kMaxLanes];
     // Mesh scenes: the BVH walk runs in k_traverse ahead of k_bounce<.., kMeshPre> (mesh_mode 2) when
     // the BVH is on and the geom table fits LDS; otherwise inside k_bounce (kMeshInline).
-    v4f* mhit[2] = {nullptr, nullptr};   // per lane, indexed by physical path slot
-    size_t lcap[2] = {0, 0};             // path capacity of each lane's buffers
+    v4f* mhit[kMaxLanes] = {};           // per lane, indexed by physical path slot
+    size_t lcap[kMaxLanes] = {};         // path capacity of each lane's buffers
     bool mesh_inline = false;            // PT_AMD_MESH_INLINE=1 at pt_create: always kMeshInline
     uint32_t* tq = nullptr;              // k_traverse ray tickets: [lane][bounce], zeroed per pass
     int grid_traverse = 0;               // k_traverse: one resident wave of workgroups
@@ -2095,8 +2099,10 @@ struct pt_ctx {
         }
         if (fin_stream) (void)hipStreamDestroy(fin_stream);
         if (ev_fork) (void)hipEventDestroy(ev_fork);
-        if (ev_join) (void)hipEventDestroy(ev_join);
-        if (lane_stream) (void)hipStreamDestroy(lane_stream);
+        for (int l = 0; l < kMaxLanes; ++l) {
+            if (ev_join[l]) (void)hipEventDestroy(ev_join[l]);
+            if (lane_stream[l]) (void)hipStreamDestroy(lane_stream[l]);
+        }
         for (void* p : allocs) (void)hipFree(p);
     }
     template <typename T>
@@ -2642,7 +2648,7 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
     if (const char* mi = std::getenv("PT_AMD_MESH_INLINE")) c->mesh_inline = std::strcmp(mi, "1") == 0;
     if (A.S.nnodes > 0) {   // k_traverse records (mesh mode 2), tickets, stack depth and grid
         if (int rc = c->alloc(&c->mhit[0], c->path_cap)) return bail(rc);
-        if (int rc = c->alloc(&c->tq, 2 * 64)) return bail(rc);
+        if (int rc = c->alloc(&c->tq, (size_t)kMaxLanes * 64)) return bail(rc);
         A.stack_rows = std::min(A.S.bvh_depth + 2, kTravLdsRows);
         if (const char* sr = std::getenv("PT_AMD_STACK_ROWS")) A.stack_rows = std::max(1, std::min(64, std::atoi(sr)));
         int per_cu = 0;
@@ -2680,28 +2686,33 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
         return bail(pt::fail(PT_ERR_HIP, std::string("hipMemset: ") + hipGetErrorString(e)));
     A.max_tiles = c->max_tiles;
     A.count_pass = 1;
-    {
+    {   // lanes 1..L-1: each its own path buffers, control words, emissive slots and stream
         const char* lv = std::getenv("PT_AMD_LANES");
-        if (sh.spp >= 2 && !(lv && std::atoi(lv) == 1)) {   // lane 1: floor(spp / 2) iterations
-            const int n1 = sh.spp / 2;
-            size_t cap1 = 0;
-            if (int rc = path_cap((long long)n1 * (long long)npix, n1, &cap1)) return bail(rc);
-            for (int b = 0; b < 2; ++b)
-                if (int rc = alloc_paths(c, c->lbuf[b], cap1)) return bail(rc);
-            c->lcap[1] = cap1;
-            if (c->mhit[0])
-                if (int rc = c->alloc(&c->mhit[1], cap1)) return bail(rc);
-            if (int rc = c->alloc(&c->lctl, 2)) return bail(rc);
-            if (int rc = c->alloc(&c->lseg, (size_t)2 * kMaxSeg)) return bail(rc);
-            if (int rc = c->alloc(&c->lemit, (size_t)64 * A.emit_stride)) return bail(rc);
-            if ((e = hipMemset(c->lctl, 0, 2 * sizeof(Ctl))) != hipSuccess ||
-                (e = hipMemset(c->lseg, 0, (size_t)2 * kMaxSeg * sizeof(int32_t))) != hipSuccess ||
-                (e = hipMemset(c->lemit, 0, (size_t)64 * A.emit_stride * sizeof(unsigned long long))) != hipSuccess ||
-                (e = hipStreamCreateWithFlags(&c->lane_stream, hipStreamNonBlocking)) != hipSuccess ||
-                (e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming)) != hipSuccess ||
-                (e = hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming)) != hipSuccess)
+        const int want = lv ? std::max(1, std::min(kMaxLanes, std::atoi(lv))) : kDefaultLanes;
+        const int L = std::min(want, sh.spp);
+        if (L >= 2) {
+            if ((e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming)) != hipSuccess)
                 return bail(pt::fail(PT_ERR_HIP, std::string("lane setup: ") + hipGetErrorString(e)));
-            c->lanes = 2;
+            for (int l = 1; l < L; ++l) {
+                const int n_l = lane_iters(sh.spp, L, l);
+                size_t cap_l = 0;
+                if (int rc = path_cap((long long)n_l * (long long)npix, n_l, &cap_l)) return bail(rc);
+                for (int b = 0; b < 2; ++b)
+                    if (int rc = alloc_paths(c, c->lbuf[l][b], cap_l)) return bail(rc);
+                c->lcap[l] = cap_l;
+                if (c->mhit[0])
+                    if (int rc = c->alloc(&c->mhit[l], cap_l)) return bail(rc);
+                if (int rc = c->alloc(&c->lctl[l], 2)) return bail(rc);
+                if (int rc = c->alloc(&c->lseg[l], (size_t)2 * kMaxSeg)) return bail(rc);
+                if (int rc = c->alloc(&c->lemit[l], (size_t)64 * A.emit_stride)) return bail(rc);
+                if ((e = hipMemset(c->lctl[l], 0, 2 * sizeof(Ctl))) != hipSuccess ||
+                    (e = hipMemset(c->lseg[l], 0, (size_t)2 * kMaxSeg * sizeof(int32_t))) != hipSuccess ||
+                    (e = hipMemset(c->lemit[l], 0, (size_t)64 * A.emit_stride * sizeof(unsigned long long))) != hipSuccess ||
+                    (e = hipStreamCreateWithFlags(&c->lane_stream[l], hipStreamNonBlocking)) != hipSuccess ||
+                    (e = hipEventCreateWithFlags(&c->ev_join[l], hipEventDisableTiming)) != hipSuccess)
+                    return bail(pt::fail(PT_ERR_HIP, std::string("lane setup: ") + hipGetErrorString(e)));
+            }
+            c->lanes = L;
         }
     }
     if ((e = hipMemset(A.image, 0, (size_t)npix * 3 * sizeof(float))) != hipSuccess ||
@@ -2714,7 +2725,7 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
     // (< the lane's paths), the histogram by (producer tile, material) (cap / 256 tiles at most)
     for (int l = 0; l < c->lanes; ++l) {
         auto& ss = c->sset[l];
-        const int n_l = l == 0 ? (c->lanes == 2 ? sh.spp - sh.spp / 2 : sh.spp) : sh.spp / 2;
+        const int n_l = lane_iters(sh.spp, c->lanes, l);
         const size_t paths = (size_t)n_l * (size_t)npix, cap = c->lcap[l];
         ss.hist_cap = (int64_t)((size_t)c->nmats * (cap / kBlock + 1) + 2);
         const size_t tiles = ((size_t)ss.hist_cap + kHistTile - 1) / kHistTile;
@@ -2771,7 +2782,7 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
         A.colbuf = c->colbuf + (size_t)h * (size_t)A.tile.P;
         if (c->fin_out[h]) HIP_TRY(hipStreamWaitEvent(st, c->ev_fin[h], 0));   // pass p-2's finalize
     }
-    const bool laned = (sorted || c->fused) && c->lanes == 2 && !spp1;
+    const bool laned = (sorted || c->fused) && c->lanes >= 2 && !spp1;
     // One bounce b of the material-sorted pipeline on stream s, for the lane whose buffers are `bufs`
     // (current one: lcur), launch counter `lc` and sort buffers `ss`: [the first bounce's producer],
     // histogram scan, scatter, producer (shade b + intersect b + 1).  Every producer flips the buffers.
@@ -2809,39 +2820,48 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
     };
     if (sorted && c->nmats > kSortMaxMats)
         return pt::fail(PT_ERR_ARG, "material-sorted shading supports at most 256 materials");
-    if (!sorted && c->fused && mmode == kMeshPre)   // k_traverse's per-bounce ray tickets (both lanes)
-        HIP_TRY(hipMemsetAsync(c->tq, 0, 2 * 64 * sizeof(uint32_t), st));
+    if (!sorted && c->fused && mmode == kMeshPre)   // k_traverse's per-bounce ray tickets (every lane)
+        HIP_TRY(hipMemsetAsync(c->tq, 0, (size_t)kMaxLanes * 64 * sizeof(uint32_t), st));
     if (laned) {
-        const int npix = A.tile.npix;
-        const int n1 = A.tile.spp / 2, n0 = A.tile.spp - n1;
-        KArgs L[2] = {A, A};
-        L[0].tile.spp = n0;
-        L[0].tile.P = n0 * npix;
-        L[1].tile.spp = n1;
-        L[1].tile.P = n1 * npix;
-        L[1].tile.iter_first = iter_first + n0;
-        L[1].colbuf = A.colbuf + (size_t)n0 * (size_t)npix;
-        L[1].ctl = c->lctl;
-        L[1].seg = c->lseg;
-        L[1].emit_slots = c->lemit;
-        L[1].count_pass = 0;
-        const hipStream_t ls[2] = {st, c->lane_stream};
-        const PathSoA* bufs[2] = {c->buf, c->lbuf};
-        uint64_t* cnt[2] = {&c->compact_launches, &c->llaunches};
+        const int npix = A.tile.npix, nl = c->lanes;
+        KArgs L[kMaxLanes];
+        hipStream_t ls[kMaxLanes];
+        const PathSoA* bufs[kMaxLanes];
+        uint64_t* cnt[kMaxLanes];
+        for (int l = 0, off = 0; l < nl; ++l) {
+            const int n_l = lane_iters(A.tile.spp, nl, l);
+            L[l] = A;
+            L[l].tile.spp = n_l;
+            L[l].tile.P = n_l * npix;
+            L[l].tile.iter_first = iter_first + off;
+            L[l].colbuf = A.colbuf + (size_t)off * (size_t)npix;
+            if (l > 0) {
+                L[l].ctl = c->lctl[l];
+                L[l].seg = c->lseg[l];
+                L[l].emit_slots = c->lemit[l];
+                L[l].count_pass = 0;
+            }
+            ls[l] = l == 0 ? st : c->lane_stream[l];
+            bufs[l] = l == 0 ? c->buf : c->lbuf[l];
+            cnt[l] = l == 0 ? &c->compact_launches : &c->llaunches[l];
+            off += n_l;
+        }
         HIP_TRY(hipEventRecord(c->ev_fork, st));   // after the wait for this colour half above
-        HIP_TRY(hipStreamWaitEvent(c->lane_stream, c->ev_fork, 0));
-        // every exit, the error returns included, orders lane 1's queued work before later work on st
+        for (int l = 1; l < nl; ++l) HIP_TRY(hipStreamWaitEvent(c->lane_stream[l], c->ev_fork, 0));
+        // every exit, the error returns included, orders the lanes' queued work before later work on st
         struct Join {
             pt_ctx* c;
             hipStream_t st;
             ~Join() {
-                (void)hipEventRecord(c->ev_join, c->lane_stream);
-                (void)hipStreamWaitEvent(st, c->ev_join, 0);
+                for (int l = 1; l < c->lanes; ++l) {
+                    (void)hipEventRecord(c->ev_join[l], c->lane_stream[l]);
+                    (void)hipStreamWaitEvent(st, c->ev_join[l], 0);
+                }
             }
         } join{c, st};
-        int lcur[2] = {0, 0};
+        int lcur[kMaxLanes] = {};
         for (int b = 0; b < c->depth; ++b)
-            for (int l = 0; l < 2; ++l) {
+            for (int l = 0; l < nl; ++l) {
                 KArgs& a = L[l];
                 a.bounce = b;
                 if (sorted) {
@@ -2976,9 +2996,9 @@ int pt_stats(pt_ctx* c, pt_stats_t* out) {
     std::vector<unsigned long long> slots((size_t)64 * c->args.emit_stride);
     HIP_TRY(hipMemcpy(slots.data(), c->args.emit_slots, slots.size() * sizeof(unsigned long long),
                       hipMemcpyDeviceToHost));
-    if (c->lemit) {   // lane 1's per-workgroup counts
+    for (int l = 1; l < c->lanes; ++l) {   // the other lanes' per-workgroup counts
         std::vector<unsigned long long> l1(slots.size());
-        HIP_TRY(hipMemcpy(l1.data(), c->lemit, l1.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(l1.data(), c->lemit[l], l1.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
         for (size_t j = 0; j < slots.size(); ++j) slots[j] += l1[j];
     }
     std::memset(out, 0, sizeof *out);

@@ -4,7 +4,7 @@ import os
 import sys
 from pathlib import Path
 ROOT = Path(__file__).resolve().parent.parent
-os.environ["PT_AMD_LIB"] = str(ROOT / "cuda_pathtracer_amd" / "build" / "libpt_amd_stamps.so")
+os.environ.setdefault("PT_AMD_LIB", str(ROOT / "cuda_pathtracer_amd" / "build" / "libpt_amd_stamps.so"))
 os.environ.setdefault("PT_AMD_NO_TORCH", "1")
 sys.path.insert(0, str(ROOT))
 import cuda_pathtracer_amd as P  # noqa: E402

@@ -572,23 +572,25 @@ def test_deferred_finalize_is_ordered_with_image_calls(cornell_path):
         p.free()
 
 
-@pytest.mark.parametrize("spp", [2, 5, 32])
-def test_two_lanes_equal_one_lane(cornell_path, monkeypatch, spp):
-    """Batched passes of the fused pipeline trace two lanes of iterations on two streams
-    (pt_render_pass): image, live-path and emissive counts equal a one-lane context (PT_AMD_LANES=1)
-    bit for bit, including odd splits (5 = 3 + 2)."""
+@pytest.mark.parametrize("spp,lanes", [(2, "2"), (5, "2"), (32, "2"), (5, "3"), (7, "4"), (32, "4"), (3, "4")])
+@pytest.mark.parametrize("sort", [False, True])
+def test_two_lanes_equal_one_lane(cornell_path, monkeypatch, spp, lanes, sort):
+    """Batched passes trace lanes of iterations on their own streams (pt_render_pass, 2-4 lanes,
+    fused and material-sorted pipelines): image, live-path and emissive counts equal a one-lane
+    context (PT_AMD_LANES=1) bit for bit, including uneven splits (5 = 3 + 2, 7 = 2 + 2 + 2 + 1) and
+    more lanes than iterations (3 iterations, 4 lanes requested)."""
     from cuda_pathtracer_amd import PathTracer
     s, _ = _pair(cornell_path, (44, 30))
     out = []
-    for lanes in ("2", "1"):
-        monkeypatch.setenv("PT_AMD_LANES", lanes)
-        pt = PathTracer(s, _gui(), spp=spp)
+    for n in (lanes, "1"):
+        monkeypatch.setenv("PT_AMD_LANES", n)
+        pt = PathTracer(s, _gui(sortbyMaterial=sort), spp=spp)
         for it in (1, 1 + spp):
             pt.render_pass(it)
         st = pt.stats()
         out.append((pt.image(), st["bounce_live"], st["bounce_emit"], st["passes"]))
         pt.free()
-    _assert_bitexact(out[0][0], out[1][0], f"two lanes vs one, spp {spp}")
+    _assert_bitexact(out[0][0], out[1][0], f"{lanes} lanes vs one, spp {spp} sort {sort}")
     assert out[0][1:] == out[1][1:]
 
 
