@@ -43,7 +43,7 @@ sys.path.insert(0, str(ROOT))
 METRIC = "Mray/s (paths×bounces/s) on Cornell scene + scan GB/s vs HBM peak, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 VALU_PEAK = 256 * 4 * 2.4e9 / 2   # wave64 VALU instructions/s: 4 SIMD-32 per CU, 2 cycles each (same guide)
-DEFAULT_LANES = 2                 # pt_render_pass lanes when PT_AMD_LANES is unset (pt_kernels.hip kDefaultLanes)
+DEFAULT_LANES = 3                 # pt_render_pass lanes when PT_AMD_LANES is unset (pt_kernels.hip kDefaultLanes)
 SEGMENT_BYTES = 184            # SURVEY.md §8d algorithmic bytes per traced segment
 PATH_BYTES = 44                # fused kernel's path state: o(12) d(12) c(12) slot(4) bounces(4)
 FB_RMW_BYTES = 24              # float3 read + write

@@ -1075,7 +1075,7 @@ __global__ __launch_bounds__(kBlock) void k_iter_bases(const KArgs A) {
 constexpr int kMaxSeg = 2048;
 constexpr int kMaxSpp = kBlock;   // batch iterations per pass (pt_shard.spp): one thread each
 constexpr int kMaxLanes = 4;      // lanes of a batched pass (pt_ctx::lanes; PT_AMD_LANES)
-constexpr int kDefaultLanes = 2;
+constexpr int kDefaultLanes = 3;   // measured: +0.7% Cornell, +1.2% config 3, +3% config 4, +2% config 5 vs 2; 4 lanes + the finalize stream exceed the box's 4 hardware queues (-10%)
 // Iterations of lane l when `spp` are split over `lanes`: the first spp % lanes lanes take one more.
 inline int lane_iters(int spp, int lanes, int l) { return spp / lanes + (l < spp % lanes ? 1 : 0); }
 
