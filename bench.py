@@ -43,7 +43,6 @@ sys.path.insert(0, str(ROOT))
 METRIC = "Mray/s (paths×bounces/s) on Cornell scene + scan GB/s vs HBM peak, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 VALU_PEAK = 256 * 4 * 2.4e9 / 2   # wave64 VALU instructions/s: 4 SIMD-32 per CU, 2 cycles each (same guide)
-DEFAULT_LANES = 3                 # pt_render_pass lanes when PT_AMD_LANES is unset (pt_kernels.hip kDefaultLanes)
 SEGMENT_BYTES = 184            # SURVEY.md §8d algorithmic bytes per traced segment
 PATH_BYTES = 44                # fused kernel's path state: o(12) d(12) c(12) slot(4) bounces(4)
 FB_RMW_BYTES = 24              # float3 read + write
@@ -411,7 +410,8 @@ def main() -> None:
     per_launch_bytes = SEGMENT_BYTES * seg_bounce / max(b_n, 1)
     avg_ms = b_ms / max(b_n, 1)
     achieved = per_launch_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-    lanes = min(int(os.environ.get("PT_AMD_LANES", str(DEFAULT_LANES))), spp, 4) \
+    default_lanes = 3 if pt.npaths >= (48 << 20) else 2   # pt_kernels.hip kThreeLanePaths
+    lanes = min(int(os.environ.get("PT_AMD_LANES", str(default_lanes))), spp, 4) \
         if (spp > 1 and (sorted_ or os.environ.get("PT_PIPELINE") != "split")) else 1
     roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": None,

@@ -1075,7 +1075,10 @@ __global__ __launch_bounds__(kBlock) void k_iter_bases(const KArgs A) {
 constexpr int kMaxSeg = 2048;
 constexpr int kMaxSpp = kBlock;   // batch iterations per pass (pt_shard.spp): one thread each
 constexpr int kMaxLanes = 4;      // lanes of a batched pass (pt_ctx::lanes; PT_AMD_LANES)
-constexpr int kDefaultLanes = 3;   // measured: +0.7% Cornell, +1.2% config 3, +3% config 4, +2% config 5 vs 2; 4 lanes + the finalize stream exceed the box's 4 hardware queues (-10%)
+constexpr long long kThreeLanePaths = 48ll << 20;   // default: 3 lanes from 48 Mi paths per pass, else 2
+// (measured, same box: Cornell 800x800 x 32 (20 M paths): 3 lanes +0.7%, within run-to-run noise,
+// while each launch shares the GPU with two others; config 3 (66 M) +1.2%, config 4 (265 M) +3%,
+// config 5 (66 M) +2%.  4 lanes + the finalize stream exceed the box's 4 hardware queues: -10%.)
 // Iterations of lane l when `spp` are split over `lanes`: the first spp % lanes lanes take one more.
 inline int lane_iters(int spp, int lanes, int l) { return spp / lanes + (l < spp % lanes ? 1 : 0); }
 
@@ -2688,7 +2691,7 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
     A.count_pass = 1;
     {   // lanes 1..L-1: each its own path buffers, control words, emissive slots and stream
         const char* lv = std::getenv("PT_AMD_LANES");
-        const int want = lv ? std::max(1, std::min(kMaxLanes, std::atoi(lv))) : kDefaultLanes;
+        const int want = lv ? std::max(1, std::min(kMaxLanes, std::atoi(lv))) : (P >= kThreeLanePaths ? 3 : 2);
         const int L = std::min(want, sh.spp);
         if (L >= 2) {
             if ((e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming)) != hipSuccess)
