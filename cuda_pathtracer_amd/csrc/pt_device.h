@@ -153,6 +153,11 @@ struct DGeom {
     int32_t bkind;   // 0: never hit (mesh), 1: oriented cube, 2: sphere, 3: world-box cube,
                      // 4: uniformly scaled sphere (world-space dot products)
     int32_t orig;    // SceneDev::bgeoms rows: index of this geom in SceneDev::geoms
+    // Cubes: the world normal of each slab code (axis * 2 + sign) — boxIntersectionTest's
+    // normalize(multiplyMV(invTranspose, (n, 0))) of a unit axis vector depends on the geom and
+    // the code only, so pt_create evaluates it once with the same float32 operations (glm's
+    // association, correctly rounded sqrt and division: the same bits as the per-hit evaluation).
+    float nrm[6][3];
 };
 
 struct DMaterial {   // == pt_material

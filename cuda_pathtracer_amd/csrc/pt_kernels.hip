@@ -158,15 +158,12 @@ __device__ __forceinline__ float box_test(const G& g, f3 ro, f3 rd, int& ncode) 
     }
     return -1.0f;
 }
+// The world normal of slab code `code`: precomputed per cube (DGeom::nrm).  Code -1 (no slab
+// bounded the hit: every slab parameter NaN) normalizes the zero vector: 0 * (1 / 0) = NaN.
 template <class G>
 __device__ __forceinline__ f3 box_normal(const G& g, int code) {
-    f3 n = F3(0.0f, 0.0f, 0.0f);
-    if (code >= 0) {
-        const float s = (code & 1) ? -1.0f : 1.0f;
-        const int a = code >> 1;
-        n = F3(a == 0 ? s : 0.0f, a == 1 ? s : 0.0f, a == 2 ? s : 0.0f);
-    }
-    return normalize(xform_vector(g.itr, n));
+    if (code < 0) return F3(__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""));
+    return F3(g.nrm[code][0], g.nrm[code][1], g.nrm[code][2]);
 }
 
 // sphereIntersectionTest (intersections.cu:60-115); normal deferred (object-space hit point kept).
@@ -540,9 +537,13 @@ constexpr int kLdsGeoms = 32;
 // geoms read without LDS bank conflicts (a 48-word row put rows r and r+4 on the same banks:
 // SQ_LDS_BANK_CONFLICT 6.8 M cycles per bounce launch).
 struct alignas(16) LGeom {
-    Affine inv, xf, itr;
+    Affine inv, xf;
+    union {
+        Affine itr;          // spheres: the hit normal's transform
+        float nrm[6][3];     // cubes: the world normal of each slab code (DGeom::nrm)
+    };
     int32_t type, material;
-    int32_t pad[5];
+    int32_t pad[2];
 };
 static_assert(sizeof(LGeom) == 208, "LGeom row stride");
 constexpr float kInf = __builtin_inff();
@@ -553,7 +554,10 @@ __device__ __forceinline__ void stage_geoms(const SceneDev& S, LGeom* s_geoms) {
         const DGeom& g = S.geoms[j];
         s_geoms[j].inv = g.inv;
         s_geoms[j].xf = g.xf;
-        s_geoms[j].itr = g.itr;
+        if (g.type == PT_GEOM_CUBE)
+            for (int q = 0; q < 18; ++q) s_geoms[j].nrm[q / 3][q % 3] = g.nrm[q / 3][q % 3];
+        else
+            s_geoms[j].itr = g.itr;
         s_geoms[j].type = g.type;
         s_geoms[j].material = g.material;
     }
@@ -2451,6 +2455,17 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
         d.inv = to_affine(g.inverse_transform);
         d.xf = to_affine(g.transform);
         d.itr = to_affine(g.inv_transpose);
+        if (d.type == PT_GEOM_CUBE)   // DGeom::nrm: glm's multiplyMV + normalize of each unit axis, in float32
+            for (int code = 0; code < 6; ++code) {
+                const float sg = (code & 1) ? -1.0f : 1.0f;
+                const int a = code >> 1;
+                const float n[3] = {a == 0 ? sg : 0.0f, a == 1 ? sg : 0.0f, a == 2 ? sg : 0.0f};
+                float v[3];
+                for (int r = 0; r < 3; ++r)
+                    v[r] = (d.itr.c[0][r] * n[0] + d.itr.c[1][r] * n[1]) + (d.itr.c[2][r] * n[2] + d.itr.z3[r]);
+                const float inv = 1.0f / std::sqrt((v[0] * v[0] + v[1] * v[1]) + v[2] * v[2]);
+                for (int r = 0; r < 3; ++r) d.nrm[code][r] = v[r] * inv;
+            }
         for (int k = 0; k < 3; ++k) { d.bmin[k] = g.min_bound[k]; d.bmax[k] = g.max_bound[k]; }
     }
     {   // scene extent: every surface point (cube/sphere corners, mesh vertices) and the camera
