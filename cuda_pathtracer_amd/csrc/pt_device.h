@@ -158,6 +158,10 @@ struct DGeom {
     // the code only, so pt_create evaluates it once with the same float32 operations (glm's
     // association, correctly rounded sqrt and division: the same bits as the per-hit evaluation).
     float nrm[6][3];
+    // Cubes: the tangent frame calculateRandomDirectionInHemisphere builds from each of those
+    // normals (interactions.cu:23-33: p1 = normalize(cross(n, dnn)), p2 = normalize(cross(n, p1))),
+    // also a function of (geom, code) only: frm[code] = (p1, p2), evaluated once by pt_create.
+    float frm[6][6];
 };
 
 struct DMaterial {   // == pt_material

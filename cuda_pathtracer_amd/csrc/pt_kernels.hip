@@ -130,6 +130,7 @@ struct Hit {
     f3 n;
     int32_t mat;
     float u, v;
+    int32_t frame = -1;   // cube hits: geom * 6 + slab code (the precomputed tangent frame, DGeom::frm)
 };
 
 // boxIntersectionTest (intersections.cu:3-58).  The world normal is deferred to the closest
@@ -498,7 +499,10 @@ __device__ __forceinline__ Hit intersect_scene(const SceneDev& S, const FlagsDev
     h.mat = g.material;
     h.u = cu;
     h.v = cv;
-    if (g.type == PT_GEOM_CUBE) h.n = box_normal(g, best_code);
+    if (g.type == PT_GEOM_CUBE) {
+        h.n = box_normal(g, best_code);
+        if (best_code >= 0) h.frame = hit_geom * 6 + best_code;
+    }
     else if (g.type == PT_GEOM_SPHERE) h.n = sphere_normal(g, best_obj, best_outside);
     else h.n = best_n;
     return h;
@@ -548,6 +552,15 @@ struct alignas(16) LGeom {
 static_assert(sizeof(LGeom) == 208, "LGeom row stride");
 constexpr float kInf = __builtin_inff();
 
+// The cubes' tangent frames (DGeom::frm) for shade(): [geom * 6 + code][6] floats.
+__device__ __forceinline__ void stage_frames(const SceneDev& S, float* s_frm) {
+    if (S.ngeoms > kLdsGeoms) return;
+    const auto* G = as_const(S.geoms);
+    for (int e = threadIdx.x; e < S.ngeoms * 36; e += blockDim.x) {
+        const int gi = e / 36, q = e % 36;
+        if (G[gi].type == PT_GEOM_CUBE) s_frm[e] = G[gi].frm[q / 6][q % 6];
+    }
+}
 __device__ __forceinline__ void stage_geoms(const SceneDev& S, LGeom* s_geoms) {
     if (S.ngeoms > kLdsGeoms) return;
     for (int j = threadIdx.x; j < S.ngeoms; j += blockDim.x) {
@@ -772,6 +785,7 @@ __device__ __forceinline__ Hit intersect_bounded(const SceneDev& S, const FlagsD
     h.u = h.v = 0.f;
     if (PRE && hit_geom == mesh_geom) tri_attrs(S.attrs[mh->idx], mh->bx, mh->by, h.n, h.u, h.v);
     else h.n = g.type == PT_GEOM_CUBE ? box_normal(g, best_code) : sphere_normal(g, best_obj, best_outside);
+    if (g.type == PT_GEOM_CUBE && best_code >= 0) h.frame = hit_geom * 6 + best_code;
     return h;
 }
 
@@ -814,16 +828,22 @@ __device__ __forceinline__ f3 tex_color(const DTexture& tx, float u, float v) { 
     return F3(0, 0, 0);
 }
 
-__device__ __forceinline__ f3 hemisphere(f3 n, Rng& rng) {   // interactions.cu:3-41
+__device__ __forceinline__ f3 hemisphere(f3 n, Rng& rng, const float* frame = nullptr) {   // interactions.cu:3-41
     const float up = sqrt_cr(rng.u01());
     const float over = sqrt_cr(1 - up * up);
     const float around = rng.u01() * kTWO_PI;
-    f3 dnn;
-    if (fabsf(n.x) < kSQRT_1_3) dnn = F3(1, 0, 0);
-    else if (fabsf(n.y) < kSQRT_1_3) dnn = F3(0, 1, 0);
-    else dnn = F3(0, 0, 1);
-    const f3 p1 = normalize(cross(n, dnn));
-    const f3 p2 = normalize(cross(n, p1));
+    f3 p1, p2;
+    if (frame) {   // a cube's face: the frame of its normal, precomputed (DGeom::frm)
+        p1 = F3(frame[0], frame[1], frame[2]);
+        p2 = F3(frame[3], frame[4], frame[5]);
+    } else {
+        f3 dnn;
+        if (fabsf(n.x) < kSQRT_1_3) dnn = F3(1, 0, 0);
+        else if (fabsf(n.y) < kSQRT_1_3) dnn = F3(0, 1, 0);
+        else dnn = F3(0, 0, 1);
+        p1 = normalize(cross(n, dnn));
+        p2 = normalize(cross(n, p1));
+    }
     float sa, ca;
     sincos_c(around, &sa, &ca);
     return (up * n + (ca * over) * p1) + (sa * over) * p2;
@@ -847,8 +867,9 @@ __device__ __forceinline__ int slot_pixel(const CamDev& cam, const TileDev& T, i
 // Returns true if the path survives.  `idx` is the path's position in the (compacted, possibly
 // material-sorted) array — the RNG key of the reference (pathtrace.cu:315).
 template <class MT>
+// `frames`: the staged tangent frames of the scene's cubes (LDS, [geom * 6 + code][6]) or null.
 __device__ __forceinline__ bool shade(const SceneDev& S, const FlagsDev& fl, int depth, int iter, int idx,
-                                      PathReg& p, const Hit& h, const MT* mats) {
+                                      PathReg& p, const Hit& h, const MT* mats, const float* frames = nullptr) {
     if (h.t <= 0.0f) { p.c = F3(0, 0, 0); return false; }
     int remaining = depth - p.bounces;
     Rng rng(iter, idx, remaining);
@@ -876,7 +897,7 @@ __device__ __forceinline__ bool shade(const SceneDev& S, const FlagsDev& fl, int
         p.d = reflect(p.d, n);
         p.c = hadamard(p.c, scol);
     } else {
-        p.d = hemisphere(n, rng);
+        p.d = hemisphere(n, rng, frames && h.frame >= 0 ? frames + 6 * h.frame : nullptr);
     }
     if (!fl.single_albedo) p.c = hadamard(p.c, mcol);   // interactions.cu:83 (second albedo)
     p.bounces += 1;
@@ -1403,8 +1424,9 @@ __global__ __launch_bounds__(kBlock) void k_bounce(const KArgs A) {
     // scene tables sized to the scene (dynamic LDS, bounce_lds_bytes): geom rows, then materials
     extern __shared__ __align__(16) uint8_t s_dyn[];
     LGeom* s_geoms = reinterpret_cast<LGeom*>(s_dyn);
-    DMaterial* s_mats =
-        reinterpret_cast<DMaterial*>(s_dyn + (MESH == kMeshInline || A.S.ngeoms > kLdsGeoms ? 0 : A.S.ngeoms) * sizeof(LGeom));
+    const int ng_lds = MESH == kMeshInline || A.S.ngeoms > kLdsGeoms ? 0 : A.S.ngeoms;
+    DMaterial* s_mats = reinterpret_cast<DMaterial*>(s_dyn + ng_lds * sizeof(LGeom));
+    float* s_frm = reinterpret_cast<float*>(s_mats + min(A.S.nmats, kLdsMats));   // [ng_lds * 6][6]
     __shared__ int32_t s_pre[FIRST ? 1 : kMaxSeg + 1];
     __shared__ int32_t s_ib[kMaxSpp + 1];
     __shared__ uint32_t s_wc[2][4];
@@ -1442,9 +1464,13 @@ __global__ __launch_bounds__(kBlock) void k_bounce(const KArgs A) {
         A.ctl[par ^ 1].chunk = (uint32_t)chunk;
     }
     if (my_it < 0) return;
-    if (MESH != kMeshInline) stage_geoms(A.S, s_geoms);
-    stage_materials(A, s_mats);
+    if (MESH != kMeshInline) {
+        stage_geoms(A.S, s_geoms);
+        stage_frames(A.S, s_frm);
+    }
+    stage_materials(A, s_mats);   // (its barrier publishes the staged tables)
     const bool lds_mats = A.S.nmats <= kLdsMats;
+    const float* frames = ng_lds > 0 ? s_frm : nullptr;
     count_bounce(A, N);
     const int it_base = __builtin_amdgcn_readfirstlane(s_ib[my_it]);
     const int first = it_base + my_c * chunk;
@@ -1498,8 +1524,8 @@ __global__ __launch_bounds__(kBlock) void k_bounce(const KArgs A) {
             // every path entering bounce b has b bounces behind it: a wave-uniform value, so the
             // shading RNG's (iteration, remaining depth) hash is computed once per wave on the SALU
             p.bounces = A.bounce;
-            alive = lds_mats ? shade(A.S, A.fl, A.tile.depth, iter, key, p, h, s_mats)
-                             : shade(A.S, A.fl, A.tile.depth, iter, key, p, h, A.S.mats);
+            alive = lds_mats ? shade(A.S, A.fl, A.tile.depth, iter, key, p, h, s_mats, frames)
+                             : shade(A.S, A.fl, A.tile.depth, iter, key, p, h, A.S.mats, frames);
             if (!alive) {
                 emitted = p.c.x != 0.0f || p.c.y != 0.0f || p.c.z != 0.0f;
                 retire<SPP1>(A, p);
@@ -2326,7 +2352,7 @@ int resident_per_cu(const void* kernel) {
 size_t bounce_lds_bytes(const SceneDev& S, int mesh) {
     const int g = (mesh == kMeshInline || S.ngeoms > kLdsGeoms) ? 0 : S.ngeoms;
     const int m = std::min(S.nmats, kLdsMats);
-    return (size_t)g * sizeof(LGeom) + (size_t)m * sizeof(DMaterial);
+    return (size_t)g * sizeof(LGeom) + (size_t)m * sizeof(DMaterial) + (size_t)g * 36 * sizeof(float);
 }
 
 // k_bounce's mesh mode for the current flags (see pt_ctx::mhit).
@@ -2465,6 +2491,26 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
                     v[r] = (d.itr.c[0][r] * n[0] + d.itr.c[1][r] * n[1]) + (d.itr.c[2][r] * n[2] + d.itr.z3[r]);
                 const float inv = 1.0f / std::sqrt((v[0] * v[0] + v[1] * v[1]) + v[2] * v[2]);
                 for (int r = 0; r < 3; ++r) d.nrm[code][r] = v[r] * inv;
+                // DGeom::frm: the hemisphere frame of that normal (float32, the device's cross/normalize)
+                const float* nn = d.nrm[code];
+                float dnn[3] = {0.0f, 0.0f, 1.0f};
+                if (std::fabs(nn[0]) < ptd::kSQRT_1_3) { dnn[0] = 1.0f; dnn[2] = 0.0f; }
+                else if (std::fabs(nn[1]) < ptd::kSQRT_1_3) { dnn[1] = 1.0f; dnn[2] = 0.0f; }
+                auto crs = [](const float* a, const float* b, float* o) {
+                    o[0] = a[1] * b[2] - b[1] * a[2];
+                    o[1] = a[2] * b[0] - b[2] * a[0];
+                    o[2] = a[0] * b[1] - b[0] * a[1];
+                };
+                auto nrmz = [](float* x) {
+                    const float iv = 1.0f / std::sqrt((x[0] * x[0] + x[1] * x[1]) + x[2] * x[2]);
+                    for (int r = 0; r < 3; ++r) x[r] = x[r] * iv;
+                };
+                float p1[3], p2[3];
+                crs(nn, dnn, p1);
+                nrmz(p1);
+                crs(nn, p1, p2);
+                nrmz(p2);
+                for (int r = 0; r < 3; ++r) { d.frm[code][r] = p1[r]; d.frm[code][3 + r] = p2[r]; }
             }
         for (int k = 0; k < 3; ++k) { d.bmin[k] = g.min_bound[k]; d.bmax[k] = g.max_bound[k]; }
     }
