@@ -29,6 +29,11 @@ GROUPS = {
            "SQ_WAIT_ANY", "SQ_ACTIVE_INST_VALU", "GRBM_GUI_ACTIVE"],
     "l2": ["TCC_HIT_sum", "TCC_MISS_sum"],                       # L2 hit rate (per-XCD L2s summed)
     "vmem": ["SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR", "SQ_INSTS_LDS", "SQ_INSTS_BRANCH"],
+    # where waves wait: issue-blocked cycles by unit, instruction-fetch stalls, in-flight levels
+    "stall1": ["SQ_WAVE_CYCLES", "SQ_WAIT_INST_LDS", "SQ_ACTIVE_INST_LDS", "SQ_ACTIVE_INST_VMEM",
+               "SQ_ACTIVE_INST_SCA", "SQ_ACTIVE_INST_MISC", "SQ_IFETCH", "SQ_IFETCH_LEVEL"],
+    "stall2": ["SQ_INST_LEVEL_VMEM", "SQ_INSTS_VMEM", "SQ_INST_LEVEL_LDS", "SQ_INSTS_LDS",
+               "SQ_INST_LEVEL_SMEM", "SQ_INSTS_SMEM", "SQ_WAIT_ANY", "SQ_LDS_BANK_CONFLICT"],
 }
 
 
