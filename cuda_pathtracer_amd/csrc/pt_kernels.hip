@@ -704,6 +704,20 @@ __device__ __forceinline__ Hit intersect_bounded(const SceneDev& S, const FlagsD
     f3 best_obj = F3(0, 0, 0);
     bool best_outside = true;
     int mesh_geom = -1;
+    // A NaN direction (glm::refract under total internal reflection, interactions.cu:70) makes
+    // every exact test return NaN (box: the NaN slabs leave tmin/tmax at -/+1e38, the hit point is
+    // NaN; sphere: NaN radicand passes, NaN t) and `t > 0` rejects it: no hit, without the plain
+    // loop over every geom that such a lane would otherwise cost its whole wave.
+    if (rd.x != rd.x || rd.y != rd.y || rd.z != rd.z) {
+        if (!PRE || !mh->any) {
+            Hit h;
+            h.t = -1.0f;
+            h.mat = 0;
+            h.n = F3(0, 0, 0);
+            h.u = h.v = 0.f;
+            return h;
+        }
+    }
     if (PRE && mh->any) {
         const auto* G = as_const(S.geoms);
         for (int i = 0; i < S.ngeoms; ++i)
@@ -1495,6 +1509,9 @@ __global__ __launch_bounds__(kBlock) void k_bounce(const KArgs A) {
         bool alive = false, emitted = false;
         PathReg p;
         STAMP(t0);
+#ifdef PT_STAMPS
+        t1 = t2 = t0;   // lanes past the end of a partial tile skip the inner stamps
+#endif
         if (i < last) {
             int q = i;   // physical index of the path (and of its k_traverse record)
             if (FIRST) {

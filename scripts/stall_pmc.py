@@ -1,7 +1,7 @@
 """Stall breakdown of the bounce kernels (rocprofv3 PMC): issue-blocked cycles by unit, instruction
 fetch, and average in-flight latency of vector-memory, LDS and scalar-memory instructions
 (SQ_INST_LEVEL_x / SQ_INSTS_x, in cycles).  Workload: the bench's Cornell passes.  Usage:
-python scripts/stall_pmc.py OUT_DIR"""
+python scripts/stall_pmc.py OUT_DIR [scene=PATH]"""
 import json
 import sys
 from pathlib import Path
@@ -11,7 +11,8 @@ sys.path.insert(0, str(ROOT / "scripts"))
 import pmc  # noqa: E402
 
 out = Path(sys.argv[1]).resolve()
-res = pmc.collect(["4", "spp=32"], out / "pmc", timeout=150, groups=("stall1", "stall2", "sq"))
+extra = [a for a in sys.argv[2:] if a.startswith("scene=")]
+res = pmc.collect(["4", "spp=32"] + extra, out / "pmc", timeout=150, groups=("stall1", "stall2", "sq", "vmem"))
 summ = {"passes": res["_passes"]}
 for name in ("k_bounce<false, false, 0>", "k_bounce<true, false, 0>"):
     m = pmc.pick(res, name) or {}

@@ -120,6 +120,35 @@ def test_materials_reflective_refractive():
     assert st["bounce_live"] == live
 
 
+@pytest.mark.parametrize("kw", [dict(), dict(sortbyMaterial=True)])
+def test_glass_cubes_total_internal_reflection(kw):
+    """Rotated glass cubes (config 4's glass objects are cubes): rays inside a cube meet its faces
+    beyond the critical angle, glm::refract returns NaN (interactions.cu:70), and the next bounce's
+    closest hit of those NaN rays is "no hit" without the per-geom loop (intersect_bounded's early
+    return) — GPU == oracle bit for bit, batched and sorted."""
+    from cuda_pathtracer_amd import CUBE, SPHERE, Scene
+    s, o = Scene(), O.OracleScene()
+    for sc in (s, o):
+        light = sc.add_material(rgb=(1, 1, 1), emittance=5.0)
+        white = sc.add_material(rgb=(0.98, 0.98, 0.98))
+        glass = sc.add_material(rgb=(0.95, 0.95, 0.95), refractive=1.0, ior=1.5)
+        dense = sc.add_material(rgb=(0.9, 0.95, 0.9), specrgb=(0.9, 0.9, 0.9), refractive=1.0, ior=2.4)
+        sc.add_geom(CUBE, light, (0, 10, 0), (0, 0, 0), (3, 0.3, 3))
+        sc.add_geom(CUBE, white, (0, 0, 0), (0, 0, 0), (10, 0.01, 10))
+        sc.add_geom(CUBE, white, (0, 5, -5), (0, 90, 0), (0.01, 10, 10))
+        for k in range(6):
+            sc.add_geom(CUBE, glass if k % 2 else dense, (-4 + 1.6 * k, 1.5 + (k % 3), -1 + 0.4 * k),
+                        (10.0 * k, 25 + 7.0 * k, 5.0 * k), (1.4, 1.4, 1.4))
+        sc.add_geom(SPHERE, glass, (0, 6, 1), (0, 0, 0), (2.0, 2.0, 2.0))
+        sc.set_camera((96, 72), 45.0, (0, 5, 10.5), (0, 3, 0), (0, 1, 0))
+    s.set_render(4, 12, "glass")
+    s.finalize()
+    o.depth = 12
+    g, r, st, live = _run(s, o, _gui(**kw), iters=2, spp=2)
+    _assert_bitexact(g, r, f"glass cubes {kw}")
+    assert st["bounce_live"] == live and r.sum() > 0
+
+
 @pytest.mark.parametrize("rank,world,spp", [(0, 2, 1), (1, 2, 1), (0, 1, 2), (1, 3, 3), (2, 4, 4), (0, 1, 100),
                                              (3, 8, 256)])
 def test_tiles_and_batched_samples(cornell_path, rank, world, spp):
