@@ -2115,7 +2115,12 @@ struct pt_ctx {
     // lane_stream with its own path buffers and control words.  The lanes are independent (every
     // path's RNG keys and colour slot depend only on its iteration), so one lane's first bounce,
     // short tail bounces and launch gaps overlap the other's work.  PT_AMD_LANES=1 disables.
+    // The caller's stream does not wait for lanes 1.. at the end of a pass (async_lanes): only the
+    // pass's finalize does, so the next pass's lane 0 starts while their tail bounces still run;
+    // lanes 1.. of the next pass wait for the caller's stream (lane 0 of this pass, the colour half).
+    // PT_AMD_SYNC_LANES=1 joins every lane into the caller's stream instead.
     int lanes = 1;                       // lanes 1.. use the arrays below; lane 0 the context's own
+    bool async_lanes = true;
     PathSoA lbuf[kMaxLanes][2]{};
     Ctl* lctl[kMaxLanes] = {};
     int32_t* lseg[kMaxLanes] = {};
@@ -2727,6 +2732,7 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
         if (int rc = alloc_paths(c, c->buf[b], c->path_cap)) return bail(rc);
     c->lcap[0] = c->path_cap;
     if (const char* mi = std::getenv("PT_AMD_MESH_INLINE")) c->mesh_inline = std::strcmp(mi, "1") == 0;
+    if (const char* sl = std::getenv("PT_AMD_SYNC_LANES")) c->async_lanes = std::strcmp(sl, "1") != 0;
     if (A.S.nnodes > 0) {   // k_traverse records (mesh mode 2), tickets, stack depth and grid
         if (int rc = c->alloc(&c->mhit[0], c->path_cap)) return bail(rc);
         if (int rc = c->alloc(&c->tq, (size_t)kMaxLanes * 64)) return bail(rc);
@@ -2901,8 +2907,8 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
     };
     if (sorted && c->nmats > kSortMaxMats)
         return pt::fail(PT_ERR_ARG, "material-sorted shading supports at most 256 materials");
-    if (!sorted && c->fused && mmode == kMeshPre)   // k_traverse's per-bounce ray tickets (every lane)
-        HIP_TRY(hipMemsetAsync(c->tq, 0, (size_t)kMaxLanes * 64 * sizeof(uint32_t), st));
+    const bool tickets = !sorted && c->fused && mmode == kMeshPre;   // k_traverse's per-bounce ray tickets
+    if (tickets && !laned) HIP_TRY(hipMemsetAsync(c->tq, 0, (size_t)kMaxLanes * 64 * sizeof(uint32_t), st));
     if (laned) {
         const int npix = A.tile.npix, nl = c->lanes;
         KArgs L[kMaxLanes];
@@ -2929,14 +2935,18 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
         }
         HIP_TRY(hipEventRecord(c->ev_fork, st));   // after the wait for this colour half above
         for (int l = 1; l < nl; ++l) HIP_TRY(hipStreamWaitEvent(c->lane_stream[l], c->ev_fork, 0));
-        // every exit, the error returns included, orders the lanes' queued work before later work on st
+        // each lane zeroes its own tickets: its previous pass's tail may still be running
+        for (int l = 0; tickets && l < nl; ++l)
+            HIP_TRY(hipMemsetAsync(c->tq + 64 * l, 0, 64 * sizeof(uint32_t), ls[l]));
+        // every exit, the error returns included, orders the lanes' queued work before the pass's
+        // finalize (async_lanes) or before later work on st
         struct Join {
             pt_ctx* c;
             hipStream_t st;
             ~Join() {
                 for (int l = 1; l < c->lanes; ++l) {
                     (void)hipEventRecord(c->ev_join[l], c->lane_stream[l]);
-                    (void)hipStreamWaitEvent(st, c->ev_join[l], 0);
+                    (void)hipStreamWaitEvent(c->async_lanes ? c->fin_stream : st, c->ev_join[l], 0);
                 }
             }
         } join{c, st};
