@@ -17,6 +17,6 @@ python3 - <<'PY'
 import json
 for line in open("gpurun_out/configs.jsonl"):
     d = json.loads(line)
-    print(d["config"]["workload"][:60], "| spp", d["config"]["spp_per_step"], "|", round(d["value"], 1), d["unit"],
+    print(d["config"]["workload"][:60], "|", round(d["value"], 1), d["unit"],
           "| ms/step", round(d["ms_per_step"], 2), "| frac", round(d["roofline"]["frac"], 3))
 PY
