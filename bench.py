@@ -2,7 +2,7 @@
 
 Workload (BASELINE.json configs[1]): path_tracer/scenes/cornell.json as-is — 800x800, DEPTH 8,
 default flags.  A step is one render pass.  On N GPUs (one process per GPU, torchrun) rank r owns
-the image rows y % N == r; a pass traces `--spp` (default 32) iterations of those rows per GPU
+the image rows y % N == r; a pass traces `--spp` (default 128) iterations of those rows per GPU
 share, i.e. spp*N samples per pixel of the rank's rows, so every GPU traces spp*800*800 camera
 paths per step (weak scaling).  Batching iterations into one pass is bit-identical to tracing
 them one pass at a time (tests/test_render_gpu.py::test_tiles_and_batched_samples); it fills the
@@ -268,16 +268,19 @@ def main() -> None:
                     help="BASELINE.json workload: cornell (configs[1], the default line) or configs 3-5 "
                          "generated by cuda_pathtracer_amd.scenes")
     ap.add_argument("--bvh-cull", action="store_true", help="pt_flags.bvh_cull extension (mesh scenes)")
-    ap.add_argument("--spp", type=int, default=32,
+    ap.add_argument("--spp", type=int, default=None,
                     help="iterations per pass and GPU-share: a pass traces spp x N iterations of the rank's rows "
                          "(so every GPU's pass has the 1-GPU pass's size); results are bit-identical to one "
-                         "iteration per pass")
+                         "iteration per pass (default: 128 for cornell, 32 for configs 3-5)")
     ap.add_argument("--scaling", choices=["strong", "weak"], default="strong",
                     help="strong (default): a step renders a FIXED batch of --samples samples per pixel of the "
-                         "whole image, split over the N GPUs by rows (8/N passes of 32N iterations at 256); "
+                         "whole image, split over the N GPUs by rows (cornell: 2 passes of 128 iterations at N=1, "
+                         "one pass of 256 from N=2); "
                          "weak: a step is one pass of spp x N iterations of the rank's rows")
     ap.add_argument("--samples", type=int, default=256, help="strong scaling: samples per pixel per step")
     args = ap.parse_args()
+    if args.spp is None:
+        args.spp = 128 if args.config == "cornell" else 32
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -410,7 +413,7 @@ def main() -> None:
     per_launch_bytes = SEGMENT_BYTES * seg_bounce / max(b_n, 1)
     avg_ms = b_ms / max(b_n, 1)
     achieved = per_launch_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-    default_lanes = 3 if pt.npaths >= (48 << 20) else 2   # pt_kernels.hip kThreeLanePaths
+    default_lanes = 3 if sorted_ and pt.npaths >= (48 << 20) else 2   # pt_kernels.hip kThreeLanePaths
     lanes = min(int(os.environ.get("PT_AMD_LANES", str(default_lanes))), spp, 4) \
         if (spp > 1 and (sorted_ or os.environ.get("PT_PIPELINE") != "split")) else 1
     roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -2775,7 +2775,10 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
     A.count_pass = 1;
     {   // lanes 1..L-1: each its own path buffers, control words, emissive slots and stream
         const char* lv = std::getenv("PT_AMD_LANES");
-        const int want = lv ? std::max(1, std::min(kMaxLanes, std::atoi(lv))) : (P >= kThreeLanePaths ? 3 : 2);
+        // (async lanes: two lanes match three on the fused pipeline at every pass size; the sorted
+        // pipeline's five launches per bounce still gain from a third lane on large passes)
+        const bool three = c->flags.sort_by_material != 0 && P >= kThreeLanePaths;
+        const int want = lv ? std::max(1, std::min(kMaxLanes, std::atoi(lv))) : (three ? 3 : 2);
         const int L = std::min(want, sh.spp);
         if (L >= 2) {
             if ((e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming)) != hipSuccess)
