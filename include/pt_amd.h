@@ -199,7 +199,12 @@ int pt_create(const pt_scene* s, const pt_flags* flags, const pt_shard* shard, p
 int pt_destroy(pt_ctx* c);                                  /* pathtraceFree */
 int pt_set_flags(pt_ctx* c, const pt_flags* flags);         /* InitDataContainer / Settings */
 /* One pass: iterations [iter_first, iter_first + spp) for this tile, accumulated into the tile
- * image.  Asynchronous on `stream`; no host synchronisation inside. */
+ * image.  Asynchronous on `stream`; no host synchronisation inside.  A batched pass (spp > 1)
+ * runs its iterations in lanes on internal streams and adds their colours into the image on a
+ * finalize stream; `stream` itself is not made to wait for every lane (the next pass starts during
+ * this one's tail).  Read the image through pt_copy_image / pt_preview_rgba / pt_reset_image (they
+ * wait for the last finalize on their stream) or the synchronising calls; issue the passes of one
+ * context on one stream, or synchronise between streams. */
 int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream);
 /* sendImageToPBO (pathtrace.cu:64-86) for the tile: d_rgba = npix * 4 bytes on the device. */
 int pt_preview_rgba(pt_ctx* c, int32_t iter, uint8_t* d_rgba, void* stream);
