@@ -1433,8 +1433,14 @@ __global__ __launch_bounds__(kBlock) void k_traverse(const KArgs A) {
 }
 
 // [raygen] -> intersect -> shade -> segmented compaction (above).
+#ifndef PT_LATER_WAVES
+#define PT_LATER_WAVES 1   // (A/B knob: minimum waves per SIMD of the later-bounce kernels)
+#endif
+// At 60 VGPRs the later bounces' occupancy is set by their 106 SGPRs (7 waves per SIMD of 800).
+// PT_LATER_WAVES=8 caps them at 78 SGPRs (8 waves, 2048 workgroups): later bounces 713 -> 708 us
+// but the first bounce running beside them 1567 -> 1604 us, -0.3% overall (same box): not shipped.
 template <bool FIRST, bool SPP1, int MESH>
-__global__ __launch_bounds__(kBlock) void k_bounce(const KArgs A) {
+__global__ __launch_bounds__(kBlock, FIRST || MESH ? 1 : PT_LATER_WAVES) void k_bounce(const KArgs A) {
     // scene tables sized to the scene (dynamic LDS, bounce_lds_bytes): geom rows, then materials
     extern __shared__ __align__(16) uint8_t s_dyn[];
     LGeom* s_geoms = reinterpret_cast<LGeom*>(s_dyn);
