@@ -623,6 +623,37 @@ def test_two_lanes_equal_one_lane(cornell_path, monkeypatch, spp, lanes, sort):
     assert out[0][1:] == out[1][1:]
 
 
+@pytest.mark.parametrize("sort", [False, True])
+def test_async_lanes_stream_ordered_reads(cornell_path, sort):
+    """Async lanes: a batched pass does not make the caller's stream wait for every lane, so the
+    next pass starts during the tail.  Six passes issued back to back on one torch stream, then the
+    image copied on that stream (pt_copy_image waits for the last finalize) and only that stream
+    synchronised — no device-wide sync — equal the oracle bit for bit, for 2 and 3 lanes."""
+    import os
+    import torch
+    from cuda_pathtracer_amd import PathTracer
+    s, o = _pair(cornell_path, (48, 40))
+    for lanes in ("2", "3"):
+        os.environ["PT_AMD_LANES"] = lanes
+        try:
+            pt = PathTracer(s, _gui(sortbyMaterial=sort), spp=6)
+        finally:
+            os.environ.pop("PT_AMD_LANES", None)
+        st = torch.cuda.Stream()
+        dst = torch.empty((40, 48, 3), dtype=torch.float32, device="cuda")
+        with torch.cuda.stream(st):
+            for k in range(6):
+                pt.render_pass(1 + 6 * k, st)
+            pt.copy_image_to(dst.data_ptr(), st)
+        st.synchronize()
+        got = dst.cpu().numpy()
+        ref = None
+        for k in range(6):
+            ref, _ = O.render_pass(o, _oflags(_gui(sortbyMaterial=sort)), 1 + 6 * k, spp=6, image=ref)
+        pt.free()
+        _assert_bitexact(got, ref, f"async lanes {lanes} sort {sort}")
+
+
 @pytest.mark.parametrize("spp", [1, 2])
 def test_config3_full_size_sorted_bitexact(cornell_path, tmp_path, spp):
     """BASELINE.json config 3 at its full size — cornell geometry at 1920x1080, DEPTH 16,
