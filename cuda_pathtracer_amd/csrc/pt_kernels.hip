@@ -23,6 +23,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
+#include <cstdio>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -120,6 +122,7 @@ struct KArgs {
     int32_t refill_min;    // k_traverse: idle lanes that trigger a refill (kRefillMin; PT_AMD_REFILL)
     int32_t tchunk;        // k_traverse: largest ray chunk per ticket grab (kTravChunk; PT_AMD_TCHUNK)
     int32_t stack_rows;    // k_traverse: LDS stack entries per thread (HybStack)
+    const uint32_t* cmask; // first bounce: per 64 tile pixels, the geoms its camera rays can hit (null: all)
 };
 
 // ------------------------------------------------------------------------------------------
@@ -694,9 +697,12 @@ __device__ __forceinline__ float exact_geom(const LGeom& L, f3 r_o, f3 r_d, int&
 // PRE: scenes with meshes whose BVH closest hit `mh` came from k_traverse.  The owning mesh geom
 // (the first in index order whose triangle range holds the hit, intersect_scene's rule) enters as an
 // exactly evaluated hit before the exact tests; mesh geoms have no bound (bkind 0).
+// gmask (wave-uniform): geoms outside it cannot be hit by this wave's rays (the first bounce's
+// camera-ray masks, pt_ctx::cmask) and are skipped; a geom no ray can hit is never a candidate
+// whose absence changes the result (every geom that can be hit is still bounded and tested).
 template <bool SEL, bool PRE = false>
 __device__ __forceinline__ Hit intersect_bounded(const SceneDev& S, const FlagsDev& fl, const LGeom* s_geoms, f3 ro,
-                                                 f3 rd, const MeshHit* mh = nullptr) {
+                                                 f3 rd, const MeshHit* mh = nullptr, uint32_t gmask = ~0u) {
     const float rl = __builtin_amdgcn_sqrtf(dot(rd, rd));
     bool plain = !(rl > 0.5f && rl < 2.0f);   // NaN / degenerate direction: the plain loop
     float t_min = kFLT_MAX;
@@ -745,10 +751,14 @@ __device__ __forceinline__ Hit intersect_bounded(const SceneDev& S, const FlagsD
             lo1 = c1 ? lo : lo1;
             g1 = c1 ? i : g1;
         };
-        for (int j = S.bk[3]; j < S.bk[4]; ++j) insert(bound_geom<3, SEL>(B[j], ro, rd, invd, rl, rinf), B[j].orig);
-        for (int j = S.bk[4]; j < S.bk[5]; ++j) insert(bound_geom<4, SEL>(B[j], ro, rd, invd, rl, rinf), B[j].orig);
-        for (int j = S.bk[1]; j < S.bk[2]; ++j) insert(bound_geom<1, SEL>(B[j], ro, rd, invd, rl, rinf), B[j].orig);
-        for (int j = S.bk[2]; j < S.bk[3]; ++j) insert(bound_geom<2, SEL>(B[j], ro, rd, invd, rl, rinf), B[j].orig);
+        for (int j = S.bk[3]; j < S.bk[4]; ++j)
+            if ((gmask >> B[j].orig) & 1u) insert(bound_geom<3, SEL>(B[j], ro, rd, invd, rl, rinf), B[j].orig);
+        for (int j = S.bk[4]; j < S.bk[5]; ++j)
+            if ((gmask >> B[j].orig) & 1u) insert(bound_geom<4, SEL>(B[j], ro, rd, invd, rl, rinf), B[j].orig);
+        for (int j = S.bk[1]; j < S.bk[2]; ++j)
+            if ((gmask >> B[j].orig) & 1u) insert(bound_geom<1, SEL>(B[j], ro, rd, invd, rl, rinf), B[j].orig);
+        for (int j = S.bk[2]; j < S.bk[3]; ++j)
+            if ((gmask >> B[j].orig) & 1u) insert(bound_geom<2, SEL>(B[j], ro, rd, invd, rl, rinf), B[j].orig);
         // pass 2: exact tests in increasing-bound order while a bound does not exceed the best hit
         auto take = [&](int gi) {
             int code;
@@ -808,9 +818,9 @@ __device__ __forceinline__ Hit intersect_bounded(const SceneDev& S, const FlagsD
 // kernel's code stays small): verify with PT_PIPELINE=split, whose rays are the fused kernel's.
 template <bool MESH, bool CHECK, bool SEL = false>
 __device__ __forceinline__ Hit closest_hit(const SceneDev& S, const FlagsDev& fl, const LGeom* s_geoms, f3 ro, f3 rd,
-                                           uint32_t* mismatch) {
+                                           uint32_t* mismatch, uint32_t gmask = ~0u) {
     if (MESH || S.ngeoms > kLdsGeoms) return intersect_scene<MESH>(S, fl, ro, rd);
-    const Hit h = intersect_bounded<SEL>(S, fl, s_geoms, ro, rd);
+    const Hit h = intersect_bounded<SEL>(S, fl, s_geoms, ro, rd, nullptr, gmask);
     if (CHECK && fl.verify) {
         const Hit r = intersect_scene<false>(S, fl, ro, rd);
         if (__float_as_uint(h.t) != __float_as_uint(r.t) || h.mat != r.mat ||
@@ -1540,7 +1550,12 @@ __global__ __launch_bounds__(kBlock, FIRST || MESH ? 1 : PT_LATER_WAVES) void k_
                 mh.id = mh.any ? __float_as_int(A.S.tris[mh.idx].a[3]) : -1;
                 h = intersect_bounded<!FIRST, true>(A.S, A.fl, s_geoms, p.o, p.d, &mh);
             } else {
-                h = closest_hit<MESH == kMeshInline, false, !FIRST>(A.S, A.fl, s_geoms, p.o, p.d, &A.stats->bound_mismatch);
+                uint32_t gm = ~0u;
+                if (FIRST && A.cmask) {   // this wave's 64 tile pixels (64-aligned: chunk and tiles are)
+                    const int lp0 = __builtin_amdgcn_readfirstlane(i - it_base);
+                    gm = A.cmask[lp0 >> 6];
+                }
+                h = closest_hit<MESH == kMeshInline, false, !FIRST>(A.S, A.fl, s_geoms, p.o, p.d, &A.stats->bound_mismatch, gm);
             }
             STAMP(t2);
             const int key = A.fl.rng_pixel ? slot_pixel(A.cam, A.tile, p.slot) : i - it_base;
@@ -1819,7 +1834,12 @@ __global__ __launch_bounds__(kBlock, MESH ? 1 : PT_PRODUCE_WAVES) void k_sort_pr
                     retire<SPP1>(A, p);
                 }
             }
-            if (alive) h = closest_hit<MESH, true, !FIRST>(A.S, A.fl, s_geoms, p.o, p.d, &A.stats->bound_mismatch);
+            uint32_t gm = ~0u;
+            if (FIRST && A.cmask) {   // the wave's 64 pixels of its iteration (tiles are 256-aligned)
+                const int lp0 = __builtin_amdgcn_readfirstlane(idx - it_base);
+                gm = A.cmask[lp0 >> 6];
+            }
+            if (alive) h = closest_hit<MESH, true, !FIRST>(A.S, A.fl, s_geoms, p.o, p.d, &A.stats->bound_mismatch, gm);
         }
         const int key = alive ? (h.t == -1.0f ? 0 : h.mat) : -1;   // misses keep materialId 0 (pathtrace.cu:466)
         emit_cnt += (uint32_t)__popcll(__ballot(emitted));
@@ -2108,6 +2128,7 @@ struct pt_ctx {
     size_t ev_used = 0;
     size_t path_cap = 0;          // entries per path buffer (>= P, see pt_create)
     std::vector<DGeom> hgeoms;    // host copy of the geom table (bounds re-derived by pt_set_flags)
+    uint32_t* d_cmask = nullptr;  // first-bounce geom masks, one per 64 tile pixels (build_cmask)
     DGeom* d_geoms = nullptr;
     DGeom* d_bgeoms = nullptr;    // the same geoms ordered by bound kind (SceneDev::bgeoms)
     double scene_ext = 0.0;       // max |coordinate| over every surface and the camera position
@@ -2326,6 +2347,162 @@ void update_bounds(pt_ctx* c, float aperture) {
         d.tslack = (float)(1.0 - 4.0 * std::sqrt(dev) - std::ldexp(1.0, -14));
     }
     c->args.S.abs_slack = (float)std::ldexp(R + 1.0, -17);
+}
+
+// ---- first-bounce geom masks ----------------------------------------------------------------
+// A wave of the first bounce traces 64 consecutive tile pixels of one iteration.  Every camera
+// ray of those pixels (any SSAA jitter in [0, 1) pixel, any lens sample within the aperture) is
+//   o + s (F - o), s >= 0,   o in cam.pos + [-a, a]^2 x {0},   F in the focal-plane image of the
+// pixels' rectangle (DoF; raygen's focus point, pathtrace.cu:203-224), or
+//   cam.pos + s v,           v in the span of the rectangle's view vectors (no DoF).
+// Bounding o and F - o (or v) by boxes and asking, axis by axis, for a common s >= 0 at which the
+// ray box meets a geom's world box gives a conservative "can hit" test (never false for a ray that
+// hits).  The geom's box is its test region [slo, shi]^3 (already wider than the exact test's
+// rounding, update_bounds) mapped by the exact inverse of `inv`, padded again.  A geom outside the
+// mask is skipped by the bounds pass of those rays: the closest hit is unchanged (intersect_bounded).
+static bool beam_meets_box(const double olo[3], const double ohi[3], const double dlo[3], const double dhi[3],
+                           const double blo[3], const double bhi[3]) {
+    double smin = 0.0, smax = HUGE_VAL;
+    for (int k = 0; k < 3; ++k) {
+        // o_lo + s d_lo <= b_hi  and  o_hi + s d_hi >= b_lo  (the ray box's extent along axis k at s)
+        const double c1 = bhi[k] - olo[k], c2 = blo[k] - ohi[k];
+        if (dlo[k] > 0.0) smax = std::min(smax, c1 / dlo[k]);
+        else if (dlo[k] < 0.0) smin = std::max(smin, c1 / dlo[k]);
+        else if (c1 < 0.0) return false;
+        if (dhi[k] > 0.0) smin = std::max(smin, c2 / dhi[k]);
+        else if (dhi[k] < 0.0) smax = std::min(smax, c2 / dhi[k]);
+        else if (c2 > 0.0) return false;
+    }
+    return smin <= smax * (1.0 + 1e-9) + 1e-12;
+}
+
+int build_cmask(pt_ctx* c) {
+    KArgs& A = c->args;
+    A.cmask = nullptr;
+    const int ng = A.S.ngeoms;
+    const char* off = std::getenv("PT_AMD_NO_CMASK");
+    if ((off && std::strcmp(off, "1") == 0) || ng <= 0 || ng > kLdsGeoms || A.S.ntris > 0) return PT_OK;
+    const TileDev& T = A.tile;
+    const CamDev& cam = A.cam;
+    const size_t nblk = ((size_t)T.npix + 63) / 64;
+    if (!c->d_cmask)
+        if (int rc = c->alloc(&c->d_cmask, nblk)) return rc;
+    // world boxes of the geoms' test regions
+    std::vector<std::array<double, 6>> gb((size_t)ng);
+    std::vector<bool> always((size_t)ng, false);
+    for (int g = 0; g < ng; ++g) {
+        const DGeom& d = c->hgeoms[(size_t)g];
+        if (d.type != PT_GEOM_CUBE && d.type != PT_GEOM_SPHERE) { always[(size_t)g] = true; continue; }
+        double M[3][3], X[3][3];
+        for (int r = 0; r < 3; ++r)
+            for (int k = 0; k < 3; ++k) M[r][k] = d.inv.c[k][r];   // q = M p + t
+        const double det = M[0][0] * (M[1][1] * M[2][2] - M[1][2] * M[2][1]) -
+                           M[0][1] * (M[1][0] * M[2][2] - M[1][2] * M[2][0]) +
+                           M[0][2] * (M[1][0] * M[2][1] - M[1][1] * M[2][0]);
+        if (!(std::fabs(det) > 0.0) || !std::isfinite(det)) { always[(size_t)g] = true; continue; }
+        for (int r = 0; r < 3; ++r)
+            for (int k = 0; k < 3; ++k) {
+                const int r1 = (k + 1) % 3, r2 = (k + 2) % 3, k1 = (r + 1) % 3, k2 = (r + 2) % 3;
+                X[r][k] = (M[r1][k1] * M[r2][k2] - M[r1][k2] * M[r2][k1]) / det;
+            }
+        const double rs = d.type == PT_GEOM_SPHERE ? std::sqrt(std::max(0.0, (double)d.r2w)) : 0.0;
+        double lo[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, hi[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
+        for (int corner = 0; corner < 8; ++corner) {
+            double q[3];
+            for (int k = 0; k < 3; ++k) {
+                const double a = std::min((double)d.slo[k], -rs), b = std::max((double)d.shi[k], rs);
+                q[k] = ((corner >> k) & 1 ? b : a) * (1.0 + 1e-4) - d.inv.c[3][k];
+            }
+            for (int r = 0; r < 3; ++r) {
+                const double v = X[r][0] * q[0] + X[r][1] * q[1] + X[r][2] * q[2];
+                lo[r] = std::min(lo[r], v);
+                hi[r] = std::max(hi[r], v);
+            }
+        }
+        for (int r = 0; r < 3; ++r) {
+            const double pad = 1e-3 + 1e-5 * std::max(std::fabs(lo[r]), std::fabs(hi[r]));
+            gb[(size_t)g][r] = lo[r] - pad;
+            gb[(size_t)g][3 + r] = hi[r] + pad;
+        }
+        if (!std::isfinite(gb[(size_t)g][0] + gb[(size_t)g][1] + gb[(size_t)g][2] + gb[(size_t)g][3] +
+                           gb[(size_t)g][4] + gb[(size_t)g][5]))
+            always[(size_t)g] = true;
+    }
+    const double pos[3] = {cam.pos[0], cam.pos[1], cam.pos[2]};
+    const double jit = A.fl.ssaa ? 1.0 : 0.0, eps = 0.01;   // pixel units
+    const bool dof = A.fl.dof != 0;
+    const double ap = std::fabs((double)A.fl.aperture), focal = A.fl.focal;
+    // rays of tile row `row`, tile columns [x0, x1]: their geoms
+    auto row_mask = [&](int row, int x0, int x1) -> uint32_t {
+        const int y = row * T.world + T.rank;
+        const double ax0 = x0 - cam.res[0] * 0.5 - eps, ax1 = x1 - cam.res[0] * 0.5 + jit + eps;
+        const double ay0 = y - cam.res[1] * 0.5 - eps, ay1 = y - cam.res[1] * 0.5 + jit + eps;
+        double v[4][3];
+        for (int q = 0; q < 4; ++q) {
+            const double ax = q & 1 ? ax1 : ax0, ay = q & 2 ? ay1 : ay0;
+            for (int k = 0; k < 3; ++k)
+                v[q][k] = (double)cam.view[k] - (double)cam.right[k] * cam.pl[0] * ax - (double)cam.up[k] * cam.pl[1] * ay;
+        }
+        double olo[3], ohi[3], dlo[3], dhi[3];
+        if (!dof) {
+            for (int k = 0; k < 3; ++k) {
+                olo[k] = pos[k] - 1e-4 * (1.0 + std::fabs(pos[k]));
+                ohi[k] = pos[k] + 1e-4 * (1.0 + std::fabs(pos[k]));
+                dlo[k] = std::min({v[0][k], v[1][k], v[2][k], v[3][k]});
+                dhi[k] = std::max({v[0][k], v[1][k], v[2][k], v[3][k]});
+                const double m = 1e-5 * (std::fabs(dlo[k]) + std::fabs(dhi[k]) + 1e-3);
+                dlo[k] -= m;
+                dhi[k] += m;
+            }
+        } else {
+            double flo[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, fhi[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
+            int sign = 0;
+            for (int q = 0; q < 4; ++q) {
+                const double n = std::sqrt(v[q][0] * v[q][0] + v[q][1] * v[q][1] + v[q][2] * v[q][2]);
+                const int sg = v[q][2] > 0.0 ? 1 : -1;
+                if (!(std::fabs(v[q][2]) > 1e-3 * n) || (sign != 0 && sg != sign)) return ~0u;   // focus plane unbounded
+                sign = sg;
+                for (int k = 0; k < 3; ++k) {
+                    const double f = pos[k] + focal * v[q][k] / std::fabs(v[q][2]);
+                    flo[k] = std::min(flo[k], f);
+                    fhi[k] = std::max(fhi[k], f);
+                }
+            }
+            for (int k = 0; k < 3; ++k) {
+                const double fp = 1e-4 * (1.0 + std::fabs(flo[k]) + std::fabs(fhi[k]));
+                const double a = k < 2 ? ap * (1.0 + 1e-4) + 1e-6 : 1e-6;
+                olo[k] = pos[k] - a - 1e-4 * (1.0 + std::fabs(pos[k]));
+                ohi[k] = pos[k] + a + 1e-4 * (1.0 + std::fabs(pos[k]));
+                dlo[k] = (flo[k] - fp) - ohi[k];
+                dhi[k] = (fhi[k] + fp) - olo[k];
+            }
+        }
+        uint32_t m = 0u;
+        for (int g = 0; g < ng; ++g)
+            if (always[(size_t)g] || beam_meets_box(olo, ohi, dlo, dhi, &gb[(size_t)g][0], &gb[(size_t)g][3]))
+                m |= 1u << g;
+        return m;
+    };
+    std::vector<uint32_t> mask(nblk, 0u);
+    for (size_t b = 0; b < nblk; ++b) {
+        const int lp0 = (int)(b * 64), lp1 = std::min(T.npix - 1, lp0 + 63);
+        const int r0 = lp0 / T.W, r1 = lp1 / T.W;
+        uint32_t m = 0u;
+        for (int r = r0; r <= r1; ++r)
+            m |= row_mask(r, r == r0 ? lp0 - r * T.W : 0, r == r1 ? lp1 - r * T.W : T.W - 1);
+        mask[b] = m;
+    }
+    if (const char* st = std::getenv("PT_AMD_CMASK_STATS")) {
+        if (std::strcmp(st, "1") == 0) {
+            double tot = 0.0;
+            for (uint32_t m : mask) tot += __builtin_popcount(m);
+            std::fprintf(stderr, "[pt_amd] camera masks: %zu blocks, %.2f of %d geoms per block\n", nblk, tot / (double)nblk, ng);
+        }
+    }
+    hipError_t e = hipMemcpy(c->d_cmask, mask.data(), nblk * sizeof(uint32_t), hipMemcpyHostToDevice);
+    if (e != hipSuccess) return pt::fail(PT_ERR_HIP, std::string("camera masks: ") + hipGetErrorString(e));
+    A.cmask = c->d_cmask;
+    return PT_OK;
 }
 
 // One block of 4P planes per parity: the fused / split pipelines use the first three as the
@@ -2837,6 +3014,7 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
                 if (int rc = c->alloc(&ss.uv[h], 2 * cap)) return bail(rc);
     }
     if (const char* pl = std::getenv("PT_PIPELINE")) c->fused = std::string(pl) != "split";
+    if (int rc = build_cmask(c)) return bail(rc);
     *out = c;
     return PT_OK;
 }
@@ -2859,7 +3037,8 @@ int pt_set_flags(pt_ctx* c, const pt_flags* f) {
         HIP_TRY(hipMemcpy(c->d_geoms, c->hgeoms.data(), c->hgeoms.size() * sizeof(DGeom), hipMemcpyHostToDevice));
         if (int rc = upload_bound_order(c)) return rc;
     }
-    return PT_OK;
+    HIP_TRY(hipDeviceSynchronize());   // (queued first bounces still read the old masks)
+    return build_cmask(c);   // SSAA / DoF / aperture / focal distance bound the camera rays
 }
 
 int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {

@@ -475,6 +475,34 @@ def test_concurrent_contexts_on_two_streams(cornell_path, room_path, spp, kw):
     _assert_bitexact(g2, r2, "room on stream 2")
 
 
+def test_camera_masks_verified_random_cameras(tmp_path, monkeypatch):
+    """First-bounce geom masks under random cameras (inside and outside the scene, fov 20-110 deg,
+    apertures up to 2, near and far focus, SSAA / DoF on and off) over stress scenes of rotated,
+    thin and overlapping primitives: every camera ray's masked closest hit equals the plain loop
+    over all geoms (PT_AMD_VERIFY_BOUNDS=1 in the material-sorted producer counts differences)."""
+    from cuda_pathtracer_amd import PathTracer, Scene, scenes
+    monkeypatch.setenv("PT_AMD_VERIFY_BOUNDS", "1")
+    rng = np.random.default_rng(2024)
+    rays = 0
+    for k in range(8):
+        s = Scene(scenes.random_primitives(tmp_path / f"s{k}", n=20, res=(48, 36), seed=100 + k))
+        eye = rng.uniform((-4.5, 0.5, -4.5), (4.5, 9.5, 12.0))
+        look = rng.uniform((-5, 0, -5), (5, 10, 5))
+        s.set_camera((int(rng.integers(40, 90)), int(rng.integers(20, 60))), float(rng.uniform(20, 110)),
+                     tuple(eye), tuple(look), (0, 1, 0))
+        s.finalize()
+        g = _gui(sortbyMaterial=True, SSAA=bool(k & 1), DoF=bool(k & 2) or k == 0,
+                 aperture=float(rng.uniform(0.0, 2.0)), focal_len=float(rng.uniform(0.5, 15.0)))
+        pt = PathTracer(s, g, spp=2)
+        for it in (1, 3):
+            pt.render_pass(it)
+        st = pt.stats()
+        pt.free()
+        assert st["bound_mismatch"] == 0, (k, st["bound_mismatch"])
+        rays += st["bounce_live"][0]
+    assert rays > 20_000
+
+
 def test_bounded_closest_hit_equals_plain_loop(config_scenes, monkeypatch):
     """The bounded closest-hit pass (pt_kernels.hip intersect_bounded) selects the same geom, t
     and normal bits as the plain per-geom loop for every ray of several passes of stress scenes
@@ -621,6 +649,43 @@ def test_two_lanes_equal_one_lane(cornell_path, monkeypatch, spp, lanes, sort):
         pt.free()
     _assert_bitexact(out[0][0], out[1][0], f"{lanes} lanes vs one, spp {spp} sort {sort}")
     assert out[0][1:] == out[1][1:]
+
+
+@pytest.mark.parametrize("cam,kw,shard", [
+    (((53, 37), 45.0, (0, 5, 10.5), (0, 5, 0)), dict(), (0, 1)),                         # 53 px rows: blocks span rows
+    (((70, 30), 80.0, (3.5, 8.0, 4.0), (-2, 1, -3)), dict(aperture=1.5, focal_len=4.0, sortbyMaterial=True), (0, 1)),   # wide lens, near focus, sorted
+    (((64, 48), 30.0, (0.5, 2.0, 3.0), (-1, 4, -1)), dict(SSAA=False, DoF=False), (1, 3)),   # inside the box, shard 1 of 3
+    (((40, 40), 100.0, (-4.5, 9.5, 4.5), (4, 0, -4)), dict(DoF=False), (2, 4)),          # grazing views of the walls
+])
+def test_first_bounce_camera_masks(cornell_path, monkeypatch, cam, kw, shard):
+    """First-bounce geom masks (pt_kernels.hip build_cmask): each wave of camera rays bounds only
+    the geoms its 64 pixels' rays can reach.  Odd widths, shards, wide apertures, cameras inside the
+    scene and grazing views: GPU == oracle bit for bit, and == the same context without masks
+    (PT_AMD_NO_CMASK=1).  Then flags changed through pt_set_flags (masks rebuilt) still match."""
+    from cuda_pathtracer_amd import PathTracer, Scene
+    res, fovy, eye, look = cam
+    rank, world = shard
+    s = Scene(cornell_path)
+    s.set_camera(res, fovy, eye, look, (0, 1, 0))
+    s.finalize()
+    o = O.OracleScene.from_json(cornell_path)
+    o.set_camera(res, fovy, eye, look, (0, 1, 0))
+    g, r, _, _ = _run(s, o, _gui(**kw), iters=4, rank=rank, world=world, spp=2)
+    _assert_bitexact(g, r, f"masks {cam} {kw}")
+    monkeypatch.setenv("PT_AMD_NO_CMASK", "1")
+    g2, _, _, _ = _run(s, o, _gui(**kw), iters=4, rank=rank, world=world, spp=2)
+    monkeypatch.delenv("PT_AMD_NO_CMASK")
+    _assert_bitexact(g, g2, "masks on vs off")
+    kw2 = dict(kw, aperture=0.8, focal_len=9.0, SSAA=not kw.get("SSAA", True), DoF=True)
+    pt = PathTracer(s, _gui(**kw), rank=rank, world=world, spp=2)
+    pt.set_flags(_gui(**kw2))
+    img = None
+    for it in (1, 3):
+        pt.render_pass(it)
+        img, _ = O.render_pass(o, _oflags(_gui(**kw2)), it, spp=2, rank=rank, world=world, image=img)
+    gi = pt.image()
+    pt.free()
+    _assert_bitexact(gi, img, f"masks after set_flags {kw2}")
 
 
 @pytest.mark.parametrize("sort", [False, True])
