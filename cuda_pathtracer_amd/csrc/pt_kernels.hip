@@ -700,6 +700,7 @@ __device__ __forceinline__ float exact_geom(const LGeom& L, f3 r_o, f3 r_d, int&
 // gmask (wave-uniform): geoms outside it cannot be hit by this wave's rays (the first bounce's
 // camera-ray masks, pt_ctx::cmask) and are skipped; a geom no ray can hit is never a candidate
 // whose absence changes the result (every geom that can be hit is still bounded and tested).
+__device__ __forceinline__ uint32_t ng_all_mask(int n) { return n >= 32 ? ~0u : (1u << n) - 1u; }
 template <bool SEL, bool PRE = false>
 __device__ __forceinline__ Hit intersect_bounded(const SceneDev& S, const FlagsDev& fl, const LGeom* s_geoms, f3 ro,
                                                  f3 rd, const MeshHit* mh = nullptr, uint32_t gmask = ~0u) {
@@ -734,7 +735,6 @@ __device__ __forceinline__ Hit intersect_bounded(const SceneDev& S, const FlagsD
         // pass 1: the three smallest lower bounds (scene data wave-uniform: scalar loads)
         float lo1 = kInf, lo2 = kInf, lo3 = kInf;
         int g1 = -1, g2 = -1;
-        uint32_t cand = 0u;   // every geom with a finite bound
         const float rinf = fmaxf(fmaxf(fabsf(ro.x), fabsf(ro.y)), fabsf(ro.z));
         const f3 invd = F3(__builtin_amdgcn_rcpf(rd.x), __builtin_amdgcn_rcpf(rd.y), __builtin_amdgcn_rcpf(rd.z));
         // one branch-free loop per bound kind (geoms sorted by kind on the host), so the scalar
@@ -743,7 +743,6 @@ __device__ __forceinline__ Hit intersect_bounded(const SceneDev& S, const FlagsD
         const auto* B = as_const(S.bgeoms);
         auto insert = [&](float lo, int i) {
             lo -= S.abs_slack;
-            cand |= lo < kInf ? (1u << i) : 0u;
             const bool c1 = lo < lo1, c2 = lo < lo2, c3 = lo < lo3;
             lo3 = c2 ? lo2 : (c3 ? lo : lo3);
             lo2 = c1 ? lo1 : (c2 ? lo : lo2);
@@ -786,8 +785,10 @@ __device__ __forceinline__ Hit intersect_bounded(const SceneDev& S, const FlagsD
             }
         }
 #endif
-        if (lo3 <= t_min) {   // a third candidate (rare): every remaining geom with a finite bound
-            uint32_t m = cand & ~(1u << g1) & ~(1u << g2);
+        if (lo3 <= t_min) {   // a third candidate (rare: 0 rays on Cornell and config 4): the exact test of
+            // every other geom the wave may hit (one with no finite bound misses exactly, so testing it
+            // changes nothing; not tracking the candidate set saves 4 VALU per geom and ray)
+            uint32_t m = (ng_all_mask(S.ngeoms) & gmask) & ~(1u << g1) & ~(1u << g2);
             while (m) {
                 take(__builtin_ctz(m));
                 m &= m - 1u;
