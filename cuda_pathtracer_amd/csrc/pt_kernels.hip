@@ -982,8 +982,17 @@ __device__ __forceinline__ void raygen(const CamDev& cam, const FlagsDev& fl, co
     raygen_at(cam, fl, T, slot, s, slot - s * T.npix, p);
 }
 
+// Path planes stream through HBM once per bounce (GBs per lane, far beyond the Infinity Cache):
+// non-temporal loads and stores (PT_NO_NT_PATHS: plain ones).
+#ifdef PT_NO_NT_PATHS
+#define PT_LD(p) (*(p))
+#define PT_ST(v, p) (*(p) = (v))
+#else
+#define PT_LD(p) __builtin_nontemporal_load(p)
+#define PT_ST(v, p) __builtin_nontemporal_store((v), (p))
+#endif
 __device__ __forceinline__ void load_path(const PathSoA& B, int i, PathReg& p) {
-    const v4f a = B.a[i], b = B.b[i], c = B.c[i];
+    const v4f a = PT_LD(B.a + i), b = PT_LD(B.b + i), c = PT_LD(B.c + i);
     p.o = F3(a[0], a[1], a[2]);
     p.d = F3(a[3], b[0], b[1]);
     p.c = F3(b[2], b[3], c[0]);
@@ -991,9 +1000,9 @@ __device__ __forceinline__ void load_path(const PathSoA& B, int i, PathReg& p) {
     p.bounces = __float_as_int(c[2]);
 }
 __device__ __forceinline__ void store_path(const PathSoA& B, int i, const PathReg& p) {
-    B.a[i] = v4f{p.o.x, p.o.y, p.o.z, p.d.x};
-    B.b[i] = v4f{p.d.y, p.d.z, p.c.x, p.c.y};
-    B.c[i] = v4f{p.c.z, __int_as_float(p.slot), __int_as_float(p.bounces), 0.0f};
+    PT_ST((v4f{p.o.x, p.o.y, p.o.z, p.d.x}), B.a + i);
+    PT_ST((v4f{p.d.y, p.d.z, p.c.x, p.c.y}), B.b + i);
+    PT_ST((v4f{p.c.z, __int_as_float(p.slot), __int_as_float(p.bounces), 0.0f}), B.c + i);
 }
 
 // A path that terminated this bounce: its colour is final (finalGather, pathtrace.cu:347-356).
@@ -1007,7 +1016,7 @@ __device__ __forceinline__ void retire(const KArgs& A, const PathReg& p) {
             px[2] += p.c.z;
         }
     } else {
-        A.colbuf[p.slot] = v4f{p.c.x, p.c.y, p.c.z, 0.0f};
+        PT_ST((v4f{p.c.x, p.c.y, p.c.z, 0.0f}), A.colbuf + p.slot);
     }
 }
 
