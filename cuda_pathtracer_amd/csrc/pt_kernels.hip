@@ -1016,7 +1016,7 @@ __device__ __forceinline__ void retire(const KArgs& A, const PathReg& p) {
             px[2] += p.c.z;
         }
     } else {
-        PT_ST((v4f{p.c.x, p.c.y, p.c.z, 0.0f}), A.colbuf + p.slot);
+        A.colbuf[p.slot] = v4f{p.c.x, p.c.y, p.c.z, 0.0f};   // (scattered: plain, so L2 can merge neighbours)
     }
 }
 
@@ -1306,7 +1306,7 @@ __global__ __launch_bounds__(kBlock) void k_traverse(const KArgs A) {
             if (s_pre[mid] <= k) lo = mid; else hi = mid - 1;
         }
         const int q = lo * chunk + (k - s_pre[lo]);
-        const v4f a = A.in.a[q], b = A.in.b[q];
+        const v4f a = PT_LD(A.in.a + q), b = PT_LD(A.in.b + q);
         o = F3(a[0], a[1], a[2]);
         d = F3(a[3], b[0], b[1]);
         return q;
@@ -1320,7 +1320,7 @@ __global__ __launch_bounds__(kBlock) void k_traverse(const KArgs A) {
             f3 o, d;
             const int q = ray(k, o, d);
             const MeshHit r = bvh_walk(S, o, d, A.fl.bvh_cull != 0, st);
-            A.mhit[q] = v4f{r.t, __int_as_float(r.any ? r.idx : -1), r.bx, r.by};
+            PT_ST((v4f{r.t, __int_as_float(r.any ? r.idx : -1), r.bx, r.by}), A.mhit + q);
         }
         return;
     }
@@ -1377,7 +1377,7 @@ __global__ __launch_bounds__(kBlock) void k_traverse(const KArgs A) {
                         enter(S.root_code);
                         have = true;
                     } else {   // misses the whole tree
-                        A.mhit[q] = v4f{r.t, __int_as_float(-1), r.bx, r.by};
+                        PT_ST((v4f{r.t, __int_as_float(-1), r.bx, r.by}), A.mhit + q);
                     }
 #ifdef PT_TRAV_STATS
                     ++n_rays;
@@ -1435,7 +1435,7 @@ __global__ __launch_bounds__(kBlock) void k_traverse(const KArgs A) {
                 next = (h1 || h2) ? (h1 ? c1 : c2) : (top == 0 ? kWalkDone : st.get(--top));
             }
             if (next == kWalkDone) {
-                A.mhit[q] = v4f{r.t, __int_as_float(r.any ? r.idx : -1), r.bx, r.by};
+                PT_ST((v4f{r.t, __int_as_float(r.any ? r.idx : -1), r.bx, r.by}), A.mhit + q);
                 have = false;
             } else if (next != kWalkNone) {
                 enter(next);
@@ -1550,7 +1550,7 @@ __global__ __launch_bounds__(kBlock, FIRST || MESH ? 1 : PT_LATER_WAVES) void k_
             STAMP(t1);
             Hit h;
             if constexpr (MESH == kMeshPre) {
-                const v4f m = A.mhit[q];
+                const v4f m = PT_LD(A.mhit + q);
                 MeshHit mh;
                 mh.t = m[0];
                 mh.idx = __float_as_int(m[1]);
@@ -1818,6 +1818,7 @@ __global__ __launch_bounds__(kBlock, MESH ? 1 : PT_PRODUCE_WAVES) void k_sort_pr
             } else {
                 const int j = SA.perm[idx];
                 const v4f* r = srec(A.in, j);
+                // (plain loads: a gather of 64-byte records whose four 16-byte pieces share a line)
                 const v4f r0 = r[0], r1 = r[1], r2 = r[2], r3 = r[3];
                 p.o = F3(r0[0], r0[1], r0[2]);
                 p.d = F3(r0[3], r1[0], r1[1]);
@@ -1881,6 +1882,8 @@ __global__ __launch_bounds__(kBlock, MESH ? 1 : PT_PRODUCE_WAVES) void k_sort_pr
             for (int w = 0; w < wave; ++w) kb += KC(k & 1, w, key);
             const int q = t * kBlock + (int)(before + rank);
             v4f* r = srec(A.out, q);
+            // (plain stores: each store instruction covers 16 of every 64 bytes, and L2 merges the
+            // four into whole lines; non-temporal ones halved config 3's rate)
             r[0] = v4f{p.o.x, p.o.y, p.o.z, p.d.x};
             r[1] = v4f{p.d.y, p.d.z, p.c.x, p.c.y};
             r[2] = v4f{p.c.z, __int_as_float(p.slot), h.t, __int_as_float(key)};
@@ -2046,7 +2049,7 @@ __global__ void k_finalize_spp(float* __restrict__ image, const v4f* __restrict_
     for (int lp = blockIdx.x * blockDim.x + threadIdx.x; lp < npix; lp += gridDim.x * blockDim.x) {
         float r = image[3 * (size_t)lp], g = image[3 * (size_t)lp + 1], b = image[3 * (size_t)lp + 2];
         for (int s = 0; s < spp; ++s) {
-            const v4f c = col[(size_t)s * npix + lp];
+            const v4f c = PT_LD(col + (size_t)s * npix + lp);
             r += c[0]; g += c[1]; b += c[2];
         }
         image[3 * (size_t)lp] = r; image[3 * (size_t)lp + 1] = g; image[3 * (size_t)lp + 2] = b;
