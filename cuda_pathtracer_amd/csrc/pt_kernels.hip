@@ -1951,8 +1951,8 @@ __global__ __launch_bounds__(kBlock) void k_sort_scatter(const KArgs A, const So
 // the tile sums (one workgroup), rescan.  No workgroup waits on another, so unlike the library's
 // single-pass scan (whose static schedule needs its whole grid co-resident) two of these can run
 // side by side.  The histogram is small (nmats x paths / 64 ints) and cache-resident.
-constexpr int kHistPer = 16;                       // ints per thread
-constexpr int kHistTile = kBlock * kHistPer;       // 4096
+constexpr int kHistPer = 4;                        // ints per thread (one 16-byte load)
+constexpr int kHistTile = kBlock * kHistPer;       // 1024: 4x the workgroups of 4096 (latency-bound scan)
 
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_w, uint32_t* total) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1967,7 +1967,7 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_w, u
 }
 
 typedef int v4i_h __attribute__((ext_vector_type(4)));
-// this thread's 16 consecutive ints (four 16-byte loads; guarded at the end of the array)
+// this thread's kHistPer consecutive ints (16-byte loads; guarded at the end of the array)
 __device__ __forceinline__ void hist_load(const int32_t* __restrict__ in, int64_t n, int64_t base, uint32_t (&x)[kHistPer]) {
     if (base + kHistPer <= n) {
 #pragma unroll
