@@ -1749,7 +1749,8 @@ __device__ __forceinline__ int tile_iteration(const int32_t* s_tb, int spp, int 
 }
 
 #ifndef PT_PRODUCE_WAVES
-#define PT_PRODUCE_WAVES 1   // (A/B knob: minimum waves per SIMD of the analytic producer)
+#define PT_PRODUCE_WAVES 7   // (A/B knob: minimum waves per SIMD of the analytic producer; 7 caps the
+                             // first bounce's producer at 72 VGPRs: config 3 +0.8% on the same box)
 #endif
 template <bool FIRST, bool SPP1, bool MESH>
 __global__ __launch_bounds__(kBlock, MESH ? 1 : PT_PRODUCE_WAVES) void k_sort_produce(const KArgs A, const SortArgs SA) {
