@@ -1088,7 +1088,15 @@ __global__ __launch_bounds__(kBlock) void k_trace(const KArgs A) {
             PathReg p;
             if (FIRST) raygen(A.cam, A.fl, A.tile, i, p);
             else load_path(A.in, i, p);
-            const Hit h = closest_hit<MESH, true, !FIRST>(A.S, A.fl, s_geoms, p.o, p.d, &A.stats->bound_mismatch);
+            uint32_t gm = ~0u;
+            if (FIRST && A.cmask) {   // the wave's 64 consecutive slots: up to two pixel blocks, or four
+                const int np = A.tile.npix;   // when they wrap into the next iteration
+                const int i0 = __builtin_amdgcn_readfirstlane(i);
+                const int l0 = i0 % np, l1 = min(i0 + 63, N - 1) % np;
+                gm = A.cmask[l0 >> 6] | A.cmask[(l1 >= l0 ? l1 : np - 1) >> 6];
+                if (l1 < l0) gm |= A.cmask[0] | A.cmask[l1 >> 6];
+            }
+            const Hit h = closest_hit<MESH, true, !FIRST>(A.S, A.fl, s_geoms, p.o, p.d, &A.stats->bound_mismatch, gm);
             const int it = SPP1 ? 0 : p.slot / A.tile.npix;
             const int iter = A.tile.iter_first + it;
             // key: index within the path's own iteration (k_iter_bases; see k_bounce)
