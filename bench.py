@@ -405,7 +405,7 @@ def main() -> None:
     mesh = scene.counts()[2] > 0
     # k_bounce<FIRST, SPP1, MESH mode>: mesh scenes run mode 2 (closest mesh hit from k_traverse)
     kprefix = f"k_bounce<false, {'true' if spp == 1 else 'false'}, {2 if mesh else 0}>"
-    kernel_name = ("material-sorted pipeline (k_sort_produce: shade + compact + intersect / histogram scan / k_sort_scatter)" if sorted_ else kprefix)
+    kernel_name = ("material-sorted pipeline (k_sort_produce: shade + compact + intersect / histogram scan + permutation)" if sorted_ else kprefix)
     kernel_min = 0
     for b in range(1, depth):
         n_out = plive[b + 1] if b + 1 < depth else 0

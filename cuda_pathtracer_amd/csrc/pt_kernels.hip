@@ -16,8 +16,8 @@
 //     one path per iteration, so this equals finalGather); spp > 1 passes write per-slot colours
 //     and a finalize kernel adds them in sample order;
 //   * material-sorted shading (flag) = stable counting sort over (iteration, material) keys:
-//     k_sort_isect (hit + histogram), one library scan, k_sort_scatter, k_sort_shade (shade in
-//     sorted order + segmented compaction);
+//     one producer per bounce (shade in sorted order, compact by material per tile, intersect,
+//     histogram), a three-kernel histogram scan whose last kernel also writes the permutation;
 //   * the split pipeline (PT_PIPELINE=split: k_trace + look-back k_compact_paths) is kept for
 //     comparison and for the bounded-hit verification mode.
 #include <hip/hip_runtime.h>
@@ -1708,7 +1708,9 @@ __global__ __launch_bounds__(kBlock) void k_compact_paths(const KArgs A) {
 //                   64-byte record is written once, with its hit.  The first bounce's producer
 //                   generates the camera rays instead of shading.
 //                   Work unit = TILE: 256 consecutive positions of one iteration's sorted range.
-//                   Tile t's survivors go, in order, to slots [256 t, 256 t + count_t) (tcnt[t]), so
+//                   Tile t's survivors go to slots [256 t, 256 t + count_t), grouped by material
+//                   (material m's run starts at the tile's exclusive prefix base(t, m) over the
+//                   materials, each survivor at base + its rank among the tile's m-survivors), so
 //                   the survivors' logical order is the tile order — stable.  Workgroups take
 //                   tiles t = b, b + G, b + 2G, ... (G = grid): every workgroup walks the sorted
 //                   order in step with the others, so the records being gathered at any moment
@@ -1717,11 +1719,14 @@ __global__ __launch_bounds__(kBlock) void k_compact_paths(const KArgs A) {
 //                   every iteration of the pass at once.
 //                   Sort keys are counted per tile: hist[iteration][material][tile of that
 //                   iteration], and every survivor gets its rank among the same-material survivors
-//                   of its tile (one ballot per material present in the wave);
+//                   of its tile (one ballot per material present in the wave); hslot holds the
+//                   first slot of each (iteration, material, tile) run, 256 t + base(t, m);
 //   scan            of the histogram (k_hist_sums / k_hist_scan_sums / k_hist_apply, no co-residency
 //                   needed): tiles are in logical order, so hist's flat exclusive scan + the in-tile
-//                   rank IS the survivor's position in the stable sort by (iteration, material);
-//   k_sort_scatter  perm[sorted position] = physical slot.
+//                   rank IS the survivor's position in the stable sort by (iteration, material).
+//                   Run e's survivors are consecutive in both orders, so k_hist_apply, once it has
+//                   offs[e], writes perm[offs[e] + r] = hslot[e] + r (r < hist[e]) itself: whole
+//                   runs of coalesced stores, no scatter kernel and no per-survivor sort key.
 // Batched passes sort every iteration on its own (stable sort by (iteration, material), as `spp`
 // sequential pathtrace() calls would): tiles never span two iterations, and an iteration's tiles
 // form one block of the histogram.
@@ -1732,15 +1737,14 @@ __global__ __launch_bounds__(kBlock) void k_compact_paths(const KArgs A) {
 __device__ __forceinline__ v4f* srec(const PathSoA& B, int j) { return B.a + ((size_t)(uint32_t)j << 2); }
 
 struct SortArgs {
-    int32_t* kr;        // [cap] per output slot: material << 24 | rank in (tile, material)
-    int32_t* tcnt;      // [cap / 256] survivors of each tile
+    int32_t* hslot;     // per (iteration, material, tile): first slot of its run (sort_hidx)
     int32_t* hist;      // per (iteration, material, tile) survivor counts (sort_hidx)
     int32_t* offs;      // its exclusive scan
     int32_t* perm;      // [P] sorted position -> physical slot
     int32_t* itb;       // [2][kMaxSpp + 1] per parity: first tile of each iteration ([spp] = tiles)
     float* uv_out;      // textured scenes: (u, v) of the output records ([2 * cap])
 };
-constexpr int kSortMaxMats = 256;  // per-tile material counts in LDS; the material is 8 bits of kr
+constexpr int kSortMaxMats = 256;  // per-tile material counts in LDS (one thread per material)
 
 // Histogram entry of tile t (iteration tiles [t0, t1)) for material m: [iteration block][material][tile].
 __device__ __forceinline__ size_t sort_hidx(int t0, int t1, int nmats, int t, int m) {
@@ -1756,6 +1760,18 @@ __device__ __forceinline__ int tile_iteration(const int32_t* s_tb, int spp, int 
     return lo;
 }
 
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_w, uint32_t* total) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t incl = lb::wave_inclusive_scan(v);
+    __syncthreads();   // previous users of s_w are done
+    if (lane == 63) s_w[wave] = incl;
+    __syncthreads();
+    uint32_t before = 0;
+    for (int w = 0; w < wave; ++w) before += s_w[w];
+    *total = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+    return before + incl - v;
+}
+
 #ifndef PT_PRODUCE_WAVES
 #define PT_PRODUCE_WAVES 7   // (A/B knob: minimum waves per SIMD of the analytic producer; 7 caps the
                              // first bounce's producer at 72 VGPRs: config 3 +0.8% on the same box)
@@ -1767,7 +1783,8 @@ __global__ __launch_bounds__(kBlock, MESH ? 1 : PT_PRODUCE_WAVES) void k_sort_pr
     __shared__ int32_t s_sb[kMaxSpp + 1];      // sorted start of every iteration (first bounce: j * npix)
     __shared__ int32_t s_tb[kMaxSpp + 1];      // first tile of every iteration ([spp] = all tiles)
     __shared__ uint32_t s_tmp[8];
-    __shared__ uint32_t s_wc[2][4];
+    __shared__ uint32_t s_mw[4];
+    __shared__ uint32_t s_base[kSortMaxMats];  // the tile's exclusive prefix over materials
     extern __shared__ uint32_t s_kc[];   // [2][4][nmats] (dynamic): per wave, survivors of each material in the tile
 #define KC(buf, w, m) s_kc[((buf) * 4 + (w)) * nmats + (m)]
     __shared__ uint32_t s_cnt;
@@ -1864,7 +1881,6 @@ __global__ __launch_bounds__(kBlock, MESH ? 1 : PT_PRODUCE_WAVES) void k_sort_pr
         const int key = alive ? (h.t == -1.0f ? 0 : h.mat) : -1;   // misses keep materialId 0 (pathtrace.cu:466)
         emit_cnt += (uint32_t)__popcll(__ballot(emitted));
         const uint64_t m = __ballot(alive);
-        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
         // this wave's row of per-material counts: cleared, then one ballot per material present ->
         // in-wave rank (lanes of that key) and the count (written by the first lane of the key).
         // Buffer k&1 was last read two tiles ago, before the previous barrier; a wave's LDS
@@ -1882,14 +1898,25 @@ __global__ __launch_bounds__(kBlock, MESH ? 1 : PT_PRODUCE_WAVES) void k_sort_pr
             if (lane == src) KC(k & 1, wave, kk) = (uint32_t)__popcll(mk);
             rem &= ~mk;
         }
-        if (lane == 0) s_wc[k & 1][wave] = (uint32_t)__popcll(m);
         __syncthreads();
-        const uint32_t w0 = s_wc[k & 1][0], w1 = s_wc[k & 1][1], w2 = s_wc[k & 1][2], w3 = s_wc[k & 1][3];
-        const uint32_t before = (wave > 0 ? w0 : 0u) + (wave > 1 ? w1 : 0u) + (wave > 2 ? w2 : 0u);
+        {   // material mm = tid: the tile's count and its run's first slot (exclusive prefix over the
+            // materials); the histogram entries of the tile
+            const int mm = tid;
+            const uint32_t cm = mm < nmats ? (KC(k & 1, 0, mm) + KC(k & 1, 1, mm)) + (KC(k & 1, 2, mm) + KC(k & 1, 3, mm)) : 0u;
+            uint32_t tot;
+            const uint32_t bm = block_excl_scan(cm, s_mw, &tot);   // (its barriers: s_base's readers are done)
+            if (mm < nmats) {
+                s_base[mm] = bm;
+                const size_t e = sort_hidx(t0, t1, nmats, t, mm);
+                SA.hist[e] = (int32_t)cm;
+                SA.hslot[e] = t * kBlock + (int32_t)bm;
+            }
+        }
+        __syncthreads();
         if (alive) {
             uint32_t kb = krank;
             for (int w = 0; w < wave; ++w) kb += KC(k & 1, w, key);
-            const int q = t * kBlock + (int)(before + rank);
+            const int q = t * kBlock + (int)(s_base[key] + kb);
             v4f* r = srec(A.out, q);
             // (plain stores: each store instruction covers 16 of every 64 bytes, and L2 merges the
             // four into whole lines; non-temporal ones halved config 3's rate)
@@ -1901,59 +1928,10 @@ __global__ __launch_bounds__(kBlock, MESH ? 1 : PT_PRODUCE_WAVES) void k_sort_pr
                 SA.uv_out[2 * (size_t)q] = h.u;
                 SA.uv_out[2 * (size_t)q + 1] = h.v;
             }
-            SA.kr[q] = (int32_t)(((uint32_t)key << 24) | kb);
-        }
-        {   // the tile's histogram entries: wave w writes materials 64 w .. 64 w + 63
-            const int mm = wave * 64 + lane;
-            if (mm < nmats)
-                SA.hist[sort_hidx(t0, t1, nmats, t, mm)] =
-                    (int32_t)((KC(k & 1, 0, mm) + KC(k & 1, 1, mm)) + (KC(k & 1, 2, mm) + KC(k & 1, 3, mm)));
-            if (tid == 0) SA.tcnt[t] = (int32_t)((w0 + w1) + (w2 + w3));
         }
     }
     flush_emissive(A, emit_cnt, &s_cnt);
 #undef KC
-}
-
-// perm[sorted position] = physical slot, for every survivor in the producer's tiles (grid-stride
-// over the tiles; a tile's slots past its survivor count are empty).
-__global__ __launch_bounds__(kBlock) void k_sort_scatter(const KArgs A, const SortArgs SA) {
-    __shared__ int32_t s_tb[kMaxSpp + 1];
-    const int par = A.parity;
-    const int nmats = A.S.nmats;
-    const int spp = A.tile.spp;
-    const int T = (int)A.ctl[par].nseg;
-    const int32_t* tb = SA.itb + (size_t)par * (kMaxSpp + 1);
-    for (int j = threadIdx.x; j <= spp; j += kBlock) s_tb[j] = tb[j];
-    __syncthreads();
-    // kU tiles per step, their loads issued together (each slot is kr -> offs -> store, dependent)
-    constexpr int kU = 4;
-    const int G = (int)gridDim.x;
-    for (int t0 = (int)blockIdx.x; t0 < T; t0 += kU * G) {
-        int q[kU];
-        size_t hb[kU];
-        int nt[kU];
-        uint32_t kr[kU];
-#pragma unroll
-        for (int u = 0; u < kU; ++u) {
-            const int t = t0 + u * G;
-            q[u] = -1;
-            if (t < T && (int)threadIdx.x < SA.tcnt[t]) {
-                const int it = tile_iteration(s_tb, spp, t);
-                q[u] = t * kBlock + (int)threadIdx.x;
-                hb[u] = sort_hidx(s_tb[it], s_tb[it + 1], nmats, t, 0);   // + key * nt
-                nt[u] = s_tb[it + 1] - s_tb[it];
-                kr[u] = (uint32_t)SA.kr[q[u]];
-            }
-        }
-        int dst[kU];
-#pragma unroll
-        for (int u = 0; u < kU; ++u)
-            if (q[u] >= 0) dst[u] = SA.offs[hb[u] + (size_t)(kr[u] >> 24) * (size_t)nt[u]] + (int)(kr[u] & 0xffffffu);
-#pragma unroll
-        for (int u = 0; u < kU; ++u)
-            if (q[u] >= 0) SA.perm[dst[u]] = q[u];
-    }
 }
 
 // Exclusive scan of the sorted pipeline's histogram when two lanes share the GPU: reduce, scan of
@@ -1962,18 +1940,6 @@ __global__ __launch_bounds__(kBlock) void k_sort_scatter(const KArgs A, const So
 // side by side.  The histogram is small (nmats x paths / 64 ints) and cache-resident.
 constexpr int kHistPer = 4;                        // ints per thread (one 16-byte load)
 constexpr int kHistTile = kBlock * kHistPer;       // 1024: 4x the workgroups of 4096 (latency-bound scan)
-
-__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_w, uint32_t* total) {
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint32_t incl = lb::wave_inclusive_scan(v);
-    __syncthreads();   // previous users of s_w are done
-    if (lane == 63) s_w[wave] = incl;
-    __syncthreads();
-    uint32_t before = 0;
-    for (int w = 0; w < wave; ++w) before += s_w[w];
-    *total = s_w[0] + s_w[1] + s_w[2] + s_w[3];
-    return before + incl - v;
-}
 
 typedef int v4i_h __attribute__((ext_vector_type(4)));
 // this thread's kHistPer consecutive ints (16-byte loads; guarded at the end of the array)
@@ -2025,8 +1991,11 @@ __global__ __launch_bounds__(kBlock) void k_hist_scan_sums(uint32_t* __restrict_
     }
 }
 
+// perm (sorted pipeline): the entries' runs, perm[offs[e] + r] = hslot[e] + r for r < in[e], for
+// the live entries but the last (the end offset, whose count is not written).
 __global__ __launch_bounds__(kBlock) void k_hist_apply(const int32_t* __restrict__ in, int32_t* __restrict__ out,
-                                                       int64_t n, const uint32_t* nlive, const uint32_t* __restrict__ sums) {
+                                                       int64_t n, const uint32_t* nlive, const uint32_t* __restrict__ sums,
+                                                       const int32_t* __restrict__ hslot, int32_t* __restrict__ perm) {
     __shared__ uint32_t s_w[4];
     n = hist_n(n, nlive);
     const int64_t base = (int64_t)blockIdx.x * kHistTile + (int64_t)threadIdx.x * kHistPer;
@@ -2036,6 +2005,24 @@ __global__ __launch_bounds__(kBlock) void k_hist_apply(const int32_t* __restrict
     for (int k = 0; k < kHistPer; ++k) v += x[k];
     uint32_t total;
     uint32_t run = block_excl_scan(v, s_w, &total) + sums[blockIdx.x];
+    if (perm) {   // the wave writes its entries' runs one after the other, 64 consecutive slots per store
+        const int lane = (int)threadIdx.x & 63;
+        uint32_t o = run;
+#pragma unroll
+        for (int k = 0; k < kHistPer; ++k) {
+            const bool live = base + k < n - 1 && x[k] != 0u;
+            const int32_t s0 = live ? hslot[base + k] : 0;
+            uint64_t rem = __ballot(live);
+            while (rem) {
+                const int src = __builtin_ctzll(rem);
+                const uint32_t ro = __builtin_amdgcn_readlane(o, src), rc = __builtin_amdgcn_readlane(x[k], src);
+                const int32_t rs = __builtin_amdgcn_readlane(s0, src);
+                for (uint32_t r = (uint32_t)lane; r < rc; r += 64) perm[ro + r] = rs + (int32_t)r;
+                rem &= rem - 1;
+            }
+            o += x[k];
+        }
+    }
     if (base + kHistPer <= n) {
 #pragma unroll
         for (int q = 0; q < kHistPer / 4; ++q) {
@@ -2177,8 +2164,8 @@ struct pt_ctx {
     uint64_t llaunches[kMaxLanes] = {};
     hipStream_t lane_stream[kMaxLanes] = {};
     hipEvent_t ev_fork = nullptr, ev_join[kMaxLanes] = {};
-    struct SortSet {   // material-sort buffers of one lane (k_sort_produce / k_sort_scatter)
-        int32_t *kr = nullptr, *tcnt = nullptr, *hist = nullptr, *offs = nullptr, *perm = nullptr, *itb = nullptr;
+    struct SortSet {   // material-sort buffers of one lane (k_sort_produce / k_hist_*)
+        int32_t *hslot = nullptr, *hist = nullptr, *offs = nullptr, *perm = nullptr, *itb = nullptr;
         float* uv[2] = {nullptr, nullptr};   // (u, v) of the records in buf[0] / buf[1]
         uint32_t* sums = nullptr;            // histogram scan: tile sums
         int64_t hist_cap = 0;                // histogram entries allocated (+ the end offset)
@@ -3016,7 +3003,7 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
         (e = hipMemset(A.status, 0, (size_t)2 * c->max_tiles * sizeof(uint64_t))) != hipSuccess ||
         (e = hipMemset(c->stats, 0, sizeof(DevStats))) != hipSuccess)
         return bail(pt::fail(PT_ERR_HIP, std::string("hipMemset: ") + hipGetErrorString(e)));
-    // material-sort buffers, per lane: kr and uv by physical slot (< cap), perm by sorted position
+    // material-sort buffers, per lane: uv by physical slot (< cap), perm by sorted position
     // (< the lane's paths), the histogram by (producer tile, material) (cap / 256 tiles at most)
     for (int l = 0; l < c->lanes; ++l) {
         auto& ss = c->sset[l];
@@ -3024,12 +3011,11 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
         const size_t paths = (size_t)n_l * (size_t)npix, cap = c->lcap[l];
         ss.hist_cap = (int64_t)((size_t)c->nmats * (cap / kBlock + 1) + 2);
         const size_t tiles = ((size_t)ss.hist_cap + kHistTile - 1) / kHistTile;
-        if (int rc = c->alloc(&ss.kr, cap)) return bail(rc);
+        if (int rc = c->alloc(&ss.hslot, (size_t)ss.hist_cap)) return bail(rc);
         if (int rc = c->alloc(&ss.perm, paths)) return bail(rc);
         if (int rc = c->alloc(&ss.hist, (size_t)ss.hist_cap)) return bail(rc);
         if (int rc = c->alloc(&ss.offs, (size_t)ss.hist_cap)) return bail(rc);
         if (int rc = c->alloc(&ss.itb, 2 * ((size_t)kMaxSpp + 1))) return bail(rc);
-        if (int rc = c->alloc(&ss.tcnt, cap / kBlock + 1)) return bail(rc);
         if (int rc = c->alloc(&ss.sums, tiles)) return bail(rc);
         if (!S.textures.empty())
             for (int h = 0; h < 2; ++h)
@@ -3092,7 +3078,7 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
             a.in = bufs[lcur];
             a.out = bufs[lcur ^ 1];
             a.hit.uv = ss.uv[lcur];
-            const SortArgs sa{ss.kr, ss.tcnt, ss.hist, ss.offs, ss.perm, ss.itb, ss.uv[lcur ^ 1]};
+            const SortArgs sa{ss.hslot, ss.hist, ss.offs, ss.perm, ss.itb, ss.uv[lcur ^ 1]};
             hipLaunchKernelGGL(produce_kernel(first, spp1, mesh), dim3(c->grid_bounce[0]), dim3(kBlock),
                                (size_t)8 * c->nmats * sizeof(uint32_t), s, a, sa);
             HIP_TRY(hipGetLastError());
@@ -3108,9 +3094,7 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
         hipLaunchKernelGGL(k_hist_sums, dim3(tiles), dim3(kBlock), 0, s, (const int32_t*)ss.hist, ss.hist_cap, nlive, ss.sums);
         hipLaunchKernelGGL(k_hist_scan_sums, dim3(1), dim3(kBlock), 0, s, ss.sums, ss.hist_cap, nlive);
         hipLaunchKernelGGL(k_hist_apply, dim3(tiles), dim3(kBlock), 0, s, (const int32_t*)ss.hist, ss.offs, ss.hist_cap,
-                           nlive, (const uint32_t*)ss.sums);
-        const SortArgs sa{ss.kr, ss.tcnt, ss.hist, ss.offs, ss.perm, ss.itb, nullptr};
-        hipLaunchKernelGGL(k_sort_scatter, dim3(c->grid_trace), dim3(kBlock), 0, s, a, sa);
+                           nlive, (const uint32_t*)ss.sums, (const int32_t*)ss.hslot, ss.perm);
         HIP_TRY(hipGetLastError());
         if (int rc = produce(false)) return rc;
         return prof_end(ev, s);
