@@ -211,10 +211,17 @@ def _pmc_leg(args, scene_path, spp_pass, sorted_, avg_ms, kernel_prefix, seg_per
             return {"pmc": res["_passes"]}
         total = sum(m["bytes_per_launch"] * m["launches"] for m in ks.values())
         segs = res.get("segments") or 0
-        return {"pmc": res["_passes"], "traffic_per_segment": total / segs if segs else None,
-                "traffic_definition": "FETCH_SIZE x 2 + WRITE_SIZE of every sorted-pipeline kernel over the "
-                                      "profiled passes / their traced segments (all bounces)",
-                "traffic_kernels": sorted(ks)}
+        out = {"pmc": res["_passes"], "traffic_per_segment": total / segs if segs else None,
+               "traffic_definition": "FETCH_SIZE x 2 + WRITE_SIZE of every sorted-pipeline kernel over the "
+                                     "profiled passes / their traced segments (all bounces); traffic = that x "
+                                     "segments per pipeline bounce, like algorithmic_bytes_per_launch",
+               "traffic_kernels": sorted(ks)}
+        if segs:
+            out["traffic"] = total / segs * seg_per_launch
+            out["traffic_frac"] = out["traffic"] / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
+            if out["traffic_frac"] < 0.5:   # measured traffic far below the HBM peak (as for k_bounce)
+                out["bound"] = "issue"
+        return out
     m = pmc.pick(res, kernel_prefix)
     if m is None or "bytes_per_launch" not in m:
         return {"pmc": res["_passes"]}
