@@ -340,7 +340,14 @@ def main() -> None:
     gui.bvhCull = bool(args.bvh_cull)
     scene = P.Scene(scene_path)
     st_r = scene.state()
-    spp = world * max(1, args.spp)          # iterations per pass of this rank's rows
+    # PT_BENCH_SHARD_OF=N (1 process only): trace exactly rank 0's share of an N-GPU strong-scaling
+    # step alone on one GPU, no gather — a rehearsal of the per-rank time at N GPUs (value = rank 0's
+    # segments / time, not a whole-job number), never the bench line of an N-GPU run
+    shard_of = int(os.environ.get("PT_BENCH_SHARD_OF", "0") or 0)
+    if shard_of and world != 1:
+        raise SystemExit("PT_BENCH_SHARD_OF is a single-process rehearsal")
+    sw = shard_of or world                  # the shard layout: rows y % sw == rank
+    spp = sw * max(1, args.spp)             # iterations per pass of this rank's rows
     passes_per_step = 1
     if args.scaling == "strong":
         passes_per_step = max(1, args.samples // spp)
@@ -349,7 +356,7 @@ def main() -> None:
         spp = args.samples // passes_per_step
     if spp > 256:   # pt_shard.spp limit (one thread of the bounce kernel's workgroup per iteration)
         raise SystemExit(f"{spp} iterations per pass > 256 (pt_shard.spp limit)")
-    pt = P.PathTracer(scene, gui, rank=rank, world=world, spp=spp)
+    pt = P.PathTracer(scene, gui, rank=rank, world=sw, spp=spp)
     stream = torch.cuda.current_stream()
     _log(rank, f"[bench] {args.scaling} scaling: tile rows={pt.rows} npix={pt.npix} paths/pass={pt.npaths} "
                f"passes/step={passes_per_step} depth={st_r.traceDepth}")
@@ -468,7 +475,8 @@ def main() -> None:
                        "samples_per_step": (args.samples if strong else spp * world),
                        "iterations_per_pass": spp, "passes_per_step": passes_per_step,
                        "paths_per_gpu_per_pass": pt.npaths,
-                       "parallelism": f"pixel rows x{world} + RCCL gather"},
+                       "parallelism": f"pixel rows x{world} + RCCL gather" if not shard_of else
+                                      f"REHEARSAL: rank 0's rows of a x{shard_of} shard, alone on one GPU"},
             "roofline": roofline,
             "segments": seg_all,
             "bounce_live_per_step": [x / args.steps for x in live],
