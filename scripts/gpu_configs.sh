@@ -1,5 +1,5 @@
 # Bench lines for BASELINE.json configs 3-5 (1 GPU), each under its own time limit.
-# Iterations per pass: the bench defaults (128 for config 3, 64 for config 4, 8 for the 100k-triangle config 5).
+# Iterations per pass: the bench defaults (128 for config 3, 64 for config 4, 32 for the 100k-triangle config 5).
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"; mkdir -p gpurun_out
@@ -11,8 +11,8 @@ run() {   # name, extra args
 }
 run cornell_hd_sorted --steps 10 || exit 1
 run multi_object_4k --steps 5 || exit 1
-run random_triangles_100k --steps 3 --spp 8 --samples 8 || exit 1
-run random_triangles_100k --steps 3 --spp 8 --samples 8 --bvh-cull || exit 1
+run random_triangles_100k --steps 2 --spp 32 --samples 32 || exit 1
+run random_triangles_100k --steps 2 --spp 32 --samples 32 --bvh-cull || exit 1
 python3 - <<'PY'
 import json
 for line in open("gpurun_out/configs.jsonl"):
