@@ -278,7 +278,7 @@ def main() -> None:
     ap.add_argument("--spp", type=int, default=None,
                     help="iterations per pass and GPU-share: a pass traces spp x N iterations of the rank's rows "
                          "(so every GPU's pass has the 1-GPU pass's size); results are bit-identical to one "
-                         "iteration per pass (default: 128 for cornell and config 3, 64 for config 4, 32 for config 5)")
+                         "iteration per pass (default: 128 for cornell, 256 for config 3, 64 for config 4, 32 for config 5)")
     ap.add_argument("--scaling", choices=["strong", "weak"], default="strong",
                     help="strong (default): a step renders a FIXED batch of --samples samples per pixel of the "
                          "whole image, split over the N GPUs by rows (cornell: 2 passes of 128 iterations at N=1, "
@@ -287,7 +287,7 @@ def main() -> None:
     ap.add_argument("--samples", type=int, default=256, help="strong scaling: samples per pixel per step")
     args = ap.parse_args()
     if args.spp is None:   # iterations per pass, measured per workload
-        args.spp = {"cornell": 128, "cornell_hd_sorted": 128, "multi_object_4k": 64, "random_triangles_100k": 32}[args.config]
+        args.spp = {"cornell": 128, "cornell_hd_sorted": 256, "multi_object_4k": 64, "random_triangles_100k": 32}[args.config]
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -1,5 +1,5 @@
 # Bench lines for BASELINE.json configs 3-5 (1 GPU), each under its own time limit.
-# Iterations per pass: the bench defaults (128 for config 3, 64 for config 4, 32 for the 100k-triangle config 5).
+# Iterations per pass: the bench defaults (256 for config 3, 64 for config 4, 32 for the 100k-triangle config 5).
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"; mkdir -p gpurun_out
