@@ -1,29 +1,37 @@
 """Benchmark: Mray/s (paths x bounces / s) on the bundled Cornell scene + scan GB/s vs HBM peak.
 
 Workload (BASELINE.json configs[1]): path_tracer/scenes/cornell.json as-is — 800x800, DEPTH 8,
-default flags.  A step is one render pass.  On N GPUs (one process per GPU, torchrun) rank r owns
-the image rows y % N == r; a pass traces `--spp` (default 128) iterations of those rows per GPU
-share, i.e. spp*N samples per pixel of the rank's rows, so every GPU traces spp*800*800 camera
-paths per step (weak scaling).  Batching iterations into one pass is bit-identical to tracing
-them one pass at a time (tests/test_render_gpu.py::test_tiles_and_batched_samples); it fills the
-GPU during the short tail bounces.  --spp 1 is exactly the reference's pathtrace() per step.
-After the timed passes the float tiles are gathered to rank 0 with one RCCL gather (inside the
-timed region).  value = all ranks' traced segments / max-over-ranks wall time / 1e6.
+default flags.  A step renders a FIXED 256 samples per pixel of the whole image (strong scaling,
+the default): on N GPUs (one process per GPU, torchrun) rank r owns the image rows y % N == r and
+traces its rows' 256 iterations as passes of `--spp` iterations (default 128 at N = 1: 2 passes;
+one pass of 256 from N = 2), so the work per step is the same at every N and the driver's 1/2/4/8
+values measure speed-up.  Batching iterations into one pass is bit-identical to tracing them one
+pass at a time (tests/test_render_gpu.py::test_batched_pass_equals_sequential_passes); --spp 1
+--samples 1 is exactly the reference's pathtrace() per step.  --scaling weak: a step is one pass of
+spp x N iterations of the rank's rows per GPU.  After the timed passes the float tiles are gathered
+to rank 0 with one RCCL gather (inside the timed region, timed separately as gather_ms; one
+untimed gather of the same shape before the timed region sets up RCCL's connections).
+value = all ranks' traced segments / max-over-ranks wall time / 1e6.
 
-Roofline: the dominant kernel is the fused bounce kernel k_bounce<false,...> (bounces >= 1).
-Its average launch time comes from HIP events recorded on its launch stream over a profiled
-segment of the same workload (rocprofv3 --kernel-trace --stats of the same command agrees:
-profiles/r02_*); its algorithmic bytes per launch are SURVEY.md §8d's 184 B per traced segment
-(ray 24 + hit write 28 + hit read 28 + path read 48 + write 48 + compaction 8) x the segments that
-launch traces.  roofline.frac = those bytes / the average launch duration / 8 TB/s,
-per launch.  Batched passes run two lanes of iterations whose launches overlap; the bytes over the
-union of the launch intervals are reported separately (roofline.aggregate).  The fused kernel itself
-needs only 44 B in + 44 B per survivor + 24 B per emissive hit (kernel_min_bytes).
+Roofline: the dominant kernel of analytic scenes is the fused bounce kernel k_bounce<false,...>
+(bounces >= 1); of mesh scenes (config 5) the BVH walk k_traverse4<false> (bounces >= 1), with the
+bounce kernel that follows it reported beside it (roofline.bounce_kernel).  Average launch times
+come from HIP events recorded on the launch stream, per kernel kind, over a profiled segment of the
+same workload (rocprofv3 --kernel-trace --stats of the same command agrees: profiles/r0*_*); the
+algorithmic bytes per launch are SURVEY.md §8d's 184 B per traced segment (ray 24 + hit write 28 +
+hit read 28 + path read 48 + write 48 + compaction 8) x the segments that launch traces
+(DESIGN.md §4).  roofline.frac = those bytes / the average launch duration / 8 TB/s, per launch;
+roofline.step_frac = the same bytes of every bounce of a step / ms_per_step / 8 TB/s.  Batched
+passes run two lanes of iterations whose launches overlap; the bytes over the union of the launch
+intervals are reported separately (roofline.aggregate).  The fused kernel itself needs only 44 B in
++ 44 B per survivor + 24 B per emissive hit (kernel_min_bytes).
 Measured in the same run (N = 1): rocprofv3 --pmc passes over the same workload (scripts/pmc.py)
 give the kernel's fabric traffic per launch (roofline.traffic, FETCH_SIZE x 2 + WRITE_SIZE) and its
 VALU wave-instructions (roofline.valu_issue: against the chip's VALU issue rate, 256 CUs x 4 SIMDs x
-2.4 GHz / 2 cycles per wave64 instruction, MI355X_MICROARCH.md) — the kernel is issue/latency-bound,
-not bandwidth-bound (roofline.limiter).
+2.4 GHz / 2 cycles per wave64 instruction, MI355X_MICROARCH.md) — the kernels are issue/latency-
+bound, not bandwidth-bound (roofline.limiter).  For the BVH walk also its memory instructions, L2
+hit rate and, with the diagnostic counter build present (scripts/trav_build.sh), the walk's lane
+counters (scripts/trav_stats.py).
 The scan kernel is measured separately at n = 2^28 (8 B/element, 2 GiB, beyond the 256 MiB MALL).
 """
 from __future__ import annotations
@@ -194,15 +202,18 @@ def compact_bench(torch, dev, n: int, reps: int) -> dict:
     return {"n": n, "kept": kept, "ms": ms, "GB/s": gbs, "frac": gbs / HBM_PEAK_GBS, "verified": ok}
 
 
-def _pmc_leg(args, scene_path, spp_pass, sorted_, avg_ms, kernel_prefix, seg_per_launch, busy_ms, launches):
+def _pmc_leg(args, scene_path, spp_pass, sorted_, avg_ms, kernel_prefix, seg_per_launch, busy_ms, launches,
+             walk=False):
     """rocprofv3 --pmc passes over the same workload (scripts/pmc.py): fabric traffic and VALU
-    wave-instructions per launch of the dominant kernel, and its wave-state split."""
+    wave-instructions per launch of the dominant kernel, and its wave-state split; for the BVH walk
+    (walk=True) also its memory instructions and L2 hit rate."""
     sys.path.insert(0, str(ROOT / "scripts"))
     import pmc
     wl = [str(args.pmc_passes), f"spp={spp_pass}", f"scene={scene_path}"] + (["sort"] if sorted_ else []) + \
          (["bvhcull"] if args.bvh_cull else [])
     out_dir = ROOT / "gpurun_out" / "bench_pmc"
-    res = pmc.collect(wl, out_dir, timeout=args.pmc_timeout)
+    groups = ("fetch", "write", "sq") + (("l2", "vmem") if walk else ())
+    res = pmc.collect(wl, out_dir, timeout=args.pmc_timeout, groups=groups)
     (out_dir / "summary.json").write_text(json.dumps(res, indent=1))
     if sorted_:   # the sorted pipeline: every kernel of a bounce, per traced segment
         ks = {k: m for k, m in res.get("kernels", {}).items()
@@ -253,6 +264,38 @@ def _pmc_leg(args, scene_path, spp_pass, sorted_, avg_ms, kernel_prefix, seg_per
         # stays the prescribed 184 B / launch time / HBM peak)
         if out["traffic_frac"] < 0.5:
             out["bound"] = "issue"
+    if walk:
+        if "TCC_HIT_sum" in m:
+            out["l2_hit_rate"] = m["TCC_HIT_sum"] / max(m["TCC_HIT_sum"] + m.get("TCC_MISS_sum", 0.0), 1.0)
+        if "SQ_INSTS_VMEM_RD" in m:
+            out["vmem_rd_per_launch"] = m["SQ_INSTS_VMEM_RD"]
+            out["vmem_rd_per_segment"] = m["SQ_INSTS_VMEM_RD"] / max(seg_per_launch, 1.0)
+        out["salu_per_segment"] = (m.get("SQ_INSTS_SALU") or 0.0) / max(seg_per_launch, 1.0)
+    return out
+
+
+def _walk_counters(scene_path, spp_pass, timeout=300) -> dict | None:
+    """The BVH walk's lane counters from the diagnostic build (scripts/trav_build.sh ->
+    cuda_pathtracer_amd/build/libpt_amd_trav.so; scripts/trav_stats.py), one pass of the same
+    scene in a subprocess, or None when the diagnostic library is absent."""
+    import subprocess
+    if not (ROOT / "cuda_pathtracer_amd" / "build" / "libpt_amd_trav.so").exists():
+        return None
+    try:
+        r = subprocess.run([sys.executable, str(ROOT / "scripts" / "trav_stats.py"), str(scene_path), str(spp_pass)],
+                           capture_output=True, text=True, timeout=timeout, cwd=str(ROOT))
+    except subprocess.TimeoutExpired:
+        return {"error": "timeout"}
+    line = (r.stdout.strip().splitlines() or [""])[-1]
+    out: dict = {"rc": r.returncode}
+    for kv in line.split():
+        if "=" in kv:
+            k, v = kv.split("=", 1)
+            try:
+                out[k] = float(v) if "." in v else int(v)
+            except ValueError:
+                out[k] = v
+    out["definition"] = "scripts/trav_stats.py (diagnostic -DPT_TRAV_STATS build, one pass of the same scene)"
     return out
 
 
@@ -268,6 +311,8 @@ def main() -> None:
     ap.add_argument("--no-scan", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 --pmc passes (traffic, VALU issue)")
     ap.add_argument("--pmc-passes", type=int, default=6)
+    ap.add_argument("--no-walk-counters", action="store_true",
+                    help="mesh scenes: skip the BVH walk's lane counters (diagnostic build, scripts/trav_stats.py)")
     ap.add_argument("--pmc-timeout", type=int, default=150)
     ap.add_argument("--scene", default=str(ROOT / "tests" / "scenes" / "cornell.json"))
     ap.add_argument("--config", default="cornell", choices=["cornell", "cornell_hd_sorted", "multi_object_4k",
@@ -319,6 +364,7 @@ def main() -> None:
 
     import cuda_pathtracer_amd as P
     from cuda_pathtracer_amd import distributed as D
+    from cuda_pathtracer_amd._native import lib as _native_lib
     P.lib()
 
     from cuda_pathtracer_amd import scenes as SG
@@ -370,6 +416,10 @@ def main() -> None:
 
     rows_all = None
     tile = torch.empty((pt.rows, pt.width, 3), dtype=torch.float32, device=dev)
+    H = scene.camera().res[1]
+    if dist is not None:   # untimed gather of the real tile shape: RCCL connects its peers on first use
+        pt.copy_image_to(tile.data_ptr(), stream)
+        D.gather_tiles(torch, dist, tile, H)
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps * passes_per_step):
@@ -377,11 +427,19 @@ def main() -> None:
         it += spp
     # single RCCL gather of the framebuffer tiles to rank 0
     pt.copy_image_to(tile.data_ptr(), stream)
+    gather_ms = None
     if dist is not None:
-        rows_all = D.gather_tiles(torch, dist, tile, scene.camera().res[1])
+        torch.cuda.synchronize()   # (the render had to finish before the gather anyway)
+        tg = time.perf_counter()
+        rows_all = D.gather_tiles(torch, dist, tile, H)
+        torch.cuda.synchronize()
+        gather_ms = (time.perf_counter() - tg) * 1e3
     barrier()
     elapsed = time.perf_counter() - t0
     s1 = pt.stats()
+    gather_ms_min = None
+    if dist is not None:   # the last rank to arrive waits least: its gather time is the collective's own
+        gather_ms_min = -D.max_over_ranks(torch, dist, -gather_ms, dev)
 
     # Kernel-level timing for the roofline: a profiled segment of the same workload right after
     # the timed region (HIP events bracket every launch on its stream; events inside the timed
@@ -406,43 +464,68 @@ def main() -> None:
         seg_all = D.sum_over_ranks(torch, dist, seg, dev)
 
     # roofline of the dominant kernel (bounces >= 1), over the profiled segment
-    b_ms, b_n, b_busy = prof["bounce"]
-    sorted_ = bool(gui.sortbyMaterial)
-    if b_n == 0:   # material-sorted pipeline: its kernels are all profiled under "sort"
-        b_ms, b_n = prof["sort"][0], max(1, prof_passes * (st_r.traceDepth - 1))
-        b_busy = prof["sort"][2]   # union over both lanes (includes the first bounce's sort kernels)
-    f_ms, f_n, _ = prof["first_bounce"]
     depth = st_r.traceDepth
     plive = [b - a for a, b in zip(sp0["bounce_live"], sp1["bounce_live"])]
     pemit = [b - a for a, b in zip(sp0["bounce_emit"], sp1["bounce_emit"])]
     seg_bounce = sum(plive[1:depth])
+    sorted_ = bool(gui.sortbyMaterial)
+    b_ms, b_n, b_busy = prof["bounce"]
+    if sorted_:   # material-sorted pipeline: every producer after the first + its histogram scans
+        b_ms, b_n, b_busy = prof["sort"]
+    t_ms, t_n, t_busy = prof["traverse"]
+    walk = t_n > 0   # mesh scene with the BVH walk in its own kernel (k_traverse / k_traverse4)
+    f_ms, f_n, _ = prof["first_bounce"]
     mesh = scene.counts()[2] > 0
+    quads = walk and not args.bvh_cull and os.environ.get("PT_AMD_TRAV") != "pairs" and \
+        _native_lib().pt_scene_bvh_quads(scene.handle, None, 0, None, None) > 0
     # k_bounce<FIRST, SPP1, MESH mode>: mesh scenes run mode 2 (closest mesh hit from k_traverse)
-    kprefix = f"k_bounce<false, {'true' if spp == 1 else 'false'}, {2 if mesh else 0}>"
-    kernel_name = ("material-sorted pipeline (k_sort_produce: shade + compact + intersect / histogram scan + permutation)" if sorted_ else kprefix)
+    bprefix = f"k_bounce<false, {'true' if spp == 1 else 'false'}, {2 if mesh else 0}>"
+    wprefix = "k_traverse4<false>" if quads else "k_traverse<false>"
+    kprefix = wprefix if walk else bprefix
+    kernel_name = ("material-sorted pipeline (k_sort_produce: shade + compact + intersect / histogram scan + permutation)"
+                   if sorted_ else kprefix)
     kernel_min = 0
     for b in range(1, depth):
         n_out = plive[b + 1] if b + 1 < depth else 0
         kernel_min += PATH_BYTES * plive[b] + PATH_BYTES * n_out + FB_RMW_BYTES * pemit[b]
-    per_launch_bytes = SEGMENT_BYTES * seg_bounce / max(b_n, 1)
-    avg_ms = b_ms / max(b_n, 1)
+    k_ms, k_n, k_busy = (t_ms, t_n, t_busy) if walk else (b_ms, b_n, b_busy)
+    per_launch_bytes = SEGMENT_BYTES * seg_bounce / max(k_n, 1)
+    avg_ms = k_ms / max(k_n, 1)
     achieved = per_launch_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     default_lanes = 3 if sorted_ and pt.npaths >= (48 << 20) else 2   # pt_kernels.hip kThreeLanePaths
     lanes = min(int(os.environ.get("PT_AMD_LANES", str(default_lanes))), spp, 4) \
         if (spp > 1 and (sorted_ or os.environ.get("PT_PIPELINE") != "split")) else 1
+    # every bounce's algorithmic bytes (184 B per segment) of one step over the step time: the
+    # byte metric at step level (near 1.0 it is saturated and stops being evidence; VALU issue is
+    # the limiter then, roofline.valu_issue)
+    step_seg = seg / max(args.steps, 1)
     roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                 "definition": "184 B (SURVEY.md §8d) x segments per launch / HIP-event average launch duration",
-                "kernel": kernel_name, "avg_launch_ms": avg_ms, "launches": b_n, "lanes": lanes,
-                "segments_per_launch": seg_bounce / max(b_n, 1),
+                "kernel": kernel_name, "avg_launch_ms": avg_ms, "launches": k_n, "lanes": lanes,
+                "segments_per_launch": seg_bounce / max(k_n, 1),
                 "algorithmic_bytes_per_launch": per_launch_bytes,
-                "kernel_min_bytes_per_launch": kernel_min / max(b_n, 1),
+                "step_frac": SEGMENT_BYTES * step_seg / (elapsed / max(args.steps, 1)) / 1e9 / HBM_PEAK_GBS
+                if world == 1 else None,
+                "step_frac_definition": "184 B x traced segments of one step (all bounces) / ms_per_step / 8 TB/s",
                 # two lanes' launches overlap: the same bytes over the union of the launch intervals
-                "aggregate": {"busy_ms": b_busy,
-                              "achieved": SEGMENT_BYTES * seg_bounce / (b_busy * 1e-3) / 1e9 if b_busy > 0 else 0.0,
-                              "frac": SEGMENT_BYTES * seg_bounce / (b_busy * 1e-3) / 1e9 / HBM_PEAK_GBS
-                              if b_busy > 0 else 0.0,
+                "aggregate": {"busy_ms": k_busy,
+                              "achieved": SEGMENT_BYTES * seg_bounce / (k_busy * 1e-3) / 1e9 if k_busy > 0 else 0.0,
+                              "frac": SEGMENT_BYTES * seg_bounce / (k_busy * 1e-3) / 1e9 / HBM_PEAK_GBS
+                              if k_busy > 0 else 0.0,
                               "definition": "184 B x segments of bounces >= 1 / union of their launch intervals"}}
+    if not walk:
+        roofline["kernel_min_bytes_per_launch"] = kernel_min / max(b_n, 1)
+    else:   # the bounce kernel after the walk (bounded closest hit with the mesh hit + shade + compact)
+        bb = SEGMENT_BYTES * seg_bounce / max(b_n, 1)
+        b_avg = b_ms / max(b_n, 1)
+        roofline["bounce_kernel"] = {
+            "kernel": bprefix, "avg_launch_ms": b_avg, "launches": b_n,
+            "achieved": bb / (b_avg * 1e-3) / 1e9 if b_avg > 0 else 0.0,
+            "frac": bb / (b_avg * 1e-3) / 1e9 / HBM_PEAK_GBS if b_avg > 0 else 0.0,
+            "kernel_min_bytes_per_launch": kernel_min / max(b_n, 1)}
+        roofline["walk_share_of_gpu_time"] = t_ms / max(t_ms + b_ms + f_ms + prof["first_traverse"][0], 1e-9)
+        roofline["first_traverse_avg_ms"] = prof["first_traverse"][0] / max(prof["first_traverse"][1], 1)
 
     result = None
     if rank == 0:
@@ -475,12 +558,16 @@ def main() -> None:
                        "samples_per_step": (args.samples if strong else spp * world),
                        "iterations_per_pass": spp, "passes_per_step": passes_per_step,
                        "paths_per_gpu_per_pass": pt.npaths,
-                       "parallelism": f"pixel rows x{world} + RCCL gather" if not shard_of else
+                       "parallelism": (f"pixel rows x{world} (world_size {world}, backend "
+                                       f"{dist.get_backend() if dist is not None else 'none'}) + one gather")
+                                      if not shard_of else
                                       f"REHEARSAL: rank 0's rows of a x{shard_of} shard, alone on one GPU"},
             "roofline": roofline,
             "segments": seg_all,
             "bounce_live_per_step": [x / args.steps for x in live],
             "first_bounce_avg_ms": f_ms / max(f_n, 1),
+            "gather_ms": gather_ms,
+            "gather_ms_last_rank": gather_ms_min,
         }
         if not args.no_scan:
             result["scan"] = scan_bench(torch, dev, args.scan_n, args.scan_reps)
@@ -500,10 +587,13 @@ def main() -> None:
     pt.free()
     if rank == 0 and world == 1 and not args.no_pmc:
         try:
-            extra = _pmc_leg(args, scene_path, spp, sorted_, avg_ms, kprefix, seg_bounce / max(b_n, 1), b_busy, b_n)
+            extra = _pmc_leg(args, scene_path, spp, sorted_, avg_ms, kprefix, seg_bounce / max(k_n, 1), k_busy, k_n,
+                             walk=walk)
         except Exception as e:   # profiling is evidence, not the measurement: never fail the bench line
             extra = {"pmc_error": repr(e)}
         roofline.update(extra)
+    if rank == 0 and world == 1 and walk and not args.no_walk_counters:
+        roofline["walk_counters"] = _walk_counters(scene_path, spp)
     if rank == 0:
         print(json.dumps(result), flush=True)
 

@@ -101,6 +101,7 @@ SIGNATURES = {
     "pt_last_error": (C.c_char_p, []),
     "pt_flags_default": (None, [C.POINTER(Flags)]),
     "pt_scene_load_json": (_I, [C.c_char_p, C.POINTER(_P)]),
+    "pt_scene_load_json_ex": (_I, [C.c_char_p, C.c_uint32, C.POINTER(_P)]),
     "pt_scene_create": (_I, [C.POINTER(_P)]),
     "pt_scene_free": (None, [_P]),
     "pt_scene_add_material": (_I, [_P, C.POINTER(Material), _IP]),
@@ -119,6 +120,7 @@ SIGNATURES = {
     "pt_scene_get_materials": (_I, [_P, C.POINTER(Material), _I]),
     "pt_scene_get_triangles": (_I, [_P, C.POINTER(Triangle), _I]),
     "pt_scene_get_bvh": (_I, [_P, C.POINTER(BvhNode), _I]),
+    "pt_scene_bvh_quads": (_I, [_P, _P, _I, _IP, _IP]),
     "pt_create": (_I, [_P, C.POINTER(Flags), C.POINTER(Shard), C.POINTER(_P)]),
     "pt_destroy": (_I, [_P]),
     "pt_set_flags": (_I, [_P, C.POINTER(Flags)]),
@@ -135,6 +137,7 @@ SIGNATURES = {
     "pt_selftest_math": (_I, [C.c_uint64, C.c_uint32, C.POINTER(C.c_uint64)]),
     "pt_profile_read": (_I, [_P, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
     "pt_profile_read_busy": (_I, [_P, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
+    "pt_profile_read_kinds": (_I, [_P, _I, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
     "pt_tonemap": (_I, [_P, _I, _I, _F, _P]),
     "pt_save_png": (_I, [C.c_char_p, _P, _I, _I, _F]),
     "pt_save_hdr": (_I, [C.c_char_p, _P, _I, _I, _F]),
@@ -156,7 +159,7 @@ def _preload_torch() -> None:
             pass
 
 
-_OPTIONAL = {"pt_selftest_math"}
+_OPTIONAL = {"pt_selftest_math", "pt_profile_read_kinds"}
 
 
 def lib() -> C.CDLL:

@@ -45,6 +45,8 @@ struct Huff {
     uint8_t size[257];
     uint32_t maxcode[18];   // one past the last code of each length, left-aligned to 16 bits
     int delta[17];          // symbol index - code, per length
+    int nsym;               // symbols defined (values[0 .. nsym))
+    bool defined;           // set by a DHT segment; a scan that names an undefined table fails
 };
 
 // Canonical code assignment (JPEG Annex C): lengths in symbol order, codes counting up.
@@ -66,6 +68,7 @@ bool build_huff(Huff& h, const int count[16]) {
         code <<= 1;
     }
     h.maxcode[17] = 0xffffffffu;
+    h.nsym = k;
     return true;
 }
 
@@ -84,7 +87,7 @@ struct Decoder {
     const uint8_t* end = nullptr;
     std::string err;
 
-    Huff huff_dc[4], huff_ac[4];
+    Huff huff_dc[4]{}, huff_ac[4]{};   // value-initialised: `defined` false until a DHT sets it
     uint8_t dequant[4][64] = {};
     int img_x = 0, img_y = 0, img_n = 0;
     int h_max = 1, v_max = 1, mcu_x = 0, mcu_y = 0;
@@ -126,7 +129,9 @@ struct Decoder {
         if (bits < n) fill();
         const uint32_t v = buf >> (32 - n);
         buf <<= n;
-        bits -= n;
+        // past a marker the buffer's low bits are zeros (as stb's): keep `bits` non-negative so a
+        // later fill never shifts by 32 or more (valid files never get here)
+        bits = bits >= n ? bits - n : 0;
         return v;
     }
     int bit() { return (int)take(1); }
@@ -136,13 +141,15 @@ struct Decoder {
         return (v >> (n - 1)) ? v : v - ((1 << n) - 1);
     }
     int huff_decode(const Huff& h) {
+        if (!h.defined) return -1;   // the scan names a table no DHT defined
         if (bits < 16) fill();
         const uint32_t top = buf >> 16;
         int k = 1;
         while (k <= 16 && top >= h.maxcode[k]) ++k;
-        if (k == 17) { bits -= 16; return -1; }
+        if (k == 17) { bits = bits >= 16 ? bits - 16 : 0; return -1; }
         if (k > bits) return -1;
         const int idx = (int)(buf >> (32 - k)) + h.delta[k];
+        if (idx < 0 || idx >= h.nsym) return -1;
         buf <<= k;
         bits -= k;
         return h.values[idx];
@@ -171,7 +178,7 @@ struct Decoder {
         Comp& C = comp[c];
         const uint8_t* dq = dequant[C.tq];
         const int t = huff_decode(huff_dc[C.hd]);
-        if (t < 0) return fail("bad huffman code");
+        if (t < 0 || t > 15) return fail("bad huffman code");
         std::memset(out, 0, 64 * sizeof(int16_t));
         const int diff = t ? receive_extend(t) : 0;
         C.dc_pred += diff;
@@ -196,6 +203,7 @@ struct Decoder {
         if (succ_high == 0) {
             std::memset(out, 0, 64 * sizeof(int16_t));
             const int t = huff_decode(huff_dc[comp[c].hd]);
+            if (t < 0 || t > 15) return fail("bad huffman code");
             const int diff = t ? receive_extend(t) : 0;
             comp[c].dc_pred += diff;
             out[0] = (int16_t)(comp[c].dc_pred * (1 << succ_low));
@@ -410,6 +418,7 @@ struct Decoder {
                     Huff& h = tc == 0 ? huff_dc[th] : huff_ac[th];
                     if (!build_huff(h, count)) return fail("bad code lengths");
                     for (int i = 0; i < n; ++i) h.values[i] = (uint8_t)get8();
+                    h.defined = true;
                     L -= n;
                 }
                 return L == 0 || fail("bad DHT len");
@@ -451,6 +460,12 @@ struct Decoder {
         for (int i = 0; i < img_n; ++i) {
             h_max = std::max(h_max, comp[i].h);
             v_max = std::max(v_max, comp[i].v);
+        }
+        // non-integer sampling ratios (e.g. H 3 beside H 2): stb 2.06 reads past its component
+        // planes there; rejected, as later stb versions do (valid files are unaffected)
+        for (int i = 0; i < img_n; ++i) {
+            if (h_max % comp[i].h != 0) return fail("bad H");
+            if (v_max % comp[i].v != 0) return fail("bad V");
         }
         mcu_x = (img_x + h_max * 8 - 1) / (h_max * 8);
         mcu_y = (img_y + v_max * 8 - 1) / (v_max * 8);
@@ -682,6 +697,10 @@ int load_texture_file(TextureHost& t) {
     size_t got;
     while ((got = std::fread(chunk, 1, sizeof chunk, f)) > 0) bytes.insert(bytes.end(), chunk, chunk + got);
     std::fclose(f);
+    // Not a JPEG (no SOI marker): PNG/BMP/TGA/... files that the reference's stbi_load also reads
+    // are left to the host — the texture keeps its path and no pixels, pt_scene_set_texture_pixels
+    // fills it, and pt_create refuses a scene with an unfilled texture.
+    if (bytes.size() < 2 || bytes[0] != 0xff || bytes[1] != 0xd8) return PT_OK;
     int32_t w = 0, h = 0, c = 0;
     if (decode_jpeg(bytes.data(), bytes.size(), &w, &h, &c, &t.pixels) != PT_OK)
         return fail(PT_ERR_IO, "Texture load error: " + t.path + ": " + g_err);

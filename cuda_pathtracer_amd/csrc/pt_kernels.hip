@@ -77,6 +77,8 @@ struct SceneDev {
     const struct DPair* __restrict__ pairs;   // child-pair layout of the BVH (bvh_walk_pairs)
     int32_t root_code;     // code of the root (see DPair), meaningful when pairs != nullptr
     v4f root_lo, root_hi;  // root box
+    const struct DQuad* __restrict__ quads;   // 4-wide collapse of the pair tree (k_traverse4), or null
+    int32_t root_qcode;    // root's code in the quad layout (quad index or leaf code)
 };
 struct CamDev {
     float pos[3], view[3], up[3], right[3], pl[2];
@@ -381,6 +383,24 @@ __device__ __forceinline__ MeshHit bvh_walk_pairs(const SceneDev& S, f3 o, f3 d,
     return r;
 }
 
+// 4-wide layout (k_traverse4): the pair entry of interior node N with each interior child X
+// replaced by X's own two children when both boxes lie inside X's box (checked on the host, so a
+// grandchild box that the ray hits implies a hit on X's box — the slab test is monotone in the box
+// bounds for a finite ray: (b - o) * inv is nondecreasing in b for inv > 0 and nonincreasing for
+// inv < 0, so X's slab intervals contain the grandchild's).  The leaves reached, and in the
+// near-first order below the triangles tested, are BVHIntersectionTest's (intersections.cu:170-224).
+//   Slots 0-1: N's left child's group (X's two children, or the child itself in slot 0), slots 2-3
+// the right child's.  meta bits: valid slots (0-3) | N's axis << 4 | left group's axis << 6 |
+// right group's axis << 8 (3: a one-slot group, never swapped).  Codes as DPair's, with interior
+// codes = quad index.  Boxes are SoA (one v4f per bound and axis) so the four slab tests run two
+// slots per packed f32 instruction.
+struct alignas(16) DQuad {
+    v4f lox, hix, loy, hiy, loz, hiz;
+    v4f code;   // int bits
+    v4f meta;   // [0]: int bits (above)
+};
+
+constexpr int kRecWalkHere = -2;   // k_traverse4 record: not walked (non-finite ray), k_bounce walks it
 constexpr int kWalkDone = (int)0x80000000;   // k_traverse: no node left (below every leaf code, first < 2^23)
 constexpr int kWalkNone = (int)0x80000001;   // k_traverse: stay (the leaf has triangles left)
 
@@ -1255,6 +1275,17 @@ constexpr int kMeshPre = 2;      // 2 closest mesh hit precomputed by k_traverse
 constexpr int kTravChunk = 256;  // rays per ticket grab
 constexpr int kRefillMin = 16;   // idle lanes that trigger a refill
 constexpr int kTravLdsRows = 32; // LDS stack entries per thread (HybStack; the rest in scratch)
+constexpr int kTrav4LdsRows = 16;   // k_traverse4: LDS stack entries per thread (5 workgroups per CU)
+#ifndef PT_FOLD_BATCH
+#define PT_FOLD_BATCH 4
+#endif
+constexpr int kFoldBatch = PT_FOLD_BATCH;   // k_traverse4: task results read per LDS round trip
+#ifndef PT_T4_LOADS
+#define PT_T4_LOADS 0    // k_traverse4 loads: 0 masked, quad first; 1 every lane; 2 masked, triangle after the box tests
+#endif
+#ifndef PT_T4_ASSIGN
+#define PT_T4_ASSIGN 0   // k_traverse4 leaf tasks: 0 owner tag + ballot + ds_bpermute; 1 task slots written by owners
+#endif
 
 // Exclusive prefix of the previous launch's segment survivor counts into s_pre[0..nseg]; returns
 // the total.  All threads of the block call it (barriers).
@@ -1460,6 +1491,357 @@ __global__ __launch_bounds__(kBlock) void k_traverse(const KArgs A) {
 #endif
 }
 
+// The four slab tests of a quad entry for a ray whose o and 1/d are finite (aabb_hit_finite's
+// arithmetic per slot: (b - o) * inv, then min/max); bit k set when slot k's box is hit.  The
+// subtractions and products run two slots per v_pk_add_f32 / v_pk_mul_f32 (the same correctly
+// rounded operations as the scalar forms).
+__device__ __forceinline__ uint32_t quad_hits(const v4f& lox, const v4f& hix, const v4f& loy, const v4f& hiy,
+                                              const v4f& loz, const v4f& hiz, f3 o, f3 inv) {
+    const v4f ox = {o.x, o.x, o.x, o.x}, oy = {o.y, o.y, o.y, o.y}, oz = {o.z, o.z, o.z, o.z};
+    const v4f ix = {inv.x, inv.x, inv.x, inv.x}, iy = {inv.y, inv.y, inv.y, inv.y}, iz = {inv.z, inv.z, inv.z, inv.z};
+    const v4f mx = (lox - ox) * ix, Mx = (hix - ox) * ix;
+    const v4f my = (loy - oy) * iy, My = (hiy - oy) * iy;
+    const v4f mz = (loz - oz) * iz, Mz = (hiz - oz) * iz;
+    uint32_t h = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const float lo = fmaxf(fmaxf(fminf(mx[k], Mx[k]), fminf(my[k], My[k])), fminf(mz[k], Mz[k]));
+        const float hi = fminf(fminf(fmaxf(mx[k], Mx[k]), fmaxf(my[k], My[k])), fmaxf(mz[k], Mz[k]));
+        h |= (!(hi < 0) && !(lo > hi)) ? (1u << k) : 0u;
+    }
+    return h;
+}
+
+// rocPRIM's wave-level LDS handoff: the stores of one lane are visible to the loads of another
+// lane of the same wave after this point.
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// k_traverse on the 4-wide layout (DQuad) with leaf work spread over the wave.
+//   Round 2's walk (k_traverse above) spent one memory round trip per pair AND per triangle, and
+// every trip ran both the box branch and the triangle branch for whichever lanes held a pair or a
+// leaf: 111 pair fetches + 112 triangle tests per config-5 ray.  Here, per trip of the wave:
+//   * lanes holding an interior node test the four boxes of its quad (128 B, loaded first thing
+//     in the trip), push the hit slots in the reference's near-first order (the far group first,
+//     within a group the far child first) and continue with the nearest hit;
+//   * the REMAINING triangles of every lane holding a leaf are dealt out as tasks, one per lane of
+//     the wave (up to 64 per trip, in lane order, by a wave prefix sum of the counts): each owner
+//     writes (its ray, the triangle index) into the task slots, each task lane loads its triangle
+//     and tests it, and the owner folds its tasks' results in triangle order with the reference's
+//     update rule (`r.t == -1 || t < r.t`: the first closest found).  A leaf costs one trip instead
+//     of one per triangle, and the triangle tests run with (nearly) every lane busy.  Tasks that do
+//     not fit this trip stay with their owner for the next.
+// Every lane issues both loads every trip (idle lanes reload a line already cached), so the wait
+// counts are static: the quad's loads first, then the triangle's, and the box tests wait for the
+// quad only.  The stack is LDS-only in trips where no lane can reach the LDS rows (wave-uniform
+// test), else HybStack's LDS/scratch split.
+// Per ray the boxes tested and their outcomes, the leaves reached, the triangles tested and their
+// order are BVHIntersectionTest's; only the scheduling across lanes differs.  Rays whose o or 1/d
+// is not finite (axis-parallel or NaN directions) get the record kRecWalkHere: the bounce kernel
+// walks them itself with the node-at-a-time walk (glm's ternary slab test, the reference's stack).
+#ifndef PT_T4_WAVES
+#define PT_T4_WAVES 1   // (A/B knob: minimum waves per SIMD of k_traverse4)
+#endif
+template <bool FIRST>
+__global__ __launch_bounds__(kBlock, PT_T4_WAVES) void k_traverse4(const KArgs A) {
+    extern __shared__ int s_tstack[];   // stack_rows entries per thread, column layout
+    __shared__ int32_t s_pre[FIRST ? 1 : kMaxSeg + 1];
+    __shared__ uint32_t s_wsum[4];
+    // leaf tasks, per task lane j: [2j] = (owner's o, triangle index), [2j + 1] = (owner's d, -),
+    // then overwritten by the task's result (t or NaN = no hit, bx, by, -)
+#if PT_T4_ASSIGN == 1
+    __shared__ v4f s_task[2 * kBlock];
+#else
+    __shared__ v4f s_task[kBlock];      // task results only (index 2j + 1 -> j below)
+#endif
+#if PT_T4_ASSIGN == 0
+    __shared__ int32_t s_own[kBlock];   // leaf tasks: tag << 6 | owner lane, at the owner's first task
+#endif
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const SceneDev& S = A.S;
+    int N, nseg = 0, chunk = 0;
+    if (FIRST) {
+        N = A.tile.P;
+    } else {
+        const int par = A.parity;
+        nseg = (int)A.ctl[par].nseg;
+        chunk = (int)A.ctl[par].chunk;
+        N = seg_prefix(reinterpret_cast<const uint32_t*>(A.seg) + (size_t)par * kMaxSeg, nseg, s_pre, s_wsum);
+    }
+    auto ray = [&](int k, f3& o, f3& d) -> int {   // as k_traverse
+        if (FIRST) {
+            PathReg p;
+            raygen(A.cam, A.fl, A.tile, k, p);
+            o = p.o;
+            d = p.d;
+            return k;
+        }
+        int lo = 0, hi = nseg - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (s_pre[mid] <= k) lo = mid; else hi = mid - 1;
+        }
+        const int q = lo * chunk + (k - s_pre[lo]);
+        const v4f a = PT_LD(A.in.a + q), b = PT_LD(A.in.b + q);
+        o = F3(a[0], a[1], a[2]);
+        d = F3(a[3], b[0], b[1]);
+        return q;
+    };
+#if PT_T4_ASSIGN == 1
+    v4f* task = s_task + wave * 128;
+#define PT_RES(j) task[2 * (j) + 1]
+#else
+    v4f* task = s_task + wave * 64;
+#define PT_RES(j) task[(j)]
+#endif
+#if PT_T4_ASSIGN == 0
+    int32_t* own = s_own + wave * 64;
+    own[lane] = 0;   // tags start at 1
+    uint32_t tag = 0;
+#endif
+    int* const col = s_tstack + tid;
+    const int rows = A.stack_rows;
+    int spill[64];
+    const HybStack hst{col, spill, rows};
+    uint32_t* ticket = A.tticket;
+    const int csz = min(A.tchunk, max(64, (N / (int)(gridDim.x * (kBlock / 64) * 2)) & ~63));
+    int cnext = 0, cend = 0;
+    bool exhausted = false, have = false, leaf = false;
+    int q = 0, cur = 0, top = 0, ti = 0, te = 0;
+    f3 o = F3(0, 0, 0), d = F3(0, 0, 0), inv = F3(0, 0, 0);
+    uint32_t negm = 0;
+    MeshHit r{false, -1, -1, kFLT_MAX, 0.f, 0.f};
+    auto enter = [&](int code) {
+        leaf = code < 0;
+        if (leaf) {
+            const int c = -code - 1;
+            ti = c >> 8;
+            te = ti + (c & 255);
+        } else {
+            cur = code;
+        }
+    };
+    auto record = [&]() { PT_ST((v4f{r.t, __int_as_float(r.any ? r.idx : -1), r.bx, r.by}), A.mhit + q); };
+    auto fold = [&](const v4f& x, int idx) {   // bvh_walk_pairs's per-triangle update
+        if (x[0] == x[0]) {
+            r.any = true;
+            if (r.t == -1.0f || x[0] < r.t) { r.t = x[0]; r.bx = x[1]; r.by = x[2]; r.idx = idx; }
+        }
+    };
+#ifdef PT_TRAV_STATS
+    uint32_t n_rays = 0, n_inner = 0, n_tris = 0, w_trips = 0, n_busy = 0, t_leaf = 0, t_inner = 0;
+#endif
+    for (;;) {
+        // ---- refill: idle lanes take the next rays of the wave's chunk ----
+        const uint64_t idle = __ballot(!have);
+        const int nidle = __popcll(idle);
+        if (nidle >= A.refill_min && !exhausted) {
+            if (cnext >= cend) {
+                int base = 0;
+                if (lane == 0) base = (int)atomicAdd(ticket, (uint32_t)csz);
+                base = __shfl(base, 0);
+                if (base >= N) exhausted = true;
+                else { cnext = base; cend = min(base + csz, N); }
+            }
+            if (!exhausted) {
+                const uint32_t rank =
+                    __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+                if (!have && cnext + (int)rank < cend) {
+                    q = ray(cnext + (int)rank, o, d);
+                    negm = (d.x < 0.0f ? 1u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 4u : 0u);
+                    inv = F3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+                    const bool finite = __builtin_isfinite(inv.x) && __builtin_isfinite(inv.y) &&
+                                        __builtin_isfinite(inv.z) && __builtin_isfinite(o.x) &&
+                                        __builtin_isfinite(o.y) && __builtin_isfinite(o.z);
+                    top = 0;
+                    r = MeshHit{false, -1, -1, kFLT_MAX, 0.f, 0.f};
+                    const float bmin[3] = {S.root_lo[0], S.root_lo[1], S.root_lo[2]};
+                    const float bmax[3] = {S.root_hi[0], S.root_hi[1], S.root_hi[2]};
+                    if (!finite) {   // left to the bounce kernel's node walk (glm's ternary slab test)
+                        PT_ST((v4f{0.f, __int_as_float(kRecWalkHere), 0.f, 0.f}), A.mhit + q);
+                    } else if (aabb_hit(bmin, bmax, o, inv)) {
+                        enter(S.root_qcode);
+                        have = true;
+                    } else {
+                        record();
+                    }
+#ifdef PT_TRAV_STATS
+                    ++n_rays;
+#endif
+                }
+                cnext = min(cnext + nidle, cend);
+            }
+        }
+        const uint64_t busy = __ballot(have);
+        if (busy == 0) {
+            if (exhausted) break;
+            continue;
+        }
+#ifdef PT_TRAV_STATS
+        if (lane == 0) { ++w_trips; n_busy += (uint32_t)__popcll(busy); }
+#endif
+        // ---- the quad of every interior lane ----
+        const bool inner = have && !leaf;
+        v4f x0, x1, x2, x3, x4, x5, x6;
+        uint32_t meta;
+#if PT_T4_LOADS == 1   // every lane loads (idle and leaf lanes: their last quad, cached): static wait counts
+        {
+#else
+        if (inner) {
+#endif
+            const v4f* qsrc = reinterpret_cast<const v4f*>(S.quads + cur);
+            x0 = qsrc[0]; x1 = qsrc[1]; x2 = qsrc[2]; x3 = qsrc[3]; x4 = qsrc[4]; x5 = qsrc[5]; x6 = qsrc[6];
+            meta = reinterpret_cast<const uint32_t*>(qsrc)[28];
+        }
+        // ---- leaf tasks: the remaining triangles of the leaf lanes, one per lane of the wave ----
+        const int cnt = (have && leaf) ? te - ti : 0;
+        const int incl = (int)lb::wave_inclusive_scan((uint32_t)cnt);
+        const int pre = incl - cnt;
+        const int T = __builtin_amdgcn_readlane(incl, 63);
+        const int cov = (cnt > 0 && pre < 64) ? min(cnt, 64 - pre) : 0;   // this trip's tasks of this lane
+        const bool is_task = lane < T;
+        f3 to = F3(0, 0, 0), td = F3(0, 0, 0);
+        int tidx = 0;
+        if (T > 0) {   // (wave-uniform)
+#if PT_T4_ASSIGN == 1   // owners write (ray, triangle index) into each of their task slots
+            for (int k = 0; k < cov; ++k) {
+                task[2 * (pre + k)] = v4f{o.x, o.y, o.z, __int_as_float(ti + k)};
+                task[2 * (pre + k) + 1] = v4f{d.x, d.y, d.z, 0.f};
+            }
+            wave_sync();
+            if (is_task) {
+                const v4f a = task[2 * lane], b = task[2 * lane + 1];
+                to = F3(a[0], a[1], a[2]);
+                tidx = __float_as_int(a[3]);
+                td = F3(b[0], b[1], b[2]);
+            }
+#else   // owners mark their first task slot (tag | lane); task lanes find it by ballot, fetch by ds_bpermute
+            if (tag == (1u << 25)) {   // (never in practice: ~10^5 trips per launch) restart the tags
+                own[lane] = 0;
+                tag = 0;
+                wave_sync();
+            }
+            ++tag;
+            if (cov > 0) own[pre] = (int32_t)((tag << 6) | (uint32_t)lane);
+            wave_sync();
+            const int v = own[lane];
+            const uint64_t heads = __ballot(is_task && ((uint32_t)v >> 6) == tag);
+            const uint64_t le = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+            const int pos = is_task ? 63 - (int)__clzll(heads & le) : lane;   // the owner's first task
+            const int ow = __shfl(v, pos) & 63;
+            tidx = __shfl(ti, ow) + (lane - pos);
+            to = F3(__shfl(o.x, ow), __shfl(o.y, ow), __shfl(o.z, ow));
+            td = F3(__shfl(d.x, ow), __shfl(d.y, ow), __shfl(d.z, ow));
+#endif
+#ifdef PT_TRAV_STATS
+            if (lane == 0) { ++t_leaf; n_tris += (uint32_t)min(T, 64); }
+#endif
+        }
+        v4f t0, t1, t2;
+        auto load_tri = [&]() {
+            const v4f* tsrc = reinterpret_cast<const v4f*>(S.tris + tidx);   // (non-task lanes: triangle 0)
+            t0 = tsrc[0]; t1 = tsrc[1]; t2 = tsrc[2];
+        };
+#if PT_T4_LOADS == 1
+        load_tri();
+#elif PT_T4_LOADS == 0
+        if (is_task) load_tri();
+#endif
+#ifdef PT_TRAV_STATS
+        {
+            const uint64_t ib = __ballot(inner);
+            if (lane == 0 && ib) { ++t_inner; n_inner += (uint32_t)__popcll(ib); }
+        }
+#endif
+        // the stack this trip: LDS only unless some lane could reach the LDS rows (3 pushes at most)
+        const bool fast = __ballot(top + 4 > rows) == 0;
+        auto push = [&](int v) {
+            if (fast) col[top * kBlock] = v;
+            else hst.set(top, v);
+            ++top;
+        };
+        auto pop = [&]() -> int {
+            if (top == 0) return kWalkDone;
+            --top;
+            return fast ? col[top * kBlock] : hst.get(top);
+        };
+        // ---- interior step ----
+        int next = kWalkNone;
+        if (inner) {
+            uint32_t hm = quad_hits(x0, x1, x2, x3, x4, x5, o, inv) & meta & 15u;
+            int c0 = __float_as_int(x6[0]), c1 = __float_as_int(x6[1]);
+            int c2 = __float_as_int(x6[2]), c3 = __float_as_int(x6[3]);
+            // near-first order: within each group by its axis, then the groups by N's axis
+            if ((negm >> ((meta >> 6) & 3u)) & 1u) {
+                const int t = c0; c0 = c1; c1 = t;
+                hm = (hm & 12u) | ((hm & 1u) << 1) | ((hm >> 1) & 1u);
+            }
+            if ((negm >> ((meta >> 8) & 3u)) & 1u) {
+                const int t = c2; c2 = c3; c3 = t;
+                hm = (hm & 3u) | ((hm & 4u) << 1) | ((hm >> 1) & 4u);
+            }
+            if ((negm >> ((meta >> 4) & 3u)) & 1u) {
+                int t = c0; c0 = c2; c2 = t;
+                t = c1; c1 = c3; c3 = t;
+                hm = ((hm & 3u) << 2) | (hm >> 2);
+            }
+            // push the later hits (farthest first), continue with the first
+            int nx = 0;
+            bool got = false;
+            if (hm & 8u) { nx = c3; got = true; }
+            if (hm & 4u) { if (got) push(nx); nx = c2; got = true; }
+            if (hm & 2u) { if (got) push(nx); nx = c1; got = true; }
+            if (hm & 1u) { if (got) push(nx); nx = c0; got = true; }
+            next = got ? nx : pop();
+        }
+        // ---- triangle tests ----
+        if (is_task) {
+#if PT_T4_LOADS == 2   // (the triangle's loads after the box tests)
+            load_tri();
+#endif
+            float bx = 0.f, by = 0.f, bz = 0.f;
+            const bool h = ray_tri(DTri{t0, t1, t2}, to, td, bx, by, bz);
+            PT_RES(lane) = v4f{h ? bz : __builtin_nanf(""), bx, by, 0.f};
+        }
+        if (T > 0) {
+            wave_sync();   // the task results
+            if (cov > 0) {   // the leaf's triangles in order (bvh_walk_pairs's loop)
+                for (int k0 = 0; k0 < cov; k0 += kFoldBatch) {   // reads of a batch issued together
+                    v4f x[kFoldBatch];
+#pragma unroll
+                    for (int k = 0; k < kFoldBatch; ++k)
+                        if (k0 + k < cov) x[k] = PT_RES(pre + k0 + k);
+#pragma unroll
+                    for (int k = 0; k < kFoldBatch; ++k)
+                        if (k0 + k < cov) fold(x[k], ti + k0 + k);
+                }
+                ti += cov;
+                if (ti == te) next = pop();
+            }
+        }
+        if (next == kWalkDone) {
+            record();
+            have = false;
+        } else if (next != kWalkNone) {
+            enter(next);
+        }
+    }
+#ifdef PT_TRAV_STATS
+    unsigned long long* g = g_trav + (blockIdx.x & 63) * 8;
+    atomicAdd(&g[0], (unsigned long long)n_rays);
+    atomicAdd(&g[1], (unsigned long long)n_inner);
+    atomicAdd(&g[2], (unsigned long long)n_tris);
+    atomicAdd(&g[3], (unsigned long long)w_trips);
+    atomicAdd(&g[4], lane == 0 ? 1ull : 0ull);
+    atomicAdd(&g[5], (unsigned long long)n_busy);
+    atomicAdd(&g[6], (unsigned long long)t_leaf);
+    atomicAdd(&g[7], (unsigned long long)t_inner);
+#endif
+}
+
 // [raygen] -> intersect -> shade -> segmented compaction (above).
 #ifndef PT_LATER_WAVES
 #define PT_LATER_WAVES 1   // (A/B knob: minimum waves per SIMD of the later-bounce kernels)
@@ -1564,8 +1946,24 @@ __global__ __launch_bounds__(kBlock, FIRST || MESH ? 1 : PT_LATER_WAVES) void k_
                 mh.idx = __float_as_int(m[1]);
                 mh.bx = m[2];
                 mh.by = m[3];
+                if (mh.idx == kRecWalkHere) {   // a non-finite ray k_traverse4 left to this kernel
+                    int wstack[64];
+                    const MeshHit w = bvh_walk(A.S, p.o, p.d, false, PrivStack{wstack});
+                    mh.t = w.t;
+                    mh.idx = w.any ? w.idx : -1;
+                    mh.bx = w.bx;
+                    mh.by = w.by;
+                }
                 mh.any = mh.idx >= 0;
                 mh.id = mh.any ? __float_as_int(A.S.tris[mh.idx].a[3]) : -1;
+                if (A.fl.verify) {   // PT_AMD_VERIFY_BOUNDS=1: the record == the reference's node walk
+                    int vstack[64];
+                    const MeshHit w = bvh_walk(A.S, p.o, p.d, A.fl.bvh_cull != 0, PrivStack{vstack});
+                    const int widx = w.any ? w.idx : -1;
+                    if (widx != mh.idx || __float_as_uint(w.t) != __float_as_uint(mh.t) ||
+                        __float_as_uint(w.bx) != __float_as_uint(mh.bx) || __float_as_uint(w.by) != __float_as_uint(mh.by))
+                        atomicAdd(&A.stats->bound_mismatch, 1u);
+                }
                 h = intersect_bounded<!FIRST, true>(A.S, A.fl, s_geoms, p.o, p.d, &mh);
             } else {
                 uint32_t gm = ~0u;
@@ -2177,6 +2575,9 @@ struct pt_ctx {
     bool mesh_inline = false;            // PT_AMD_MESH_INLINE=1 at pt_create: always kMeshInline
     uint32_t* tq = nullptr;              // k_traverse ray tickets: [lane][bounce], zeroed per pass
     int grid_traverse = 0;               // k_traverse: one resident wave of workgroups
+    int grid_traverse4 = 0;              // k_traverse4 (4-wide layout): the same for its footprint
+    int quad_occ = 0;                    // k_traverse4: bound on its stack occupancy (build_quads)
+    bool trav_quads = false;             // mesh mode 2 walks the 4-wide layout (PT_AMD_TRAV=pairs: off)
     hipStream_t fin_stream = nullptr;
     hipEvent_t ev_pass[2] = {}, ev_fin[2] = {};
     bool fin_out[2] = {false, false};
@@ -2612,22 +3013,160 @@ int launch_k(pt_ctx* c, K kernel, int grid, hipStream_t st, int kind, const KArg
     return prof_end(ev, st);
 }
 
-// One bounce of the fused pipeline: [k_traverse (mesh mode 2)] + k_bounce, profiled as one launch.
+// One bounce of the fused pipeline: [k_traverse (mesh mode 2)] + k_bounce.  Profiled as two kinds:
+// the walk (PT_KIND_TRAVERSE / PT_KIND_FIRST_TRAVERSE) and the bounce kernel (PT_KIND_BOUNCE /
+// PT_KIND_FIRST_BOUNCE), each bracketed by its own events on the launch stream.
 // `cap`: path capacity of the lane's buffers (k_traverse's later-bounce grid covers every slot).
 int launch_bounce(pt_ctx* c, bool first, bool spp1, int mesh, hipStream_t st, const KArgs& a, size_t cap) {
     ProfEv* ev;
-    if (int rc = prof_begin(c, st, first ? PT_KIND_FIRST_BOUNCE : PT_KIND_BOUNCE, &ev)) return rc;
     (void)cap;
     if (mesh == kMeshPre) {
+        if (int rc = prof_begin(c, st, first ? PT_KIND_FIRST_TRAVERSE : PT_KIND_TRAVERSE, &ev)) return rc;
         const size_t lds = (size_t)a.stack_rows * kBlock * sizeof(int);
-        if (first) hipLaunchKernelGGL(k_traverse<true>, dim3(c->grid_traverse), dim3(kBlock), lds, st, a);
+        const bool quad = c->trav_quads && !a.fl.bvh_cull;
+        if (quad && first) hipLaunchKernelGGL(k_traverse4<true>, dim3(c->grid_traverse4), dim3(kBlock), lds, st, a);
+        else if (quad) hipLaunchKernelGGL(k_traverse4<false>, dim3(c->grid_traverse4), dim3(kBlock), lds, st, a);
+        else if (first) hipLaunchKernelGGL(k_traverse<true>, dim3(c->grid_traverse), dim3(kBlock), lds, st, a);
         else hipLaunchKernelGGL(k_traverse<false>, dim3(c->grid_traverse), dim3(kBlock), lds, st, a);
         HIP_TRY(hipGetLastError());
+        if (int rc = prof_end(ev, st)) return rc;
     }
+    if (int rc = prof_begin(c, st, first ? PT_KIND_FIRST_BOUNCE : PT_KIND_BOUNCE, &ev)) return rc;
     hipLaunchKernelGGL(bounce_kernel(first, spp1, mesh), dim3(c->grid_bounce[first]), dim3(kBlock),
                        bounce_lds_bytes(a.S, mesh), st, a);
     HIP_TRY(hipGetLastError());
     return prof_end(ev, st);
+}
+
+// The 4-wide layout (DQuad) of the flattened tree `nodes` (DNode encoding: left child = i + 1).
+// An interior child X of a quad's node is replaced by its two children when both boxes lie inside
+// X's box as floats (the nesting k_traverse4's exactness rests on); otherwise it keeps one slot.
+// Also bounds the walk's stack: per quad (valid slots - 1) pushes, summed along the worst path.
+// Leaves of zero triangles (never built by the SAH builder) or a bound beyond the stack's capacity
+// leave the quad layout off (k_traverse's pair walk runs instead).
+// The flattened reference tree (BVH_tree.h:54-61) in the device encoding (DNode).
+std::vector<DNode> to_dnodes(const std::vector<pt_bvh_node>& bvh) {
+    std::vector<DNode> nodes(bvh.size());
+    for (size_t i = 0; i < bvh.size(); ++i) {
+        const pt_bvh_node& b = bvh[i];
+        const int32_t meta = b.sub_areas > 0 ? b.sub_areas : -(b.axis + 1);
+        const int32_t link = b.sub_areas > 0 ? b.first_area_idx : b.rchild_idx;
+        for (int k = 0; k < 3; ++k) { nodes[i].lo[k] = b.bmin[k]; nodes[i].hi[k] = b.bmax[k]; }
+        nodes[i].lo[3] = bits_to_float(meta);
+        nodes[i].hi[3] = bits_to_float(link);
+    }
+    return nodes;
+}
+
+// Host part: fills `quads`, the root's code and the stack bound; false = no quad layout.
+bool make_quads(const std::vector<DNode>& nodes, std::vector<DQuad>& quads, int32_t& root_code, int32_t& root_occ) {
+    const size_t n = nodes.size();
+    quads.clear();
+    if (n == 0) return false;
+    auto meta = [&](size_t i) { return __float_as_int_host(nodes[i].lo[3]); };
+    auto link = [&](size_t i) { return __float_as_int_host(nodes[i].hi[3]); };
+    for (size_t i = 0; i < n; ++i)
+        if (meta(i) == 0 || (meta(i) < 0 && (link(i) <= (int32_t)i + 1 || (size_t)link(i) >= n)))
+            return false;   // (a zero-triangle leaf is indistinguishable here; malformed links)
+    auto inside = [&](size_t in, size_t out) {
+        for (int k = 0; k < 3; ++k)
+            if (!(nodes[in].lo[k] >= nodes[out].lo[k] && nodes[in].hi[k] <= nodes[out].hi[k])) return false;
+        return true;
+    };
+    std::vector<int32_t> occ;   // stack bound of the walk below each quad
+    std::vector<int32_t> qid(n, -1);
+    auto leaf_code = [&](size_t i) { return -(link(i) * 256 + meta(i)) - 1; };
+    // first pass: assign quad ids in DFS order
+    std::vector<size_t> order;
+    {
+        std::vector<size_t> stk{0};
+        if (meta(0) > 0) stk.clear();
+        while (!stk.empty()) {
+            const size_t i = stk.back();
+            stk.pop_back();
+            qid[i] = (int32_t)order.size();
+            order.push_back(i);
+            const size_t ch[2] = {i + 1, (size_t)link(i)};
+            std::vector<size_t> kids;
+            for (size_t x : ch) {
+                if (meta(x) > 0) continue;
+                const size_t g[2] = {x + 1, (size_t)link(x)};
+                if (inside(g[0], x) && inside(g[1], x)) {
+                    for (size_t y : g)
+                        if (meta(y) <= 0) kids.push_back(y);
+                } else {
+                    kids.push_back(x);
+                }
+            }
+            for (auto it = kids.rbegin(); it != kids.rend(); ++it) stk.push_back(*it);
+        }
+    }
+    quads.resize(std::max<size_t>(order.size(), 1));
+    occ.assign(order.size(), 0);
+    for (size_t qi = 0; qi < order.size(); ++qi) {
+        const size_t i = order[qi];
+        DQuad& Q = quads[qi];
+        std::memset(&Q, 0, sizeof Q);
+        uint32_t valid = 0, axes[2] = {3u, 3u};
+        int32_t codes[4] = {0, 0, 0, 0};
+        size_t box[4] = {0, 0, 0, 0};
+        const size_t ch[2] = {i + 1, (size_t)link(i)};
+        for (int g = 0; g < 2; ++g) {
+            const size_t x = ch[g];
+            auto slot = [&](int s, size_t y) {
+                valid |= 1u << s;
+                box[s] = y;
+                codes[s] = meta(y) > 0 ? leaf_code(y) : qid[y];
+            };
+            if (meta(x) <= 0 && inside(x + 1, x) && inside((size_t)link(x), x)) {
+                slot(2 * g, x + 1);
+                slot(2 * g + 1, (size_t)link(x));
+                axes[g] = (uint32_t)(-meta(x) - 1);
+            } else {
+                slot(2 * g, x);
+            }
+        }
+        for (int s = 0; s < 4; ++s) {
+            const DNode& b = nodes[box[s]];
+            Q.lox[s] = b.lo[0]; Q.hix[s] = b.hi[0];
+            Q.loy[s] = b.lo[1]; Q.hiy[s] = b.hi[1];
+            Q.loz[s] = b.lo[2]; Q.hiz[s] = b.hi[2];
+            Q.code[s] = bits_to_float(codes[s]);
+        }
+        const uint32_t m = valid | ((uint32_t)(-meta(i) - 1) << 4) | (axes[0] << 6) | (axes[1] << 8);
+        Q.meta[0] = bits_to_float((int32_t)m);
+    }
+    // stack bound: children quads come later in DFS order, so a reverse sweep sees them first
+    root_occ = 0;
+    for (size_t qi = order.size(); qi-- > 0;) {
+        const DQuad& Q = quads[qi];
+        const uint32_t m = (uint32_t)__float_as_int_host(Q.meta[0]);
+        int32_t deepest = 0, nv = 0;
+        for (int s = 0; s < 4; ++s) {
+            if (!((m >> s) & 1u)) continue;
+            ++nv;
+            const int32_t cd = __float_as_int_host(Q.code[s]);
+            if (cd >= 0) deepest = std::max(deepest, occ[(size_t)cd]);
+        }
+        occ[qi] = nv - 1 + deepest;
+        root_occ = occ[qi];
+    }
+    if (order.empty()) root_occ = 0;
+    root_code = meta(0) > 0 ? leaf_code(0) : 0;
+    return root_occ <= 64;   // HybStack holds rows + 64 >= 64 entries
+}
+
+int build_quads(pt_ctx* c, const std::vector<DNode>& nodes) {
+    std::vector<DQuad> quads;
+    int32_t root_code = 0, occ = 0;
+    if (!make_quads(nodes, quads, root_code, occ)) return PT_OK;
+    DQuad* d_quads;
+    if (int rc = c->alloc(&d_quads, quads.size())) return rc;
+    HIP_TRY(hipMemcpy(d_quads, quads.data(), quads.size() * sizeof(DQuad), hipMemcpyHostToDevice));
+    c->args.S.quads = d_quads;
+    c->args.S.root_qcode = root_code;
+    c->quad_occ = occ;
+    return PT_OK;
 }
 
 // SceneDev::bgeoms: the geom table stably ordered by bkind, each row keeping its index in `orig`.
@@ -2794,15 +3333,7 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
         A.S.ntris = (int)tr.size();
     }
     if (!S.bvh.empty()) {
-        std::vector<DNode> nodes(S.bvh.size());
-        for (size_t i = 0; i < S.bvh.size(); ++i) {
-            const pt_bvh_node& b = S.bvh[i];
-            const int32_t meta = b.sub_areas > 0 ? b.sub_areas : -(b.axis + 1);
-            const int32_t link = b.sub_areas > 0 ? b.first_area_idx : b.rchild_idx;
-            for (int k = 0; k < 3; ++k) { nodes[i].lo[k] = b.bmin[k]; nodes[i].hi[k] = b.bmax[k]; }
-            nodes[i].lo[3] = bits_to_float(meta);
-            nodes[i].hi[3] = bits_to_float(link);
-        }
+        const std::vector<DNode> nodes = to_dnodes(S.bvh);
         DNode* d_nodes;
         if (int rc = c->alloc(&d_nodes, nodes.size())) return bail(rc);
         if ((e = hipMemcpy(d_nodes, nodes.data(), nodes.size() * sizeof(DNode), hipMemcpyHostToDevice)) != hipSuccess)
@@ -2853,6 +3384,7 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
             A.S.pairs = d_pairs;
             A.S.root_code = code(0);
             for (int k = 0; k < 4; ++k) { A.S.root_lo[k] = nodes[0].lo[k]; A.S.root_hi[k] = nodes[0].hi[k]; }
+            if (int rc = build_quads(c, nodes)) return bail(rc);
         }
     }
     if (!S.textures.empty()) {
@@ -2928,14 +3460,22 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
     if (A.S.nnodes > 0) {   // k_traverse records (mesh mode 2), tickets, stack depth and grid
         if (int rc = c->alloc(&c->mhit[0], c->path_cap)) return bail(rc);
         if (int rc = c->alloc(&c->tq, (size_t)kMaxLanes * 64)) return bail(rc);
-        A.stack_rows = std::min(A.S.bvh_depth + 2, kTravLdsRows);
+        const char* tv = std::getenv("PT_AMD_TRAV");
+        c->trav_quads = A.S.quads != nullptr && !(tv && std::strcmp(tv, "pairs") == 0);
+        A.stack_rows = c->trav_quads ? std::max(1, std::min(c->quad_occ, kTrav4LdsRows))
+                                     : std::min(A.S.bvh_depth + 2, kTravLdsRows);
         if (const char* sr = std::getenv("PT_AMD_STACK_ROWS")) A.stack_rows = std::max(1, std::min(64, std::atoi(sr)));
+        const size_t slds = (size_t)A.stack_rows * kBlock * sizeof(int);
         int per_cu = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_traverse<false>, kBlock,
-                                                         (size_t)A.stack_rows * kBlock * sizeof(int)) != hipSuccess ||
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_traverse<false>, kBlock, slds) != hipSuccess ||
             per_cu <= 0)
             per_cu = 4;
         c->grid_traverse = cus * per_cu;
+        per_cu = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_traverse4<false>, kBlock, slds) != hipSuccess ||
+            per_cu <= 0)
+            per_cu = 4;
+        c->grid_traverse4 = cus * per_cu;
         A.refill_min = kRefillMin;
         A.tchunk = kTravChunk;
         if (const char* tc = std::getenv("PT_AMD_TCHUNK")) A.tchunk = std::max(64, std::min(4096, std::atoi(tc)));
@@ -3072,7 +3612,6 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
     auto sort_bounce = [&](KArgs& a, pt_ctx::SortSet& ss, hipStream_t s, int b, int& lcur, uint64_t& lc,
                            const PathSoA* bufs) -> int {
         ProfEv* ev;
-        if (int rc = prof_begin(c, s, PT_KIND_SORT, &ev)) return rc;
         auto produce = [&](bool first) -> int {
             a.parity = (int)(lc & 1);
             a.in = bufs[lcur];
@@ -3086,8 +3625,12 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
             lcur ^= 1;
             return PT_OK;
         };
-        if (b == 0)
+        if (b == 0) {   // raygen + intersection of the camera rays: profiled as the first bounce
+            if (int rc = prof_begin(c, s, PT_KIND_FIRST_BOUNCE, &ev)) return rc;
             if (int rc = produce(true)) return rc;
+            if (int rc = prof_end(ev, s)) return rc;
+        }
+        if (int rc = prof_begin(c, s, PT_KIND_SORT, &ev)) return rc;
         a.parity = (int)(lc & 1);
         const uint32_t* nlive = &a.ctl[a.parity].hist_live;
         const int tiles = (int)((ss.hist_cap + kHistTile - 1) / kHistTile);
@@ -3317,16 +3860,17 @@ int pt_debug_stamps(unsigned long long* out8, int32_t reset) {
 #endif
 
 #ifdef PT_TRAV_STATS
-// Diagnostic build only (scripts/trav_stats.py): k_traverse's counters summed over their slots:
-// out[0] rays, [1] pair fetches, [2] triangle tests, [3] sum over waves of the longest lane's
-// steps (pairs + triangles), [4] waves.
-int pt_debug_trav(unsigned long long* out5, int32_t reset) {
+// Diagnostic build only (scripts/trav_stats.py): k_traverse[4]'s counters summed over their slots:
+// out[0] rays, [1] interior fetches (pairs, or quads), [2] triangle tests, [3] wave trips (loop
+// iterations with a busy lane), [4] waves; k_traverse4 only: [5] busy lane-trips, [6] trips with
+// leaf tasks, [7] trips with an interior lane.
+int pt_debug_trav(unsigned long long* out8, int32_t reset) {
     HIP_TRY(hipDeviceSynchronize());
     static unsigned long long h[64 * 8];
     HIP_TRY(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_trav), sizeof h));
-    for (int k = 0; k < 5; ++k) {
-        out5[k] = 0;
-        for (int q = 0; q < 64; ++q) out5[k] += h[q * 8 + k];
+    for (int k = 0; k < 8; ++k) {
+        out8[k] = 0;
+        for (int q = 0; q < 64; ++q) out8[k] += h[q * 8 + k];
     }
     if (reset) {
         std::memset(h, 0, sizeof h);
@@ -3335,6 +3879,18 @@ int pt_debug_trav(unsigned long long* out5, int32_t reset) {
     return PT_OK;
 }
 #endif
+
+int pt_scene_bvh_quads(const pt_scene* scene, void* out, int32_t cap, int32_t* root_code, int32_t* stack_bound) {
+    if (!scene) return -PT_ERR_ARG;
+    const auto& S = *reinterpret_cast<const pt::Scene*>(scene);
+    std::vector<DQuad> quads;
+    int32_t rc = 0, occ = 0;
+    if (!make_quads(to_dnodes(S.bvh), quads, rc, occ)) return 0;
+    if (root_code) *root_code = rc;
+    if (stack_bound) *stack_bound = occ;
+    if (out && cap > 0) std::memcpy(out, quads.data(), std::min<size_t>((size_t)cap, quads.size()) * sizeof(DQuad));
+    return (int)quads.size();
+}
 
 int pt_selftest_math(uint64_t n, uint32_t seed, uint64_t* mismatches) {
     if (!mismatches) return pt::fail(PT_ERR_ARG, "null argument");
@@ -3359,35 +3915,45 @@ int pt_profile_enable(pt_ctx* c, int32_t on) {
     return PT_OK;
 }
 
-int pt_profile_read_busy(pt_ctx* c, double ms[4], double busy_ms[4], uint64_t launches[4]) {
-    if (!c || !ms || !launches) return pt::fail(PT_ERR_ARG, "null argument");
-    std::vector<std::pair<double, double>> iv[4];   // per kind: [start, end) after the first event
-    for (int k = 0; k < 4; ++k) { ms[k] = 0.0; launches[k] = 0; if (busy_ms) busy_ms[k] = 0.0; }
+int pt_profile_read_kinds(pt_ctx* c, int32_t nkinds, double* ms, double* busy_ms, uint64_t* launches) {
+    if (!c || !ms || !launches || nkinds < 0) return pt::fail(PT_ERR_ARG, "bad argument");
+    std::vector<std::pair<double, double>> iv[PT_KIND_COUNT];   // per kind: [start, end) after the first event
+    double m[PT_KIND_COUNT] = {}, busy[PT_KIND_COUNT] = {};
+    uint64_t n[PT_KIND_COUNT] = {};
     for (size_t i = 0; i < c->ev_used; ++i) {
         ProfEv& ev = c->events[i];
         HIP_TRY(hipEventSynchronize(ev.b));
         float t = 0.f, t0 = 0.f;
         HIP_TRY(hipEventElapsedTime(&t, ev.a, ev.b));
         HIP_TRY(hipEventElapsedTime(&t0, c->events[0].a, ev.a));
-        ms[ev.kind] += t;
-        launches[ev.kind] += 1;
+        m[ev.kind] += t;
+        n[ev.kind] += 1;
         iv[ev.kind].push_back({(double)t0, (double)t0 + (double)t});
     }
-    if (busy_ms)   // union of each kind's launch intervals: lanes run kernels of one kind concurrently
-        for (int k = 0; k < 4; ++k) {
-            std::sort(iv[k].begin(), iv[k].end());
-            double end = -1e300;
-            for (const auto& x : iv[k]) {
-                if (x.first > end) { busy_ms[k] += x.second - x.first; end = x.second; }
-                else if (x.second > end) { busy_ms[k] += x.second - end; end = x.second; }
-            }
+    // union of each kind's launch intervals: lanes run kernels of one kind concurrently
+    for (int k = 0; k < PT_KIND_COUNT; ++k) {
+        std::sort(iv[k].begin(), iv[k].end());
+        double end = -1e300;
+        for (const auto& x : iv[k]) {
+            if (x.first > end) { busy[k] += x.second - x.first; end = x.second; }
+            else if (x.second > end) { busy[k] += x.second - end; end = x.second; }
         }
+    }
+    for (int k = 0; k < nkinds; ++k) {
+        ms[k] = k < PT_KIND_COUNT ? m[k] : 0.0;
+        launches[k] = k < PT_KIND_COUNT ? n[k] : 0;
+        if (busy_ms) busy_ms[k] = k < PT_KIND_COUNT ? busy[k] : 0.0;
+    }
     c->ev_used = 0;
     return PT_OK;
 }
 
+int pt_profile_read_busy(pt_ctx* c, double ms[4], double busy_ms[4], uint64_t launches[4]) {
+    return pt_profile_read_kinds(c, 4, ms, busy_ms, launches);
+}
+
 int pt_profile_read(pt_ctx* c, double ms[4], uint64_t launches[4]) {
-    return pt_profile_read_busy(c, ms, nullptr, launches);
+    return pt_profile_read_kinds(c, 4, ms, nullptr, launches);
 }
 
 }  // extern "C"

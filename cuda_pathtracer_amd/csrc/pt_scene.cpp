@@ -236,8 +236,20 @@ int scene_add_geom(Scene& S, int32_t type, int32_t mat, const float* t, const fl
     return (int)S.geoms.size() - 1;
 }
 
-// Scene::loadFromJSON (scene.cpp:33-219)
-static int load_json(Scene& S, const std::string& path) {
+// Does the file opt in to the refraction extension?  Top-level "Extensions": {"REFRACTION": true}
+// (or a list holding "REFRACTION"); the reference loader ignores unknown top-level keys.
+static bool file_wants_refraction(const jl::Value& root) {
+    if (!root.has("Extensions")) return false;
+    const jl::Value& e = root["Extensions"];
+    if (e.kind == jl::Value::Object) return e.has("REFRACTION") && e["REFRACTION"].kind == jl::Value::Bool && e["REFRACTION"].b;
+    if (e.kind == jl::Value::Array)
+        for (const auto& x : e.arr)
+            if (x.kind == jl::Value::String && x.str == "REFRACTION") return true;
+    return false;
+}
+
+// Scene::loadFromJSON (scene.cpp:33-219).  `options`: PT_LOAD_* bits (pt_amd.h).
+static int load_json(Scene& S, const std::string& path, uint32_t options) {
     bool ok = false;
     const std::string text = read_file(path, &ok);
     if (!ok) return fail(PT_ERR_IO, "cannot read scene file " + path);
@@ -249,6 +261,10 @@ static int load_json(Scene& S, const std::string& path) {
     }
     try {
         const std::string dir = parent_dir(path);
+        // The reference reads neither REFRACTIVE nor IOR (scene.cpp:46-56: hasRefractive and
+        // indexOfRefraction stay 0), so by default neither do we; the
+        // extension is on only when the caller asks (PT_LOAD_REFRACTION) or the file opts in.
+        const bool refraction = (options & PT_LOAD_REFRACTION) != 0 || file_wants_refraction(root);
         // Materials: std::map iteration order == sorted names (scene.cpp:42-74).
         std::map<std::string, int> name_to_id;
         const jl::Value& mats = root["Materials"];
@@ -264,10 +280,10 @@ static int load_json(Scene& S, const std::string& path) {
             m.has_reflective = p.has("REFLECTIVE") ? (float)p["REFLECTIVE"].number() : 0.0f;
             m.emittance = p.has("EMITTANCE") ? (float)p["EMITTANCE"].number() : 0.0f;
             for (int i = 0; i < 3; ++i) { m.color[i] = rgb[i]; m.spec_color[i] = spec[i]; }
-            // Build extension (north-star config 4, off by default in the reference loader, which
-            // never reads these keys): REFRACTIVE / IOR.  Absent keys keep the reference's zeros.
-            if (p.has("REFRACTIVE")) m.has_refractive = (float)p["REFRACTIVE"].number();
-            if (p.has("IOR")) m.ior = (float)p["IOR"].number();
+            // Extension (north-star config 4; off by default, see above): REFRACTIVE / IOR.  Absent
+            // keys keep the reference's zeros.
+            if (refraction && p.has("REFRACTIVE")) m.has_refractive = (float)p["REFRACTIVE"].number();
+            if (refraction && p.has("IOR")) m.ior = (float)p["IOR"].number();
             m.texture_id = -1;
             name_to_id[kv.first] = (int)S.materials.size();
             if (p.has("TEXTURE_FILE") && !p["TEXTURE_FILE"].string().empty()) {
@@ -369,10 +385,13 @@ int pt_scene_create(pt_scene** out) {
 
 void pt_scene_free(pt_scene* s) { delete reinterpret_cast<pt::Scene*>(s); }
 
-int pt_scene_load_json(const char* path, pt_scene** out) {
+int pt_scene_load_json(const char* path, pt_scene** out) { return pt_scene_load_json_ex(path, 0u, out); }
+
+int pt_scene_load_json_ex(const char* path, uint32_t options, pt_scene** out) {
     if (!path || !out) return fail(PT_ERR_ARG, "null argument");
+    if (options & ~(uint32_t)PT_LOAD_REFRACTION) return fail(PT_ERR_ARG, "unknown PT_LOAD_* option");
     auto* S = new pt::Scene();
-    int rc = pt::load_json(*S, path);
+    int rc = pt::load_json(*S, path, options);
     if (!rc) rc = pt::scene_finalize(*S);
     if (rc) { delete S; return rc; }
     *out = reinterpret_cast<pt_scene*>(S);

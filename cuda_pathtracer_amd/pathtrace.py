@@ -89,15 +89,46 @@ def decode_jpeg(data: bytes) -> np.ndarray:
 
 class Scene:
     """Scene description; `Scene(path)` loads a reference JSON scene file (textures decoded
-    natively, pt_decode_jpeg)."""
+    natively, pt_decode_jpeg).  refraction=True reads the REFRACTIVE / IOR material keys the
+    reference loader ignores (PT_LOAD_REFRACTION; a file may also opt in with
+    "Extensions": {"REFRACTION": true}); by default they are ignored, like scene.cpp:46-56."""
 
-    def __init__(self, filename: str | os.PathLike | None = None):
+    def __init__(self, filename: str | os.PathLike | None = None, refraction: bool = False):
         self._h = C.c_void_p()
         L = lib()
         if filename is None:
             check_pt(L.pt_scene_create(C.byref(self._h)))
             return
-        check_pt(L.pt_scene_load_json(str(filename).encode(), C.byref(self._h)))
+        check_pt(L.pt_scene_load_json_ex(str(filename).encode(), 1 if refraction else 0, C.byref(self._h)))
+        self._fill_non_jpeg_textures()
+
+    def texture_path(self, tid: int) -> str:
+        buf = C.create_string_buffer(4096)
+        check_pt(lib().pt_scene_texture_path(self._h, int(tid), buf, 4096))
+        return buf.value.decode()
+
+    def _fill_non_jpeg_textures(self) -> None:
+        """Texture files that are not JPEG (PNG, BMP, TGA: stbi_load reads them too) are left
+        undecoded by the native loader (include/pt_amd.h); decode them here.  These formats are
+        lossless, so any decoder yields stbi_load(path, &w, &h, &comp, 0)'s texels; palette images
+        are expanded to RGB(A) as stb does."""
+        ntex = self.counts()[4]
+        for tid in range(ntex):
+            path = self.texture_path(tid)
+            with open(path, "rb") as f:
+                head = f.read(2)
+            if head == b"\xff\xd8":
+                continue
+            from PIL import Image   # (host-side file IO only; not on the render path)
+            with Image.open(path) as im:
+                if im.mode == "P":
+                    im = im.convert("RGBA" if "transparency" in im.info else "RGB")
+                elif im.mode not in ("L", "LA", "RGB", "RGBA"):
+                    im = im.convert("RGB")
+                px = np.ascontiguousarray(np.asarray(im, dtype=np.uint8))
+            h, w = px.shape[:2]
+            comps = 1 if px.ndim == 2 else px.shape[2]
+            check_pt(lib().pt_scene_set_texture_pixels(self._h, tid, w, h, comps, px.ctypes.data_as(C.c_void_p)))
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -266,16 +297,18 @@ class PathTracer:
     def profile(self, on: bool = True) -> None:
         check_pt(lib().pt_profile_enable(self._h, int(on)))
 
-    KINDS = ("first_bounce", "bounce", "compact", "sort")
+    # PT_KIND_* of include/pt_amd.h, in order
+    KINDS = ("first_bounce", "bounce", "compact", "sort", "traverse", "first_traverse")
 
     def profile_read(self) -> dict:
         """{kind: (summed ms, launches, busy ms)} since the previous read (HIP events on the launch
         streams); busy ms = the union of the kind's launch intervals (lanes overlap launches)."""
-        ms = (C.c_double * 4)()
-        busy = (C.c_double * 4)()
-        n = (C.c_uint64 * 4)()
-        check_pt(lib().pt_profile_read_busy(self._h, ms, busy, n))
-        return {k: (float(ms[i]), int(n[i]), float(busy[i])) for i, k in enumerate(self.KINDS)}
+        k = len(self.KINDS)
+        ms = (C.c_double * k)()
+        busy = (C.c_double * k)()
+        n = (C.c_uint64 * k)()
+        check_pt(lib().pt_profile_read_kinds(self._h, k, ms, busy, n))
+        return {name: (float(ms[i]), int(n[i]), float(busy[i])) for i, name in enumerate(self.KINDS)}
 
 
 def tonemap(image: np.ndarray, samples: float) -> np.ndarray:

@@ -4,7 +4,9 @@ Each generator writes a scene file (and, for meshes, an OBJ under Models/) into 
 returns its path; generation is deterministic for a given seed.  The files use only the keys the
 reference loader reads (scene.cpp:33-219), plus the REFRACTIVE / IOR extension for config 4
 (the reference loader ignores those keys — SURVEY.md §2 quirk 1 — so refraction is parity-unpinned
-against the reference itself; the CPU oracle restates the build's refraction).
+against the reference itself; the CPU oracle restates the build's refraction).  Scenes with glass
+opt in with the top-level "Extensions": {"REFRACTION": true} (pt_scene_load_json_ex); without it
+the loaders ignore the keys, as the reference's does.
 
   cornell_hd        config 3: cornell.json geometry, 1920x1080, DEPTH 16 (run with material sort on)
   multi_object      config 4: Cornell-style room with a grid of spheres and boxes — diffuse,
@@ -94,7 +96,8 @@ def multi_object(out_dir, res=(3840, 2160), depth=8, grid=(4, 3), seed=4) -> str
                 objs.append({"TYPE": "cube", "MATERIAL": mat, "TRANS": [x, size / 2 + 0.01, z],
                              "ROTAT": [0.0, float(rng.uniform(0, 90)), 0.0], "SCALE": [size, size, size]})
             k += 1
-    scene = {"Materials": mats, "Camera": _camera(res, depth, 5000, "multi_object"), "Objects": objs}
+    scene = {"Materials": mats, "Camera": _camera(res, depth, 5000, "multi_object"), "Objects": objs,
+             "Extensions": {"REFRACTION": True}}
     return _write(out_dir, "multi_object", scene)
 
 
@@ -145,7 +148,8 @@ def random_primitives(out_dir, n=24, res=(640, 480), depth=8, seed=7, extra_mate
                      "TRANS": [float(v) for v in rng.uniform((-4.5, 0.0, -4.5), (4.5, 9.5, 3.0))],
                      "ROTAT": [float(v) for v in rng.uniform(0.0, 360.0, 3)],
                      "SCALE": [float(v) for v in scale]})
-    scene = {"Materials": mats, "Camera": _camera(res, depth, 5000, "random_primitives"), "Objects": objs}
+    scene = {"Materials": mats, "Camera": _camera(res, depth, 5000, "random_primitives"), "Objects": objs,
+             "Extensions": {"REFRACTION": True}}
     return _write(out_dir, f"random_primitives_{seed}" + (f"_m{extra_materials}" if extra_materials else ""), scene)
 
 

@@ -154,15 +154,26 @@ void pt_flags_default(pt_flags* f);
 
 /* ---- scene ---------------------------------------------------------------------------- */
 int pt_scene_load_json(const char* path, pt_scene** out);   /* Scene::Scene(filename) incl. pt_scene_finalize */
+/* Loader extensions, all off by default (pt_scene_load_json == options 0 == the reference's loader).
+ * PT_LOAD_REFRACTION: read the material keys REFRACTIVE and IOR, which the reference's
+ * Scene::loadFromJSON never reads (scene.cpp:46-56; refraction is unreachable from its files).  A
+ * file can also opt in itself with the top-level key "Extensions": {"REFRACTION": true}, which the
+ * reference ignores; a reference scene file therefore loads exactly as the reference loads it. */
+#define PT_LOAD_REFRACTION 1u
+int pt_scene_load_json_ex(const char* path, uint32_t options, pt_scene** out);
 int pt_scene_create(pt_scene** out);
 void pt_scene_free(pt_scene* s);
 int pt_scene_add_material(pt_scene* s, const pt_material* m, int32_t* id_out);
 /* Texture pixels (row-major, `components` bytes per texel; only 3 is shaded, like the reference). */
 int pt_scene_add_texture(pt_scene* s, int32_t width, int32_t height, int32_t components,
                          const uint8_t* pixels, int32_t* id_out);
-/* JSON scenes reference textures by file (scene.cpp:61-71).  pt_scene_load_json decodes them with
- * pt_decode_jpeg (below) and fails with PT_ERR_IO where the reference prints "Texture load error!"
- * and exits.  pt_scene_set_texture_pixels replaces a texture's pixels (hosts with their own decoder). */
+/* JSON scenes reference textures by file (scene.cpp:61-71).  pt_scene_load_json decodes JPEG files
+ * with pt_decode_jpeg (below) and fails with PT_ERR_IO where the reference prints "Texture load
+ * error!" and exits (missing file, corrupt JPEG).  Files that are not JPEG (no SOI marker: PNG, BMP,
+ * TGA, ... which the reference's stbi_load also reads) are NOT decoded here: the texture keeps its
+ * path and no pixels, the host fills it with pt_scene_set_texture_pixels (the Python Scene does so
+ * for lossless formats, whose texels any decoder reproduces), and pt_create refuses a scene with a
+ * texture left unfilled.  pt_scene_set_texture_pixels also replaces a decoded texture's pixels. */
 int pt_scene_texture_path(const pt_scene* s, int32_t id, char* buf, int32_t cap);
 int pt_scene_set_texture_pixels(pt_scene* s, int32_t id, int32_t width, int32_t height,
                                 int32_t components, const uint8_t* pixels);
@@ -191,6 +202,11 @@ int pt_scene_get_geoms(const pt_scene* s, pt_geom* out, int32_t cap);
 int pt_scene_get_materials(const pt_scene* s, pt_material* out, int32_t cap);
 int pt_scene_get_triangles(const pt_scene* s, pt_triangle* out, int32_t cap);
 int pt_scene_get_bvh(const pt_scene* s, pt_bvh_node* out, int32_t cap);
+/* Inspection (host only, used by the tests): the 4-wide layout the BVH walk of mesh scenes runs on
+ * (128-byte entries: lo.x, hi.x, lo.y, hi.y, lo.z, hi.z, codes, meta — each 4 slots; layout and
+ * codes in pt_kernels.hip DQuad).  Returns the entry count (0: no 4-wide layout for this tree; the
+ * pair walk runs) and copies min(count, cap) entries; *root_code / *stack_bound as pt_create uses. */
+int pt_scene_bvh_quads(const pt_scene* s, void* out, int32_t cap, int32_t* root_code, int32_t* stack_bound);
 
 /* ---- render context -------------------------------------------------------------------- */
 /* pathtraceInit: uploads the scene to the current HIP device, allocates SoA path buffers for
@@ -225,16 +241,24 @@ int pt_stats(pt_ctx* c, pt_stats_t* out);                   /* synchronises the 
 /* Per-kernel device timing with hipEvents recorded on the launch stream (for the roofline).  When
  * enabled, pt_render_pass brackets every launch with pooled events; pt_profile_read synchronises
  * and returns, per kernel kind, the summed milliseconds and launch counts since the last read. */
-#define PT_KIND_FIRST_BOUNCE 0   /* bounce 0: k_bounce<FIRST> (fused) or k_trace<FIRST> (split)  */
+#define PT_KIND_FIRST_BOUNCE 0   /* bounce 0: k_bounce<FIRST> (fused), k_trace<FIRST> (split), or the
+                                    first k_sort_produce (sorted: raygen + intersection)           */
 #define PT_KIND_BOUNCE 1         /* bounces >= 1: k_bounce (fused) or k_trace (split)          */
 #define PT_KIND_COMPACT 2        /* split pipeline only: k_compact_paths                        */
-#define PT_KIND_SORT 3           /* material-sorted mode: raygen/isect/scan/scatter/shade      */
+#define PT_KIND_SORT 3           /* material-sorted mode, per bounce: histogram scan + producer
+                                    (shade bounce b, compact, intersect bounce b + 1)              */
+#define PT_KIND_TRAVERSE 4       /* mesh scenes, bounces >= 1: the BVH walk k_traverse[4]       */
+#define PT_KIND_FIRST_TRAVERSE 5 /* mesh scenes, bounce 0: the BVH walk of the camera rays       */
+#define PT_KIND_COUNT 6
 int pt_profile_enable(pt_ctx* c, int32_t on);
+/* The first four kinds (pt_profile_read_kinds returns all of them). */
 int pt_profile_read(pt_ctx* c, double ms[4], uint64_t launches[4]);
 /* Same, plus busy_ms[kind]: the length of the union of that kind's launch intervals.  Batched
  * passes of the fused pipeline run two lanes of iterations concurrently (pt_render_pass), so
  * launches of one kind overlap and busy_ms < ms. */
 int pt_profile_read_busy(pt_ctx* c, double ms[4], double busy_ms[4], uint64_t launches[4]);
+/* Every kind: arrays of nkinds entries (kinds >= PT_KIND_COUNT read 0).  busy_ms may be NULL. */
+int pt_profile_read_kinds(pt_ctx* c, int32_t nkinds, double* ms, double* busy_ms, uint64_t* launches);
 
 /* Device self-check of the range-gated correctly rounded sqrt / division cores the kernels use
  * (pt_device.h) against hipcc's library sqrtf and '/': n operand sets from `seed` (random bit

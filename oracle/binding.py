@@ -253,8 +253,13 @@ class OracleScene:
         self.cam = camera(res, fovy, eye, lookat, up)
 
     @classmethod
-    def from_json(cls, path) -> "OracleScene":
+    def from_json(cls, path, refraction: bool = False) -> "OracleScene":
+        """Scene::loadFromJSON (scene.cpp:33-219).  REFRACTIVE / IOR are read only with
+        refraction=True or a top-level "Extensions": {"REFRACTION": true} (the build's loader
+        extension; the reference reads neither key, scene.cpp:46-56)."""
         data = json.loads(Path(path).read_text())
+        ext = data.get("Extensions", {})
+        refraction = refraction or (ext.get("REFRACTION") is True if isinstance(ext, dict) else "REFRACTION" in ext)
         sc = cls()
         ids = {}
         base = Path(path).resolve().parent
@@ -266,7 +271,8 @@ class OracleScene:
                 tex = sc.add_texture(base / "Textures" / p["TEXTURE_FILE"])
             ids[name] = sc.add_material(rgb=rgb, specrgb=p.get("SPECRGB", rgb), specex=p.get("SPECEX", 1.0),
                                         reflective=p.get("REFLECTIVE", 0.0), emittance=p.get("EMITTANCE", 0.0),
-                                        refractive=p.get("REFRACTIVE", 0.0), ior=p.get("IOR", 0.0), texture_id=tex)
+                                        refractive=p.get("REFRACTIVE", 0.0) if refraction else 0.0,
+                                        ior=p.get("IOR", 0.0) if refraction else 0.0, texture_id=tex)
         for o in data["Objects"]:
             typ = {"sphere": 0, "cube": 1, "mesh": 2}[o["TYPE"]]
             mat = ids.get(o["MATERIAL"], 0)

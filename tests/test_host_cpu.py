@@ -192,3 +192,45 @@ def test_hdr_matches_stb_restatement_and_decodes(shape):
     ref = (img / np.float32(4.0))[:, ::-1]
     # RGBE shares one exponent per pixel: error <= 2^-7 of the pixel's largest component
     assert (np.abs(dec - ref) <= ref.max(axis=2, keepdims=True) * 2 ** -7 + 1e-30).all()
+
+
+def _cornell_with_refraction_keys(tmp_path, opt_in=None):
+    """cornell.json with REFRACTIVE / IOR added to two materials (keys the reference ignores)."""
+    scene = json.loads((SCENES / "cornell.json").read_text())
+    scene["Materials"]["specular_white"]["REFRACTIVE"] = 1.0
+    scene["Materials"]["specular_white"]["IOR"] = 1.5
+    scene["Materials"]["diffuse_red"]["IOR"] = 2.4
+    if opt_in is not None:
+        scene["Extensions"] = opt_in
+    path = tmp_path / "cornell_refr.json"
+    path.write_text(json.dumps(scene))
+    return path
+
+
+def _mat_table(s):
+    return [(tuple(m.color), m.has_reflective, m.has_refractive, m.ior, m.emittance) for m in s.materials()]
+
+
+def test_refraction_keys_ignored_by_default(tmp_path):
+    """scene.cpp:46-56 never reads REFRACTIVE or IOR: by default the
+    product's and the oracle's loaders ignore them too, so a reference scene that carries the keys
+    loads exactly like the bundled file (the GPU render equality is test_render_gpu.py's
+    test_refraction_keys_render_like_bundled_scene).  The extension is on with PT_LOAD_REFRACTION
+    (refraction=True) or the file's own "Extensions": {"REFRACTION": true}."""
+    path = _cornell_with_refraction_keys(tmp_path)
+    bundled = _mat_table(P.Scene(SCENES / "cornell.json"))
+    assert _mat_table(P.Scene(path)) == bundled
+    assert all(m[2] == 0.0 and m[3] == 0.0 for m in bundled)
+    on = _mat_table(P.Scene(path, refraction=True))
+    assert on != bundled and any(m[2] == 1.0 and m[3] == np.float32(1.5) for m in on)
+    for opt_in in ({"REFRACTION": True}, ["REFRACTION"]):
+        assert _mat_table(P.Scene(_cornell_with_refraction_keys(tmp_path, opt_in))) == on
+    assert _mat_table(P.Scene(_cornell_with_refraction_keys(tmp_path, {"REFRACTION": False}))) == bundled
+    # the oracle follows the same rule
+    o_off = [(m.has_refractive, m.ior) for m in O.OracleScene.from_json(path).materials]
+    o_on = [(m.has_refractive, m.ior) for m in O.OracleScene.from_json(path, refraction=True).materials]
+    assert o_off == [(m[2], m[3]) for m in bundled] and o_on == [(m[2], m[3]) for m in on]
+    with pytest.raises(N.PtError):
+        import ctypes as C
+        h = C.c_void_p()
+        N.check_pt(N.lib().pt_scene_load_json_ex(str(path).encode(), 0x80, C.byref(h)))

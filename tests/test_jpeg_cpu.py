@@ -98,3 +98,88 @@ def test_scene_loader_decodes_textures(tmp_path):
     p.write_text(json.dumps(spec))
     with pytest.raises(Exception, match="Texture load error"):
         Scene(p)
+
+
+def _segments(data: bytes):
+    """(marker, start, end) of the JPEG header segments up to SOS (end exclusive)."""
+    out, i = [], 2
+    while i + 4 <= len(data):
+        assert data[i] == 0xFF
+        m = data[i + 1]
+        L = (data[i + 2] << 8) | data[i + 3]
+        out.append((m, i, i + 2 + L))
+        if m == 0xDA:
+            break
+        i += 2 + L
+    return out
+
+
+def _decode_rc(data: bytes) -> int:
+    L = N.lib()
+    w, h, c = C.c_int32(), C.c_int32(), C.c_int32()
+    rc = L.pt_decode_jpeg(data, len(data), C.byref(w), C.byref(h), C.byref(c), None, 0)
+    if rc != 0:
+        return rc
+    out = np.zeros(w.value * h.value * c.value, np.uint8)
+    return L.pt_decode_jpeg(data, len(data), C.byref(w), C.byref(h), C.byref(c),
+                            out.ctypes.data_as(C.c_void_p), out.size)
+
+
+def test_corrupt_jpegs_fail_cleanly():
+    """a scan naming a Huffman table no DHT defined, non-integer sampling ratios and
+    corrupted entropy data are reported as errors (stb 2.06 reads out of bounds on the first two),
+    never a crash.  Valid files decode as before (the byte-equality tests above)."""
+    good = (SCENES / "Textures" / "chair.jpg").read_bytes()
+    assert _decode_rc(good) == 0
+    segs = _segments(good)
+    # 1) every DHT removed: the scan's tables are undefined
+    no_dht = bytearray(good[:2])
+    last = 2
+    for m, a, b in segs:
+        no_dht += good[last:a]
+        if m != 0xC4:
+            no_dht += good[a:b]
+        last = b
+    no_dht += good[last:]
+    assert _decode_rc(bytes(no_dht)) != 0
+    # 2) SOF with sampling factors 3 and 2 (h_max % h != 0)
+    sof = next((a, b) for m, a, b in segs if m in (0xC0, 0xC2))
+    bad = bytearray(good)
+    ncomp = bad[sof[0] + 9]
+    if ncomp == 3:
+        bad[sof[0] + 11] = 0x31   # component 1: H 3, V 1
+        bad[sof[0] + 14] = 0x21   # component 2: H 2, V 1
+        assert _decode_rc(bytes(bad)) != 0
+    # 3) random byte corruption of the entropy-coded data: errors or garbage, never a crash
+    rng = np.random.default_rng(11)
+    sos_end = segs[-1][2]
+    for _ in range(60):
+        b = bytearray(good)
+        for pos in rng.integers(sos_end, len(b) - 2, 8):
+            b[pos] = int(rng.integers(0, 256))
+        _decode_rc(bytes(b))
+
+
+def test_non_jpeg_texture_left_to_host(tmp_path):
+    """a PNG texture (stbi_load reads PNG too) is not decoded by the native JPEG path; the
+    native loader leaves it unfilled and the Python Scene fills it (lossless: the texels are the
+    file's).  A missing file still fails the load."""
+    import json
+    from PIL import Image
+    from cuda_pathtracer_amd import Scene
+    spec = json.loads((SCENES / "room.json").read_text())
+    (tmp_path / "Models").symlink_to(SCENES / "Models")
+    (tmp_path / "Textures").mkdir()
+    for m in spec["Materials"].values():
+        if m.get("TEXTURE_FILE"):
+            name = m["TEXTURE_FILE"]
+            Image.open(SCENES / "Textures" / name).convert("RGB").save(tmp_path / "Textures" / (name + ".png"))
+            m["TEXTURE_FILE"] = name + ".png"
+    p = tmp_path / "room_png.json"
+    p.write_text(json.dumps(spec))
+    s = Scene(p)
+    assert s.counts()[4] == 2 and s.texture_path(0).endswith(".png")
+    # the raw C loader alone leaves the textures unfilled (pt_create would refuse the scene)
+    h = C.c_void_p()
+    assert N.lib().pt_scene_load_json(str(p).encode(), C.byref(h)) == 0
+    N.lib().pt_scene_free(h)

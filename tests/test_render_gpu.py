@@ -523,6 +523,63 @@ def test_bounded_closest_hit_equals_plain_loop(config_scenes, monkeypatch):
     assert total > 100_000
 
 
+@pytest.mark.parametrize("walk", ["quad", "pairs"])
+def test_bvh_walk_records_equal_reference_walk(room_path, config_scenes, tmp_path, monkeypatch, walk):
+    """Every k_traverse4 (4-wide layout + leaf tasks; PT_AMD_TRAV=pairs: round 2's pair walk)
+    record — closest triangle, t, barycentrics — equals the reference's node-at-a-time
+    BVHIntersectionTest re-run on the device for the same ray (PT_AMD_VERIFY_BOUNDS=1 in the mesh
+    bounce kernel counts differences): room (textured chairs), the 3000-triangle scene and config 5's
+    100k-triangle tree, every bounce of several batched passes."""
+    from cuda_pathtracer_amd import PathTracer, Scene, scenes
+    monkeypatch.setenv("PT_AMD_VERIFY_BOUNDS", "1")
+    if walk == "pairs":
+        monkeypatch.setenv("PT_AMD_TRAV", "pairs")
+    big = scenes.random_triangles(tmp_path, n=100_000, res=(320, 180), depth=32)
+    total = 0
+    for path, spp in ((room_path, 4), (config_scenes["random_triangles"], 4), (big, 2)):
+        s = Scene(path)
+        if path == room_path:
+            s.set_camera((96, 72), 45.0, (0, 5, 10.5), (0, 5, 0), (0, 1, 0))
+            s.finalize()
+        pt = PathTracer(s, _gui(), spp=spp)
+        for k in range(2):
+            pt.render_pass(1 + spp * k)
+        st = pt.stats()
+        pt.free()
+        assert st["bound_mismatch"] == 0, (path, st["bound_mismatch"])
+        total += st["segments"]
+    assert total > 200_000
+
+
+def test_refraction_keys_render_like_bundled_scene(cornell_path, tmp_path):
+    """A reference scene file carrying REFRACTIVE / IOR (keys scene.cpp:46-56 never reads) renders
+    bit-identically to the bundled cornell.json when the loader extension is off (the default),
+    and differently — with glass — when it is on (PT_LOAD_REFRACTION), against the oracle."""
+    import json
+    from cuda_pathtracer_amd import PathTracer, Scene
+    scene = json.loads(open(cornell_path).read())
+    scene["Materials"]["specular_white"]["REFRACTIVE"] = 1.0
+    scene["Materials"]["specular_white"]["IOR"] = 1.5
+    path = tmp_path / "cornell_refr.json"
+    path.write_text(json.dumps(scene))
+    def render(s):
+        s.set_camera((64, 64), 45.0, (0, 5, 10.5), (0, 5, 0), (0, 1, 0))
+        s.finalize()
+        pt = PathTracer(s, _gui(), spp=2)
+        pt.render_pass(1)
+        img = pt.image()
+        pt.free()
+        return img
+    base = render(Scene(cornell_path))
+    assert np.array_equal(render(Scene(path)), base)
+    glass = render(Scene(path, refraction=True))
+    assert not np.array_equal(glass, base)
+    o = O.OracleScene.from_json(path, refraction=True)
+    o.set_camera((64, 64), 45.0, (0, 5, 10.5), (0, 5, 0), (0, 1, 0))
+    ref = O.render_pass(o, O.flags(), 1, spp=2)[0]
+    _assert_bitexact(glass, ref, "cornell + REFRACTIVE/IOR, extension on")
+
+
 def test_resume_from_checkpoint_is_bitexact(cornell_path, tmp_path):
     """Extension: checkpoint the float accumulator after 2 passes, resume in
     a fresh context at the next iteration index: identical to rendering the 4 passes in one go."""
