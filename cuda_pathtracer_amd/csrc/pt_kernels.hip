@@ -394,11 +394,15 @@ __device__ __forceinline__ MeshHit bvh_walk_pairs(const SceneDev& S, f3 o, f3 d,
 // right group's axis << 8 (3: a one-slot group, never swapped).  Codes as DPair's, with interior
 // codes = quad index.  Boxes are SoA (one v4f per bound and axis) so the four slab tests run two
 // slots per packed f32 instruction.
+// An interior code carries its quad's meta bits above the index (kQuadMetaShift), so a walk learns
+// the order of a quad's slots from the code that led to it and loads 112 of the entry's 128 bytes.
 struct alignas(16) DQuad {
     v4f lox, hix, loy, hiy, loz, hiz;
     v4f code;   // int bits
-    v4f meta;   // [0]: int bits (above)
+    v4f meta;   // [0]: int bits (above; also in the interior codes that point here)
 };
+constexpr int kQuadMetaShift = 21;                        // interior code = quad index | meta << 21
+constexpr int kQuadIdxMask = (1 << kQuadMetaShift) - 1;   // (a layout of more quads is not built)
 
 constexpr int kRecWalkHere = -2;   // k_traverse4 record: not walked (non-finite ray), k_bounce walks it
 constexpr int kWalkDone = (int)0x80000000;   // k_traverse: no node left (below every leaf code, first < 2^23)
@@ -1283,6 +1287,9 @@ constexpr int kFoldBatch = PT_FOLD_BATCH;   // k_traverse4: task results read pe
 #ifndef PT_T4_LOADS
 #define PT_T4_LOADS 0    // k_traverse4 loads: 0 masked, quad first; 1 every lane; 2 masked, triangle after the box tests
 #endif
+#ifndef PT_T4_OVERLAP
+#define PT_T4_OVERLAP 1  // k_traverse4: a leaf sent out whole and the node after it in one trip
+#endif
 #ifndef PT_T4_ASSIGN
 #define PT_T4_ASSIGN 0   // k_traverse4 leaf tasks: 0 owner tag + ballot + ds_bpermute; 1 task slots written by owners
 #endif
@@ -1683,19 +1690,18 @@ __global__ __launch_bounds__(kBlock, PT_T4_WAVES) void k_traverse4(const KArgs A
 #ifdef PT_TRAV_STATS
         if (lane == 0) { ++w_trips; n_busy += (uint32_t)__popcll(busy); }
 #endif
-        // ---- the quad of every interior lane ----
-        const bool inner = have && !leaf;
-        v4f x0, x1, x2, x3, x4, x5, x6;
-        uint32_t meta;
-#if PT_T4_LOADS == 1   // every lane loads (idle and leaf lanes: their last quad, cached): static wait counts
-        {
-#else
-        if (inner) {
-#endif
-            const v4f* qsrc = reinterpret_cast<const v4f*>(S.quads + cur);
-            x0 = qsrc[0]; x1 = qsrc[1]; x2 = qsrc[2]; x3 = qsrc[3]; x4 = qsrc[4]; x5 = qsrc[5]; x6 = qsrc[6];
-            meta = reinterpret_cast<const uint32_t*>(qsrc)[28];
-        }
+        // the stack this trip: LDS only unless some lane could reach the LDS rows (3 pushes at most)
+        const bool fast = __ballot(top + 4 > rows) == 0;
+        auto push = [&](int v) {
+            if (fast) col[top * kBlock] = v;
+            else hst.set(top, v);
+            ++top;
+        };
+        auto pop = [&]() -> int {
+            if (top == 0) return kWalkDone;
+            --top;
+            return fast ? col[top * kBlock] : hst.get(top);
+        };
         // ---- leaf tasks: the remaining triangles of the leaf lanes, one per lane of the wave ----
         const int cnt = (have && leaf) ? te - ti : 0;
         const int incl = (int)lb::wave_inclusive_scan((uint32_t)cnt);
@@ -1703,6 +1709,33 @@ __global__ __launch_bounds__(kBlock, PT_T4_WAVES) void k_traverse4(const KArgs A
         const int T = __builtin_amdgcn_readlane(incl, 63);
         const int cov = (cnt > 0 && pre < 64) ? min(cnt, 64 - pre) : 0;   // this trip's tasks of this lane
         const bool is_task = lane < T;
+        bool inner = have && !leaf;
+#if PT_T4_OVERLAP
+        // A leaf lane whose remaining triangles all go out this trip already takes its next node
+        // (everything after the leaf in the walk's order): an interior node is tested in this same
+        // trip, beside its leaf's triangle tests, whose results are folded first (the order of the
+        // triangles is unchanged: the node's triangles are tested in later trips).
+        int after_leaf = kWalkNone;
+        if (cov > 0 && cov == cnt) {
+            after_leaf = pop();
+            if (after_leaf >= 0) {
+                cur = after_leaf;
+                inner = true;
+            }
+        }
+#endif
+        // ---- the quad of every interior lane ----
+        v4f x0, x1, x2, x3, x4, x5, x6;
+        uint32_t meta;
+#if PT_T4_LOADS == 1   // every lane loads (idle and leaf lanes: their last quad, cached): static wait counts
+        {
+#else
+        if (inner) {
+#endif
+            const v4f* qsrc = reinterpret_cast<const v4f*>(S.quads + (cur & kQuadIdxMask));
+            x0 = qsrc[0]; x1 = qsrc[1]; x2 = qsrc[2]; x3 = qsrc[3]; x4 = qsrc[4]; x5 = qsrc[5]; x6 = qsrc[6];
+        }
+        meta = (uint32_t)cur >> kQuadMetaShift;   // (the code that led here carries the quad's meta)
         f3 to = F3(0, 0, 0), td = F3(0, 0, 0);
         int tidx = 0;
         if (T > 0) {   // (wave-uniform)
@@ -1756,18 +1789,6 @@ __global__ __launch_bounds__(kBlock, PT_T4_WAVES) void k_traverse4(const KArgs A
             if (lane == 0 && ib) { ++t_inner; n_inner += (uint32_t)__popcll(ib); }
         }
 #endif
-        // the stack this trip: LDS only unless some lane could reach the LDS rows (3 pushes at most)
-        const bool fast = __ballot(top + 4 > rows) == 0;
-        auto push = [&](int v) {
-            if (fast) col[top * kBlock] = v;
-            else hst.set(top, v);
-            ++top;
-        };
-        auto pop = [&]() -> int {
-            if (top == 0) return kWalkDone;
-            --top;
-            return fast ? col[top * kBlock] : hst.get(top);
-        };
         // ---- interior step ----
         int next = kWalkNone;
         if (inner) {
@@ -1819,7 +1840,11 @@ __global__ __launch_bounds__(kBlock, PT_T4_WAVES) void k_traverse4(const KArgs A
                         if (k0 + k < cov) fold(x[k], ti + k0 + k);
                 }
                 ti += cov;
+#if PT_T4_OVERLAP
+                if (ti == te && !inner) next = after_leaf;   // (inner: the quad step above set `next`)
+#else
                 if (ti == te) next = pop();
+#endif
             }
         }
         if (next == kWalkDone) {
@@ -3101,8 +3126,27 @@ bool make_quads(const std::vector<DNode>& nodes, std::vector<DQuad>& quads, int3
             for (auto it = kids.rbegin(); it != kids.rend(); ++it) stk.push_back(*it);
         }
     }
+    if (order.size() > (size_t)kQuadIdxMask) return false;
     quads.resize(std::max<size_t>(order.size(), 1));
     occ.assign(order.size(), 0);
+    // each quad's meta first: the interior codes pointing at a quad carry it
+    std::vector<uint32_t> qmeta(order.size(), 0);
+    for (size_t qi = 0; qi < order.size(); ++qi) {
+        const size_t i = order[qi];
+        uint32_t valid = 0, axes[2] = {3u, 3u};
+        const size_t ch[2] = {i + 1, (size_t)link(i)};
+        for (int g = 0; g < 2; ++g) {
+            const size_t x = ch[g];
+            if (meta(x) <= 0 && inside(x + 1, x) && inside((size_t)link(x), x)) {
+                valid |= 3u << (2 * g);
+                axes[g] = (uint32_t)(-meta(x) - 1);
+            } else {
+                valid |= 1u << (2 * g);
+            }
+        }
+        qmeta[qi] = valid | ((uint32_t)(-meta(i) - 1) << 4) | (axes[0] << 6) | (axes[1] << 8);
+    }
+    auto qcode = [&](size_t y) { return (int32_t)((uint32_t)qid[y] | (qmeta[(size_t)qid[y]] << kQuadMetaShift)); };
     for (size_t qi = 0; qi < order.size(); ++qi) {
         const size_t i = order[qi];
         DQuad& Q = quads[qi];
@@ -3116,7 +3160,7 @@ bool make_quads(const std::vector<DNode>& nodes, std::vector<DQuad>& quads, int3
             auto slot = [&](int s, size_t y) {
                 valid |= 1u << s;
                 box[s] = y;
-                codes[s] = meta(y) > 0 ? leaf_code(y) : qid[y];
+                codes[s] = meta(y) > 0 ? leaf_code(y) : qcode(y);
             };
             if (meta(x) <= 0 && inside(x + 1, x) && inside((size_t)link(x), x)) {
                 slot(2 * g, x + 1);
@@ -3146,13 +3190,13 @@ bool make_quads(const std::vector<DNode>& nodes, std::vector<DQuad>& quads, int3
             if (!((m >> s) & 1u)) continue;
             ++nv;
             const int32_t cd = __float_as_int_host(Q.code[s]);
-            if (cd >= 0) deepest = std::max(deepest, occ[(size_t)cd]);
+            if (cd >= 0) deepest = std::max(deepest, occ[(size_t)(cd & kQuadIdxMask)]);
         }
         occ[qi] = nv - 1 + deepest;
         root_occ = occ[qi];
     }
     if (order.empty()) root_occ = 0;
-    root_code = meta(0) > 0 ? leaf_code(0) : 0;
+    root_code = meta(0) > 0 ? leaf_code(0) : qcode(0);
     return root_occ <= 64;   // HybStack holds rows + 64 >= 64 entries
 }
 

@@ -34,6 +34,9 @@ GROUPS = {
                "SQ_ACTIVE_INST_SCA", "SQ_ACTIVE_INST_MISC", "SQ_IFETCH", "SQ_IFETCH_LEVEL"],
     "stall2": ["SQ_INST_LEVEL_VMEM", "SQ_INSTS_VMEM", "SQ_INST_LEVEL_LDS", "SQ_INSTS_LDS",
                "SQ_INST_LEVEL_SMEM", "SQ_INSTS_SMEM", "SQ_WAIT_ANY", "SQ_LDS_BANK_CONFLICT"],
+    # vector L1: accesses, requests to L2 and their summed latency (average L2 round trip per request)
+    "tcp": ["TCP_TOTAL_ACCESSES_sum", "TCP_TCC_READ_REQ_sum", "TCP_TCC_READ_REQ_LATENCY_sum", "TCP_TCP_LATENCY_sum"],
+    "ta": ["TA_TA_BUSY_sum", "TA_ADDR_STALLED_BY_TC_CYCLES_sum"],
 }
 
 

@@ -22,6 +22,7 @@ import cuda_pathtracer_amd as P
 from cuda_pathtracer_amd import _native as N
 from oracle import binding as O
 
+IDX_MASK = (1 << 21) - 1   # interior code = quad index | meta << 21
 QUAD_DTYPE = np.dtype([("lox", "<f4", 4), ("hix", "<f4", 4), ("loy", "<f4", 4), ("hiy", "<f4", 4),
                        ("loz", "<f4", 4), ("hiz", "<f4", 4), ("code", "<i4", 4), ("meta", "<i4", 4)])
 assert QUAD_DTYPE.itemsize == 128
@@ -103,8 +104,9 @@ def _walk_quads(pn, Q, root_code, o, d, max_stack):
                 break
             code = stack.pop()
             continue
-        q = Q[code]
-        meta = int(q["meta"][0])
+        q = Q[code & IDX_MASK]
+        meta = (code >> 21) & 1023   # the code carries its quad's meta (k_traverse4 reads it there)
+        assert meta == int(q["meta"][0])
         hm = 0
         for k in range(4):
             lo = np.array([q["lox"][k], q["loy"][k], q["loz"][k]], f32)
@@ -156,13 +158,13 @@ def _check_structure(pn, Q, root, bound):
                 continue
             cd = int(q["code"][k])
             if cd >= 0:
-                assert cd < nq
+                assert (cd & IDX_MASK) < nq and (cd >> 21) == int(Q[cd & IDX_MASK]["meta"][0])
             else:
                 c = -cd - 1
                 leaves.add((c >> 8, c & 255))
     real = {(int(x["first_area_idx"]), int(x["sub_areas"])) for x in pn if x["sub_areas"] > 0}
     assert leaves == real, "every leaf is a slot of exactly the quads that reach it"
-    assert root == 0 and 0 < bound <= 64
+    assert (root & IDX_MASK) == 0 and (root >> 21) == int(Q[0]["meta"][0]) and 0 < bound <= 64
 
 
 @pytest.mark.parametrize("which", ["room", "tri3000", "tri20000"])
