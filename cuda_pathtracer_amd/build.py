@@ -130,8 +130,30 @@ def build_pin(verbose: bool = False, force: bool = False) -> Path:
     return PIN_LIB
 
 
+TESTHOOKS_LIB = PKG / "build" / "libpt_amd_testhooks.so"
+
+
+def build_test_hooks(verbose: bool = False, force: bool = False) -> Path:
+    """Test infrastructure: the library with sc_kernels.hip's test hooks compiled in
+    (-DPT_SC_TEST_HOOKS: PT_AMD_TEST_SCAN_OVERSUB), loaded only by tests/test_scan_gpu.py's
+    stall test through PT_AMD_LIB.  The shipping libpt_amd.so has no hook."""
+    objdir = PKG / "build"
+    src = CSRC / "sc_kernels.hip"
+    obj = objdir / "sc_kernels_testhooks.o"
+    headers = list(CSRC.glob("*.h")) + list((ROOT / "include").glob("*.h"))
+    if force or _stale(obj, [src] + headers):
+        _run([HIPCC, "-x", "hip", f"--offload-arch={ARCH}", *COMMON, "-DPT_SC_TEST_HOOKS", "-I", str(ROOT / "include"),
+              "-c", str(src), "-o", str(obj)], verbose)
+    others = [objdir / (s + ".o") for s in DEVICE_SRCS + HOST_SRCS if s != "sc_kernels.hip"]
+    if force or _stale(TESTHOOKS_LIB, [obj] + others):
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(TESTHOOKS_LIB), str(obj),
+              *map(str, others), "-lz"], verbose)
+    return TESTHOOKS_LIB
+
+
 def build_all(verbose: bool = False, force: bool = False) -> None:
     build_native(verbose, force)
+    build_test_hooks(verbose, force)
     build_oracle(verbose, force)
     build_cpp_tests(verbose, force)
     build_pin(verbose, force)

@@ -47,13 +47,18 @@ std::atomic<bool> g_schedule_claimed{[] {
     return v && std::strcmp(v, "claim") == 0;
 }()};
 
-// Test hook (tests/test_scan_gpu.py): PT_AMD_TEST_SCAN_OVERSUB=k launches the look-back kernels on
-// k x the co-resident grid, so the static schedule stalls and must report its spin bound.
+#ifdef PT_SC_TEST_HOOKS
+// Test build only (build/libpt_amd_testhooks.so, tests/test_scan_gpu.py): PT_AMD_TEST_SCAN_OVERSUB=k
+// launches the look-back kernels on k x the co-resident grid, so the static schedule stalls and must
+// report its spin bound.  The shipping library has no such hook.
 const int g_test_oversub = [] {
     const char* v = std::getenv("PT_AMD_TEST_SCAN_OVERSUB");
     const int k = v ? std::atoi(v) : 1;
     return k >= 1 && k <= 16 ? k : 1;
 }();
+#else
+constexpr int g_test_oversub = 1;
+#endif
 
 int fail(int code, const std::string& msg) { g_err = msg; return code; }
 int hip_fail(hipError_t e, const char* where) {

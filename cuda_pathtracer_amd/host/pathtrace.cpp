@@ -33,8 +33,8 @@ pt_flags flags_of(const GuiDataContainer* g) {
         f.focal_dist = g->focal_len;
         f.single_albedo = g->singleAlbedo;
         f.bvh_cull = g->bvhCull;
-        f.shared_gpu = g->sharedGPU || f.shared_gpu;
-        f.rng_key_pixel = g->rngKeyPixel;   // PT_AMD_SCHEDULE=claim also selects it
+        f.shared_gpu = g->sharedGPU || f.shared_gpu;   // PT_AMD_SCHEDULE=claim also selects it
+        f.rng_key_pixel = g->rngKeyPixel;
     }
     return f;
 }

@@ -72,19 +72,33 @@ def _check_dev_i32(t, name: str):
         raise TypeError(f"{name} must be a contiguous int32 CUDA tensor")
 
 
-def scan_device(d_in, d_out=None, stream=None):
-    """Exclusive scan of a device int32 tensor (single-pass decoupled look-back)."""
+def _checked(stream, check: bool) -> None:
+    """check=True: wait for the call and read the workspace's device error word (sc_workspace_check).
+    The device-pointer entry points are asynchronous; a static-schedule look-back that could not get
+    the whole GPU (another process or stream holding part of it) drains with wrong results and sets
+    that word instead of failing the call — check=True (or sc_set_tile_schedule(1) for shared GPUs)
+    turns it into an exception."""
+    if check:
+        import torch
+        torch.cuda.synchronize()
+        check_sc(lib().sc_workspace_check(None))
+
+
+def scan_device(d_in, d_out=None, stream=None, check: bool = False):
+    """Exclusive scan of a device int32 tensor (single-pass decoupled look-back).  check: see _checked."""
     import torch
     _check_dev_i32(d_in, "d_in")
     if d_out is None:
         d_out = torch.empty_like(d_in)
     _check_dev_i32(d_out, "d_out")
     check_sc(lib().sc_scan_exclusive_i32(d_in.data_ptr(), d_out.data_ptr(), d_in.numel(), None, _stream_ptr(stream)))
+    _checked(stream, check)
     return d_out
 
 
-def compact_device(d_in, d_out=None, stream=None):
-    """Returns (d_out, d_count): non-zero elements first (in order), count as a 1-element int64 tensor."""
+def compact_device(d_in, d_out=None, stream=None, check: bool = False):
+    """Returns (d_out, d_count): non-zero elements first (in order), count as a 1-element int64 tensor.
+    check: see _checked."""
     import torch
     _check_dev_i32(d_in, "d_in")
     if d_out is None:
@@ -93,11 +107,13 @@ def compact_device(d_in, d_out=None, stream=None):
     cnt = torch.zeros(1, dtype=torch.int64, device=d_in.device)
     check_sc(lib().sc_compact_i32(d_in.data_ptr(), d_out.data_ptr(), d_in.numel(), cnt.data_ptr(), None,
                                   _stream_ptr(stream)))
+    _checked(stream, check)
     return d_out, cnt
 
 
-def partition_device(d_flags, d_perm=None, stream=None):
-    """Stable partition of indices (live first, then dead), like pathtrace.cu:366-376 `keep`."""
+def partition_device(d_flags, d_perm=None, stream=None, check: bool = False):
+    """Stable partition of indices (live first, then dead), like pathtrace.cu:366-376 `keep`.
+    check: see _checked."""
     import torch
     _check_dev_i32(d_flags, "d_flags")
     if d_perm is None:
@@ -105,12 +121,13 @@ def partition_device(d_flags, d_perm=None, stream=None):
     live = torch.zeros(1, dtype=torch.int64, device=d_flags.device)
     check_sc(lib().sc_partition_i32(d_flags.data_ptr(), d_perm.data_ptr(), d_flags.numel(), live.data_ptr(), None,
                                     _stream_ptr(stream)))
+    _checked(stream, check)
     return d_perm, live
 
 
-def live_indices_device(d_flags, d_idx=None, stream=None):
+def live_indices_device(d_flags, d_idx=None, stream=None, check: bool = False):
     """Index list of the non-zero flags, in order (sc_partition_indices): returns (d_idx, count)
-    with the count as a 1-element int32 tensor; d_idx beyond the count is untouched."""
+    with the count as a 1-element int32 tensor; d_idx beyond the count is untouched.  check: see _checked."""
     import torch
     _check_dev_i32(d_flags, "d_flags")
     if d_idx is None:
@@ -119,4 +136,5 @@ def live_indices_device(d_flags, d_idx=None, stream=None):
     cnt = torch.zeros(1, dtype=torch.int32, device=d_flags.device)
     check_sc(lib().sc_partition_indices(d_flags.data_ptr(), d_idx.data_ptr(), d_flags.numel(), cnt.data_ptr(), None,
                                         _stream_ptr(stream)))
+    _checked(stream, check)
     return d_idx, cnt

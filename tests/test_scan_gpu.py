@@ -97,6 +97,24 @@ def test_live_indices_match_keep(gpu_device, n):
     assert (got[ref_live:] == -7).all()
 
 
+def test_device_wrappers_check_option(gpu_device):
+    """the asynchronous device entry points report a look-back stall only through the
+    workspace's error word; check=True synchronises and reads it (sc_workspace_check).  On a GPU this
+    process has to itself every call succeeds, and the results are the oracle's."""
+    import torch
+    from cuda_pathtracer_amd import compact_device, live_indices_device, partition_device, scan_device
+    a = _gen(300_001, 50, 3)
+    d = torch.from_numpy(a).to(gpu_device)
+    np.testing.assert_array_equal(scan_device(d, check=True).cpu().numpy(), O.scan(a))
+    out, cnt = compact_device(torch.from_numpy(_gen(300_001, 4, 4)).to(gpu_device), check=True)
+    assert int(cnt.item()) == len(O.compact_without_scan(_gen(300_001, 4, 4)))
+    f = _gen(100_000, 2, 5)
+    perm, live = partition_device(torch.from_numpy(f).to(gpu_device), check=True)
+    assert int(live.item()) == O.partition_indices(f)[1]
+    idx, c2 = live_indices_device(torch.from_numpy(f).to(gpu_device), check=True)
+    assert int(c2.item()) == O.partition_indices(f)[1]
+
+
 def test_edge_cases(gpu_device):
     import torch
     from cuda_pathtracer_amd import compact_device, scan_device
@@ -269,7 +287,7 @@ print("RESULT", rc, rc2, rc3, ok3, "|", msg)
 
 def test_static_schedule_stall_is_reported(gpu_device, tmp_path):
     """a static-schedule scan whose grid is not co-resident (forced here with the
-    PT_AMD_TEST_SCAN_OVERSUB=4 test hook: 4x the resident grid) hits its bounded spin; the device
+    PT_AMD_TEST_SCAN_OVERSUB=4 hook of the test-hook build: 4x the resident grid) hits its bounded spin; the device
     error word is read back — sc_workspace_check and the host-pointer helper return SC_ERR_HIP
     instead of SC_OK with wrong prefixes — and the claimed schedule still completes correctly."""
     import os
@@ -277,7 +295,9 @@ def test_static_schedule_stall_is_reported(gpu_device, tmp_path):
     import sys
     from pathlib import Path
     root = str(Path(__file__).resolve().parent.parent)
-    env = dict(os.environ, PT_AMD_TEST_SCAN_OVERSUB="4")
+    hooks = Path(root) / "cuda_pathtracer_amd" / "build" / "libpt_amd_testhooks.so"   # build.build_test_hooks
+    assert hooks.exists(), "test-hook library missing (build() builds it)"
+    env = dict(os.environ, PT_AMD_TEST_SCAN_OVERSUB="4", PT_AMD_LIB=str(hooks))
     res = subprocess.run([sys.executable, "-c", _STALL_SCRIPT, root], env=env, capture_output=True, text=True,
                          timeout=120)
     line = [x for x in res.stdout.splitlines() if x.startswith("RESULT")]
