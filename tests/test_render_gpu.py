@@ -790,6 +790,29 @@ def test_config3_full_size_sorted_bitexact(cornell_path, tmp_path, spp):
     assert st["bounce_live"] == live and live[0] == spp * 1920 * 1080
 
 
+def test_config4_full_size_bitexact(tmp_path, monkeypatch):
+    """BASELINE.json config 4 at its full width — 3840x2160, the 12-object room (diffuse, mirror,
+    glass) — one iteration, GPU == oracle bit for bit with the first-bounce camera masks on (one
+    per 64 pixels of the 4K tile); then the split pipeline under PT_AMD_VERIFY_BOUNDS=1 re-runs the
+    plain closest-hit loop for every ray of the same iteration and counts 0 differences."""
+    from cuda_pathtracer_amd import PathTracer, Scene, scenes
+    path = scenes.multi_object(tmp_path, res=(3840, 2160), depth=8)
+    g, r, st, live = _run(Scene(path), O.OracleScene.from_json(path), _gui(), iters=1)
+    _assert_bitexact(g, r, "config 4 full size")
+    assert st["bounce_live"] == live and live[0] == 3840 * 2160 and r.sum() > 0
+    monkeypatch.setenv("PT_AMD_VERIFY_BOUNDS", "1")
+    monkeypatch.setenv("PT_PIPELINE", "split")
+    # (claimed tile schedule: the diagnostic split pipeline's look-back at this size outruns the
+    # static schedule's co-resident grid)
+    pt = PathTracer(Scene(path), _gui(sharedGPU=True))
+    pt.render_pass(1)
+    vs = pt.stats()
+    gv = pt.image()
+    pt.free()
+    assert vs["bound_mismatch"] == 0 and vs["segments"] == sum(live)
+    _assert_bitexact(gv, r, "config 4 full size, split pipeline")
+
+
 def test_sorted_multitile_histogram_scan(cornell_path):
     """Two-lane sorted passes with a histogram of nmats x (P/2)/64 = 5 x 1875 > 4096 entries per lane
     (several tiles of k_hist_sums / k_hist_scan_sums / k_hist_apply, multi-element threads in the
