@@ -216,16 +216,24 @@ def _pmc_leg(args, scene_path, spp_pass, sorted_, avg_ms, kernel_prefix, seg_per
     res = pmc.collect(wl, out_dir, timeout=args.pmc_timeout, groups=groups)
     (out_dir / "summary.json").write_text(json.dumps(res, indent=1))
     if sorted_:   # the sorted pipeline: every kernel of a bounce, per traced segment
+        # bounces >= 1 only, like the numerator: the first producer (camera rays, k_sort_produce<true>)
+        # is left out of the bytes, and bounce 0's paths out of the segments
         ks = {k: m for k, m in res.get("kernels", {}).items()
-              if k.startswith(("k_sort_", "k_hist_", "k_scan_lag", "k_scan_tiles"))}
+              if k.startswith(("k_sort_", "k_hist_", "k_scan_lag", "k_scan_tiles"))
+              and not k.startswith("k_sort_produce<true")}
         if not ks or not all("bytes_per_launch" in m for m in ks.values()):
             return {"pmc": res["_passes"]}
         total = sum(m["bytes_per_launch"] * m["launches"] for m in ks.values())
-        segs = res.get("segments") or 0
+        live = res.get("bounce_live")
+        segs = sum(live[1:]) if live else 0
+        first = next((m for k, m in res.get("kernels", {}).items() if k.startswith("k_sort_produce<true")), None)
         out = {"pmc": res["_passes"], "traffic_per_segment": total / segs if segs else None,
-               "traffic_definition": "FETCH_SIZE x 2 + WRITE_SIZE of every sorted-pipeline kernel over the "
-                                     "profiled passes / their traced segments (all bounces); traffic = that x "
-                                     "segments per pipeline bounce, like algorithmic_bytes_per_launch",
+               "traffic_definition": "FETCH_SIZE x 2 + WRITE_SIZE of the sorted-pipeline kernels of bounces >= 1 "
+                                     "(every k_sort_produce<false> + the histogram scans) over the profiled passes "
+                                     "/ their traced segments of bounces >= 1; traffic = that x segments per "
+                                     "pipeline bounce, like algorithmic_bytes_per_launch",
+               "first_producer_bytes_per_path": (first["bytes_per_launch"] * first["launches"] / live[0])
+               if first and "bytes_per_launch" in first and live and live[0] else None,
                "traffic_kernels": sorted(ks)}
         if segs:
             out["traffic"] = total / segs * seg_per_launch

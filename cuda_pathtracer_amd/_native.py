@@ -113,6 +113,8 @@ SIGNATURES = {
     "pt_scene_set_camera": (_I, [_P, _I, _I, _F, _FP, _FP, _FP]),
     "pt_scene_set_render": (_I, [_P, _I, _I, C.c_char_p]),
     "pt_scene_finalize": (_I, [_P]),
+    "pt_scene_set_bvh_builder": (_I, [_P, _I]),
+    "pt_scene_bvh_build_info": (_I, [_P, _IP, C.POINTER(C.c_double)]),
     "pt_scene_counts": (_I, [_P, _IP, _IP, _IP, _IP, _IP]),
     "pt_scene_get_camera": (_I, [_P, C.POINTER(Camera)]),
     "pt_scene_get_render": (_I, [_P, _IP, _IP, C.c_char_p, _I]),

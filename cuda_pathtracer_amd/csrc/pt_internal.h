@@ -32,6 +32,9 @@ struct Scene {
     bool camera_set = false;
     bool finalized = false;
     bool bvh_built = false;
+    int32_t bvh_builder = 0;     // requested: 0 host (pt_mesh.cpp), 1 device (bvh_build.hip)
+    int32_t bvh_on_device = 0;   // the last build ran on the device
+    double bvh_ms = 0.0;         // the last build's wall time (host clock)
 };
 
 int scene_add_geom(Scene& S, int32_t type, int32_t mat, const float* t, const float* r, const float* s);
@@ -42,6 +45,8 @@ int add_mesh(Scene& S, int32_t mat, const float* t, const float* r, const float*
              const float* nrm, int32_t nnrm, const float* uv, int32_t nuv, const int32_t* face_sizes, int32_t nfaces,
              const int32_t* ip, const int32_t* in, const int32_t* it, int32_t* id_out);
 int build_bvh(Scene& S);
+// Device SAH build (bvh_build.hip): PT_OK, 1 = not on the device (the caller builds on the host), or an error.
+int build_bvh_device(Scene& S, double* ms);
 // JPEG textures (pt_jpeg.cpp): stbi_load(path, ..., req_comp = 0) restated
 int decode_jpeg(const uint8_t* data, size_t size, int32_t* width, int32_t* height, int32_t* components,
                 std::vector<uint8_t>* pixels);

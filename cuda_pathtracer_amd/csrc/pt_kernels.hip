@@ -913,21 +913,31 @@ __device__ __forceinline__ int slot_pixel(const CamDev& cam, const TileDev& T, i
     return (lp - row * T.W) + (row * T.world + T.rank) * cam.res[0];
 }
 
+// shade()'s two exits that draw no random numbers (pathtrace.cu:318-330): a miss (colour 0) and an
+// emissive hit (colour x material colour x emittance).  True if the path ends there; p.c is then
+// its final colour.  The sorted pipeline takes these exits one launch early (k_sort_produce).
+template <class MT>
+__device__ __forceinline__ bool shade_ends(const Hit& h, const MT* mats, PathReg& p) {
+    if (h.t <= 0.0f) { p.c = F3(0, 0, 0); return true; }
+    const MT& m = mats[h.mat];
+    if (m.emittance > 0.0f) {
+        p.c = hadamard(p.c, F3(m.color[0], m.color[1], m.color[2]) * m.emittance);
+        return true;
+    }
+    return false;
+}
+
 // Returns true if the path survives.  `idx` is the path's position in the (compacted, possibly
 // material-sorted) array — the RNG key of the reference (pathtrace.cu:315).
 template <class MT>
 // `frames`: the staged tangent frames of the scene's cubes (LDS, [geom * 6 + code][6]) or null.
 __device__ __forceinline__ bool shade(const SceneDev& S, const FlagsDev& fl, int depth, int iter, int idx,
                                       PathReg& p, const Hit& h, const MT* mats, const float* frames = nullptr) {
-    if (h.t <= 0.0f) { p.c = F3(0, 0, 0); return false; }
+    if (shade_ends(h, mats, p)) return false;
     int remaining = depth - p.bounces;
     Rng rng(iter, idx, remaining);
     const MT& m = mats[h.mat];
     const f3 mcol = F3(m.color[0], m.color[1], m.color[2]);
-    if (m.emittance > 0.0f) {
-        p.c = hadamard(p.c, mcol * m.emittance);
-        return false;
-    }
     const f3 hitp = point_on_ray(p.o, p.d, h.t);
     const f3 n = h.n;
     p.o = hitp + 0.0001f * n;
@@ -1069,6 +1079,22 @@ __device__ __forceinline__ void flush_emissive(const KArgs& A, uint32_t cnt, uin
     if (threadIdx.x == 0 && *s_cnt) {
         unsigned long long* slot = A.emit_slots + (size_t)A.bounce * A.emit_stride + blockIdx.x;
         *slot += *s_cnt;
+    }
+}
+
+// Two counters: emissions of this launch's bounce and of bounce `b2` (the sorted producer retires
+// the emissive hits of the next bounce, k_sort_produce).
+__device__ __forceinline__ void flush_emissive2(const KArgs& A, uint32_t cnt, int b2, uint32_t cnt2, uint32_t* s_cnt) {
+    if (threadIdx.x == 0) { s_cnt[0] = 0u; s_cnt[1] = 0u; }
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) {
+        if (cnt) atomicAdd(&s_cnt[0], cnt);
+        if (cnt2) atomicAdd(&s_cnt[1], cnt2);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (s_cnt[0]) A.emit_slots[(size_t)A.bounce * A.emit_stride + blockIdx.x] += s_cnt[0];
+        if (s_cnt[1]) A.emit_slots[(size_t)b2 * A.emit_stride + blockIdx.x] += s_cnt[1];
     }
 }
 
@@ -2166,6 +2192,7 @@ struct SortArgs {
     int32_t* perm;      // [P] sorted position -> physical slot
     int32_t* itb;       // [2][kMaxSpp + 1] per parity: first tile of each iteration ([spp] = tiles)
     float* uv_out;      // textured scenes: (u, v) of the output records ([2 * cap])
+    uint32_t* dead;     // one bit per output slot: the path ended in this launch (no record; 8 words per tile)
 };
 constexpr int kSortMaxMats = 256;  // per-tile material counts in LDS (one thread per material)
 
@@ -2208,9 +2235,10 @@ __global__ __launch_bounds__(kBlock, MESH ? 1 : PT_PRODUCE_WAVES) void k_sort_pr
     __shared__ uint32_t s_tmp[8];
     __shared__ uint32_t s_mw[4];
     __shared__ uint32_t s_base[kSortMaxMats];  // the tile's exclusive prefix over materials
+    __shared__ uint32_t s_dead[2][kBlock / 32];   // per tile (two in flight): SA.dead's words
     extern __shared__ uint32_t s_kc[];   // [2][4][nmats] (dynamic): per wave, survivors of each material in the tile
 #define KC(buf, w, m) s_kc[((buf) * 4 + (w)) * nmats + (m)]
-    __shared__ uint32_t s_cnt;
+    __shared__ uint32_t s_cnt[2];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int par = A.parity;
     const int spp = A.tile.spp;
@@ -2246,10 +2274,11 @@ __global__ __launch_bounds__(kBlock, MESH ? 1 : PT_PRODUCE_WAVES) void k_sort_pr
     }
     if ((int)blockIdx.x >= T) return;
     if (!MESH) stage_geoms(A.S, s_geoms);
-    stage_materials(A, s_mats);
+    if (tid < 2 * (kBlock / 32)) s_dead[tid / (kBlock / 32)][tid % (kBlock / 32)] = 0u;
+    stage_materials(A, s_mats);   // (its barrier also orders s_dead's clearing)
     const bool lds_mats = nmats <= kLdsMats;
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    uint32_t emit_cnt = 0;
+    uint32_t emit_cnt = 0, emit_next = 0;
     int k = 0;
     for (int t = (int)blockIdx.x; t < T; t += (int)gridDim.x, ++k) {
         const int it = tile_iteration(s_tb, spp, t);
@@ -2261,11 +2290,11 @@ __global__ __launch_bounds__(kBlock, MESH ? 1 : PT_PRODUCE_WAVES) void k_sort_pr
         PathReg p;
         Hit h;
         if (idx < s_sb[it + 1]) {
+            const int j = FIRST ? 0 : SA.perm[idx];   // j < 0: the path ended in the previous launch
             if (FIRST) {
                 raygen(A.cam, A.fl, A.tile, idx, p);
                 alive = true;
-            } else {
-                const int j = SA.perm[idx];
+            } else if (j >= 0) {
                 const v4f* r = srec(A.in, j);
                 // (plain loads: a gather of 64-byte records whose four 16-byte pieces share a line)
                 const v4f r0 = r[0], r1 = r[1], r2 = r[2], r3 = r[3];
@@ -2322,6 +2351,10 @@ __global__ __launch_bounds__(kBlock, MESH ? 1 : PT_PRODUCE_WAVES) void k_sort_pr
             rem &= ~mk;
         }
         __syncthreads();
+        if (k > 0 && tid < kBlock / 32) {   // the previous tile's SA.dead words (its ORs are behind the barrier)
+            SA.dead[(size_t)(t - (int)gridDim.x) * (kBlock / 32) + tid] = s_dead[(k - 1) & 1][tid];
+            s_dead[(k - 1) & 1][tid] = 0u;   // (next written two tiles on, after this tile's second barrier)
+        }
         {   // material mm = tid: the tile's count and its run's first slot (exclusive prefix over the
             // materials); the histogram entries of the tile
             const int mm = tid;
@@ -2336,24 +2369,42 @@ __global__ __launch_bounds__(kBlock, MESH ? 1 : PT_PRODUCE_WAVES) void k_sort_pr
             }
         }
         __syncthreads();
+        bool em_next = false;
         if (alive) {
             uint32_t kb = krank;
             for (int w = 0; w < wave; ++w) kb += KC(k & 1, w, key);
             const int q = t * kBlock + (int)(s_base[key] + kb);
-            v4f* r = srec(A.out, q);
-            // (plain stores: each store instruction covers 16 of every 64 bytes, and L2 merges the
-            // four into whole lines; non-temporal ones halved config 3's rate)
-            r[0] = v4f{p.o.x, p.o.y, p.o.z, p.d.x};
-            r[1] = v4f{p.d.y, p.d.z, p.c.x, p.c.y};
-            r[2] = v4f{p.c.z, __int_as_float(p.slot), h.t, __int_as_float(key)};
-            r[3] = v4f{h.n.x, h.n.y, h.n.z, 0.0f};
-            if (A.S.texs) {
-                SA.uv_out[2 * (size_t)q] = h.u;
-                SA.uv_out[2 * (size_t)q + 1] = h.v;
+            // A path whose new ray misses or meets an emitter ends at the next shade without drawing
+            // a random number (shade_ends): it keeps its sorted position (the next launch's RNG keys
+            // count it), but ends here — retired with the colour that shade would give it, its slot
+            // flagged in SA.dead (k_hist_apply marks its perm entry), and no record written or read.
+            PathReg e = p;
+            const bool ends = lds_mats ? shade_ends(h, s_mats, e) : shade_ends(h, A.S.mats, e);
+            if (ends) {
+                atomicOr(&s_dead[k & 1][(q - t * kBlock) >> 5], 1u << (q & 31));
+                em_next = e.c.x != 0.0f || e.c.y != 0.0f || e.c.z != 0.0f;
+                retire<SPP1>(A, e);
+            } else {
+                v4f* r = srec(A.out, q);
+                // (plain stores: each store instruction covers 16 of every 64 bytes, and L2 merges the
+                // four into whole lines; non-temporal ones halved config 3's rate)
+                r[0] = v4f{p.o.x, p.o.y, p.o.z, p.d.x};
+                r[1] = v4f{p.d.y, p.d.z, p.c.x, p.c.y};
+                r[2] = v4f{p.c.z, __int_as_float(p.slot), h.t, __int_as_float(key)};
+                r[3] = v4f{h.n.x, h.n.y, h.n.z, 0.0f};
+                if (A.S.texs) {
+                    SA.uv_out[2 * (size_t)q] = h.u;
+                    SA.uv_out[2 * (size_t)q + 1] = h.v;
+                }
             }
         }
+        emit_next += (uint32_t)__popcll(__ballot(em_next));
     }
-    flush_emissive(A, emit_cnt, &s_cnt);
+    __syncthreads();   // the last tile's SA.dead words
+    if (k > 0 && tid < kBlock / 32)
+        SA.dead[(size_t)((int)blockIdx.x + (k - 1) * (int)gridDim.x) * (kBlock / 32) + tid] = s_dead[(k - 1) & 1][tid];
+    // (the camera rays' ends are bounce 0's; a later producer's are the next bounce's)
+    flush_emissive2(A, emit_cnt, FIRST ? A.bounce : A.bounce + 1, emit_next, s_cnt);
 #undef KC
 }
 
@@ -2418,7 +2469,8 @@ __global__ __launch_bounds__(kBlock) void k_hist_scan_sums(uint32_t* __restrict_
 // the live entries but the last (the end offset, whose count is not written).
 __global__ __launch_bounds__(kBlock) void k_hist_apply(const int32_t* __restrict__ in, int32_t* __restrict__ out,
                                                        int64_t n, const uint32_t* nlive, const uint32_t* __restrict__ sums,
-                                                       const int32_t* __restrict__ hslot, int32_t* __restrict__ perm) {
+                                                       const int32_t* __restrict__ hslot, int32_t* __restrict__ perm,
+                                                       const uint32_t* __restrict__ dead) {
     __shared__ uint32_t s_w[4];
     n = hist_n(n, nlive);
     const int64_t base = (int64_t)blockIdx.x * kHistTile + (int64_t)threadIdx.x * kHistPer;
@@ -2429,18 +2481,40 @@ __global__ __launch_bounds__(kBlock) void k_hist_apply(const int32_t* __restrict
     uint32_t total;
     uint32_t run = block_excl_scan(v, s_w, &total) + sums[blockIdx.x];
     if (perm) {   // the wave writes its entries' runs one after the other, 64 consecutive slots per store
+        // Each live entry's tile's 8 SA.dead words go to LDS first (all loads in flight at once),
+        // so the stores below do not wait on a load per run.
+        __shared__ uint32_t s_dm[kHistTile * (kBlock / 32)];
         const int lane = (int)threadIdx.x & 63;
+        int32_t s0[kHistPer];
+#pragma unroll
+        for (int k = 0; k < kHistPer; ++k) {
+            const bool live = base + k < n - 1 && x[k] != 0u;
+            s0[k] = live ? hslot[base + k] : 0;
+        }
+#pragma unroll
+        for (int k = 0; k < kHistPer; ++k) {
+            if (base + k < n - 1 && x[k] != 0u) {
+                const v4i_h* d = reinterpret_cast<const v4i_h*>(dead + (size_t)((uint32_t)s0[k] >> 8) * (kBlock / 32));
+                v4i_h* l = reinterpret_cast<v4i_h*>(s_dm + ((int)threadIdx.x * kHistPer + k) * (kBlock / 32));
+                l[0] = d[0];
+                l[1] = d[1];
+            }
+        }
+        wave_sync();   // (each wave reads only its own entries' rows)
         uint32_t o = run;
 #pragma unroll
         for (int k = 0; k < kHistPer; ++k) {
             const bool live = base + k < n - 1 && x[k] != 0u;
-            const int32_t s0 = live ? hslot[base + k] : 0;
             uint64_t rem = __ballot(live);
             while (rem) {
                 const int src = __builtin_ctzll(rem);
                 const uint32_t ro = __builtin_amdgcn_readlane(o, src), rc = __builtin_amdgcn_readlane(x[k], src);
-                const int32_t rs = __builtin_amdgcn_readlane(s0, src);
-                for (uint32_t r = (uint32_t)lane; r < rc; r += 64) perm[ro + r] = rs + (int32_t)r;
+                const uint32_t rs = (uint32_t)__builtin_amdgcn_readlane(s0[k], src);
+                const uint32_t* dm = s_dm + (((int)threadIdx.x & ~63) + src) * kHistPer * (kBlock / 32) + k * (kBlock / 32);
+                for (uint32_t r = (uint32_t)lane; r < rc; r += 64) {   // (slots whose path ended: sign bit set)
+                    const uint32_t b = (rs & (kBlock - 1)) + r;   // (a run lies inside its tile's 256 slots)
+                    perm[ro + r] = (int32_t)((rs + r) | (((dm[b >> 5] >> (b & 31)) & 1u) << 31));
+                }
                 rem &= rem - 1;
             }
             o += x[k];
@@ -2589,6 +2663,7 @@ struct pt_ctx {
     hipEvent_t ev_fork = nullptr, ev_join[kMaxLanes] = {};
     struct SortSet {   // material-sort buffers of one lane (k_sort_produce / k_hist_*)
         int32_t *hslot = nullptr, *hist = nullptr, *offs = nullptr, *perm = nullptr, *itb = nullptr;
+        uint32_t* dead = nullptr;   // (k_sort_produce -> k_hist_apply: slots whose path ended)
         float* uv[2] = {nullptr, nullptr};   // (u, v) of the records in buf[0] / buf[1]
         uint32_t* sums = nullptr;            // histogram scan: tile sums
         int64_t hist_cap = 0;                // histogram entries allocated (+ the end offset)
@@ -3597,6 +3672,7 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
         const size_t tiles = ((size_t)ss.hist_cap + kHistTile - 1) / kHistTile;
         if (int rc = c->alloc(&ss.hslot, (size_t)ss.hist_cap)) return bail(rc);
         if (int rc = c->alloc(&ss.perm, paths)) return bail(rc);
+        if (int rc = c->alloc(&ss.dead, (cap / kBlock + 2) * (kBlock / 32))) return bail(rc);
         if (int rc = c->alloc(&ss.hist, (size_t)ss.hist_cap)) return bail(rc);
         if (int rc = c->alloc(&ss.offs, (size_t)ss.hist_cap)) return bail(rc);
         if (int rc = c->alloc(&ss.itb, 2 * ((size_t)kMaxSpp + 1))) return bail(rc);
@@ -3661,7 +3737,7 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
             a.in = bufs[lcur];
             a.out = bufs[lcur ^ 1];
             a.hit.uv = ss.uv[lcur];
-            const SortArgs sa{ss.hslot, ss.hist, ss.offs, ss.perm, ss.itb, ss.uv[lcur ^ 1]};
+            const SortArgs sa{ss.hslot, ss.hist, ss.offs, ss.perm, ss.itb, ss.uv[lcur ^ 1], ss.dead};
             hipLaunchKernelGGL(produce_kernel(first, spp1, mesh), dim3(c->grid_bounce[0]), dim3(kBlock),
                                (size_t)8 * c->nmats * sizeof(uint32_t), s, a, sa);
             HIP_TRY(hipGetLastError());
@@ -3681,7 +3757,7 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
         hipLaunchKernelGGL(k_hist_sums, dim3(tiles), dim3(kBlock), 0, s, (const int32_t*)ss.hist, ss.hist_cap, nlive, ss.sums);
         hipLaunchKernelGGL(k_hist_scan_sums, dim3(1), dim3(kBlock), 0, s, ss.sums, ss.hist_cap, nlive);
         hipLaunchKernelGGL(k_hist_apply, dim3(tiles), dim3(kBlock), 0, s, (const int32_t*)ss.hist, ss.offs, ss.hist_cap,
-                           nlive, (const uint32_t*)ss.sums, (const int32_t*)ss.hslot, ss.perm);
+                           nlive, (const uint32_t*)ss.sums, (const int32_t*)ss.hslot, ss.perm, (const uint32_t*)ss.dead);
         HIP_TRY(hipGetLastError());
         if (int rc = produce(false)) return rc;
         return prof_end(ev, s);

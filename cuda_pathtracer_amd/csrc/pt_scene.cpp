@@ -4,6 +4,7 @@
 // BVH_tree.cpp.  Matrix and camera arithmetic follow glm 0.9.6.3's association so the GPU
 // renders from exactly the numbers the reference host would have produced.
 #include <cfloat>
+#include <chrono>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -345,7 +346,20 @@ int scene_finalize(Scene& S) {
         if (g.material_id < 0 || g.material_id >= (int)S.materials.size())
             return fail(PT_ERR_ARG, "geom references a missing material");
     finalize_camera(S);
-    const int rc = build_bvh(S);
+    // BVH (scene.cpp:218 -> BVH_tree.cpp:156): the host restatement, or the same tree built on the
+    // current HIP device (falls back to the host for the cases bvh_build.hip leaves to it)
+    S.bvh_on_device = 0;
+    int rc = 1;
+    if (S.bvh_builder == 1) {
+        rc = build_bvh_device(S, &S.bvh_ms);
+        if (rc == PT_OK) S.bvh_on_device = 1;
+        else if (rc != 1) return rc;
+    }
+    if (rc == 1) {
+        const auto t0 = std::chrono::steady_clock::now();
+        rc = build_bvh(S);
+        S.bvh_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
     if (rc) return rc;
     S.finalized = true;
     return PT_OK;
@@ -389,12 +403,28 @@ int pt_scene_load_json(const char* path, pt_scene** out) { return pt_scene_load_
 
 int pt_scene_load_json_ex(const char* path, uint32_t options, pt_scene** out) {
     if (!path || !out) return fail(PT_ERR_ARG, "null argument");
-    if (options & ~(uint32_t)PT_LOAD_REFRACTION) return fail(PT_ERR_ARG, "unknown PT_LOAD_* option");
+    if (options & ~(uint32_t)(PT_LOAD_REFRACTION | PT_LOAD_DEVICE_BVH)) return fail(PT_ERR_ARG, "unknown PT_LOAD_* option");
     auto* S = new pt::Scene();
+    S->bvh_builder = (options & PT_LOAD_DEVICE_BVH) ? 1 : 0;
     int rc = pt::load_json(*S, path, options);
     if (!rc) rc = pt::scene_finalize(*S);
     if (rc) { delete S; return rc; }
     *out = reinterpret_cast<pt_scene*>(S);
+    return PT_OK;
+}
+
+int pt_scene_set_bvh_builder(pt_scene* s, int32_t device) {
+    if (!s || (device != 0 && device != 1)) return fail(PT_ERR_ARG, "bad argument");
+    auto& S = *reinterpret_cast<pt::Scene*>(s);
+    S.bvh_builder = device;
+    return PT_OK;
+}
+
+int pt_scene_bvh_build_info(const pt_scene* s, int32_t* on_device, double* ms) {
+    if (!s) return fail(PT_ERR_ARG, "null scene");
+    const auto& S = *reinterpret_cast<const pt::Scene*>(s);
+    if (on_device) *on_device = S.bvh_on_device;
+    if (ms) *ms = S.bvh_ms;
     return PT_OK;
 }
 

@@ -93,14 +93,29 @@ class Scene:
     reference loader ignores (PT_LOAD_REFRACTION; a file may also opt in with
     "Extensions": {"REFRACTION": true}); by default they are ignored, like scene.cpp:46-56."""
 
-    def __init__(self, filename: str | os.PathLike | None = None, refraction: bool = False):
+    def __init__(self, filename: str | os.PathLike | None = None, refraction: bool = False,
+                 device_bvh: bool = False):
+        """device_bvh=True builds the BVH on the current HIP device (pt_scene_set_bvh_builder: the
+        same tree as the host build, byte for byte)."""
         self._h = C.c_void_p()
         L = lib()
         if filename is None:
             check_pt(L.pt_scene_create(C.byref(self._h)))
+            if device_bvh:
+                check_pt(L.pt_scene_set_bvh_builder(self._h, 1))
             return
-        check_pt(L.pt_scene_load_json_ex(str(filename).encode(), 1 if refraction else 0, C.byref(self._h)))
+        opts = (1 if refraction else 0) | (2 if device_bvh else 0)
+        check_pt(L.pt_scene_load_json_ex(str(filename).encode(), opts, C.byref(self._h)))
         self._fill_non_jpeg_textures()
+
+    def set_bvh_builder(self, device: bool) -> None:
+        check_pt(lib().pt_scene_set_bvh_builder(self._h, 1 if device else 0))
+
+    def bvh_build_info(self) -> tuple[bool, float]:
+        """(the last BVH build ran on the device, its wall time in ms)."""
+        d, ms = C.c_int32(), C.c_double()
+        check_pt(lib().pt_scene_bvh_build_info(self._h, C.byref(d), C.byref(ms)))
+        return bool(d.value), float(ms.value)
 
     def texture_path(self, tid: int) -> str:
         buf = C.create_string_buffer(4096)

@@ -160,6 +160,8 @@ int pt_scene_load_json(const char* path, pt_scene** out);   /* Scene::Scene(file
  * file can also opt in itself with the top-level key "Extensions": {"REFRACTION": true}, which the
  * reference ignores; a reference scene file therefore loads exactly as the reference loads it. */
 #define PT_LOAD_REFRACTION 1u
+/* PT_LOAD_DEVICE_BVH: build the scene's BVH on the current HIP device (pt_scene_set_bvh_builder). */
+#define PT_LOAD_DEVICE_BVH 2u
 int pt_scene_load_json_ex(const char* path, uint32_t options, pt_scene** out);
 int pt_scene_create(pt_scene** out);
 void pt_scene_free(pt_scene* s);
@@ -193,6 +195,12 @@ int pt_scene_set_camera(pt_scene* s, int32_t res_x, int32_t res_y, float fovy, c
 int pt_scene_set_render(pt_scene* s, int32_t iterations, int32_t depth, const char* file);
 /* Camera orbit recompute of the first frame (main.cpp:59-73,117-136) + BVH build (scene.cpp:218). */
 int pt_scene_finalize(pt_scene* s);
+/* Where pt_scene_finalize builds the BVH (BVH_tree.cpp:27-181's SAH tree): 0 (default) on the host,
+ * 1 on the current HIP device — the same nodes, byte for byte, and the same triangle order
+ * (bvh_build.hip); a tree the device builder leaves to the host (NaN vertex coordinates) is built
+ * there.  pt_scene_bvh_build_info: where the last build ran and its wall time in ms. */
+int pt_scene_set_bvh_builder(pt_scene* s, int32_t device);
+int pt_scene_bvh_build_info(const pt_scene* s, int32_t* on_device, double* ms);
 int pt_scene_counts(const pt_scene* s, int32_t* ngeoms, int32_t* nmats, int32_t* ntris,
                     int32_t* nnodes, int32_t* ntex);
 int pt_scene_get_camera(const pt_scene* s, pt_camera* out);

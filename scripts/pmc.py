@@ -80,6 +80,9 @@ def collect(workload: list[str], out_dir: Path, timeout: int = 120, groups=("fet
         for line in (out_dir / f"{g}.log").read_text().splitlines():   # prof_render.py: segments [live...]
             if line[:1].isdigit():
                 res["segments"] = int(line.split()[0])
+                if "[" in line:
+                    import ast
+                    res["bounce_live"] = ast.literal_eval(line[line.index("["):])
         vals, dur = _load(d)
         for k, cs in vals.items():
             for c, v in cs.items():
