@@ -927,18 +927,24 @@ __device__ __forceinline__ bool shade_ends(const Hit& h, const MT* mats, PathReg
     return false;
 }
 
-// Returns true if the path survives.  `idx` is the path's position in the (compacted, possibly
-// material-sorted) array — the RNG key of the reference (pathtrace.cu:315).
+// Does shade() read the incoming direction for this material (a refractive one, or one that may
+// reflect: `rng.u01() < has_reflective` can hold)?  A diffuse bounce only needs the normal.
 template <class MT>
+__device__ __forceinline__ bool mat_needs_dir(const MT& m) {
+    return m.has_refractive != 0.0f || m.has_reflective > 0.0f;
+}
+
+// shade() past its two early exits, from the hit point (getPointOnRay, pathtrace.cu:323): the
+// material-sorted pipeline stores the hit point instead of the ray's origin and length.
 // `frames`: the staged tangent frames of the scene's cubes (LDS, [geom * 6 + code][6]) or null.
-__device__ __forceinline__ bool shade(const SceneDev& S, const FlagsDev& fl, int depth, int iter, int idx,
-                                      PathReg& p, const Hit& h, const MT* mats, const float* frames = nullptr) {
-    if (shade_ends(h, mats, p)) return false;
+template <class MT>
+__device__ __forceinline__ bool shade_from(const SceneDev& S, const FlagsDev& fl, int depth, int iter, int idx,
+                                           PathReg& p, const Hit& h, f3 hitp, const MT* mats,
+                                           const float* frames = nullptr) {
     int remaining = depth - p.bounces;
     Rng rng(iter, idx, remaining);
     const MT& m = mats[h.mat];
     const f3 mcol = F3(m.color[0], m.color[1], m.color[2]);
-    const f3 hitp = point_on_ray(p.o, p.d, h.t);
     const f3 n = h.n;
     p.o = hitp + 0.0001f * n;
     const f3 alb = m.texture_id != -1 ? tex_color(S.texs[m.texture_id], h.u, h.v) : mcol;
@@ -974,6 +980,15 @@ __device__ __forceinline__ bool shade(const SceneDev& S, const FlagsDev& fl, int
         p.c = cq;
     }
     return true;
+}
+
+// Returns true if the path survives.  `idx` is the path's position in the (compacted, possibly
+// material-sorted) array — the RNG key of the reference (pathtrace.cu:315).
+template <class MT>
+__device__ __forceinline__ bool shade(const SceneDev& S, const FlagsDev& fl, int depth, int iter, int idx,
+                                      PathReg& p, const Hit& h, const MT* mats, const float* frames = nullptr) {
+    if (shade_ends(h, mats, p)) return false;
+    return shade_from(S, fl, depth, iter, idx, p, h, point_on_ray(p.o, p.d, h.t), mats, frames);
 }
 
 // generateRayFromCamera (pathtrace.cu:183-227) for tile slot `slot`.
@@ -2179,17 +2194,25 @@ __global__ __launch_bounds__(kBlock) void k_compact_paths(const KArgs A) {
 // Batched passes sort every iteration on its own (stable sort by (iteration, material), as `spp`
 // sequential pathtrace() calls would): tiles never span two iterations, and an iteration's tiles
 // form one block of the histogram.
-// Path j of the sorted pipeline is ONE 64-byte record, so the gather reads one 64-byte span:
-//   r0 = (o.xyz, d.x)   r1 = (d.yz, c.rg)   r2 = (c.b, slot, t, material)   r3 = (n.xyz, 0)
-// `bounces` is not stored: every path entering bounce b has b bounces behind it.  Texture
-// coordinates (textured scenes only) go to a side array, double-buffered like the records.
-__device__ __forceinline__ v4f* srec(const PathSoA& B, int j) { return B.a + ((size_t)(uint32_t)j << 2); }
+// Path j of the sorted pipeline is ONE 48-byte record (only paths that go on to be shaded have one:
+// a miss or an emitter ends in the producer), so the gather reads one 48-byte span:
+//   r0 = (hit point.xyz, c.r)   r1 = (c.gb, slot, material)   r2 = (n.xyz, 0)
+// The hit point (getPointOnRay, as shade computes it) replaces the ray's origin and length; the
+// ray's direction, which only a refractive or possibly reflective material reads (mat_needs_dir),
+// goes to a side plane (the block's fourth) for those paths alone.  `bounces` is not stored: every
+// path entering bounce b has b bounces behind it.  Texture coordinates (textured scenes only) go to
+// a side array, double-buffered like the records.
+__device__ __forceinline__ v4f* srec(const PathSoA& B, int j) { return B.a + 3 * (size_t)(uint32_t)j; }
+__device__ __forceinline__ v4f* sdir(const PathSoA& B, int j) { return B.c + (B.b - B.a) + (size_t)(uint32_t)j; }
 
 struct SortArgs {
     int32_t* hslot;     // per (iteration, material, tile): first slot of its run (sort_hidx)
     int32_t* hist;      // per (iteration, material, tile) survivor counts (sort_hidx)
-    int32_t* offs;      // its exclusive scan
-    int32_t* perm;      // [P] sorted position -> physical slot
+    int32_t* offs;      // its exclusive scan: sorted positions (RNG keys)
+    int32_t* hist2;     // per entry: survivors that did not end in the producer (records to shade)
+    int32_t* offs2;     // its exclusive scan: the next producer's work positions
+    int32_t* perm;      // [P] work position -> physical slot
+    int32_t* fpos;      // [P] work position -> sorted position
     int32_t* itb;       // [2][kMaxSpp + 1] per parity: first tile of each iteration ([spp] = tiles)
     float* uv_out;      // textured scenes: (u, v) of the output records ([2 * cap])
     uint32_t* dead;     // one bit per output slot: the path ended in this launch (no record; 8 words per tile)
@@ -2226,28 +2249,37 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_w, u
 #define PT_PRODUCE_WAVES 7   // (A/B knob: minimum waves per SIMD of the analytic producer; 7 caps the
                              // first bounce's producer at 72 VGPRs: config 3 +0.8% on the same box)
 #endif
+#ifndef PT_PRODUCE_WAVES_FIRST
+#define PT_PRODUCE_WAVES_FIRST PT_PRODUCE_WAVES
+#endif
 template <bool FIRST, bool SPP1, bool MESH>
-__global__ __launch_bounds__(kBlock, MESH ? 1 : PT_PRODUCE_WAVES) void k_sort_produce(const KArgs A, const SortArgs SA) {
+__global__ __launch_bounds__(kBlock, MESH ? 1 : (FIRST ? PT_PRODUCE_WAVES_FIRST : PT_PRODUCE_WAVES))
+void k_sort_produce(const KArgs A, const SortArgs SA) {
     __shared__ DMaterial s_mats[kLdsMats];
     __shared__ LGeom s_geoms[MESH ? 1 : kLdsGeoms];
-    __shared__ int32_t s_sb[kMaxSpp + 1];      // sorted start of every iteration (first bounce: j * npix)
+    __shared__ int32_t s_sb[kMaxSpp + 1];      // work start of every iteration (first bounce: j * npix)
+    __shared__ int32_t s_fb[kMaxSpp + 1];      // sorted start of every iteration (RNG key base)
     __shared__ int32_t s_tb[kMaxSpp + 1];      // first tile of every iteration ([spp] = all tiles)
     __shared__ uint32_t s_tmp[8];
     __shared__ uint32_t s_mw[4];
     __shared__ uint32_t s_base[kSortMaxMats];  // the tile's exclusive prefix over materials
     __shared__ uint32_t s_dead[2][kBlock / 32];   // per tile (two in flight): SA.dead's words
-    extern __shared__ uint32_t s_kc[];   // [2][4][nmats] (dynamic): per wave, survivors of each material in the tile
+    extern __shared__ uint32_t s_kc[];   // [2][2][4][nmats] (dynamic): per wave, survivors of each material in the tile
 #define KC(buf, w, m) s_kc[((buf) * 4 + (w)) * nmats + (m)]
+#define KL(buf, w, m) s_kc[(8 + (buf) * 4 + (w)) * nmats + (m)]   // (those that did not end here)
     __shared__ uint32_t s_cnt[2];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int par = A.parity;
     const int spp = A.tile.spp;
     const int nmats = A.S.nmats;
     if (FIRST) {
-        for (int j = tid; j <= spp; j += kBlock) s_sb[j] = j * A.tile.npix;
-    } else {   // the scanned histogram at each iteration's first entry (the previous producer's tiles)
+        for (int j = tid; j <= spp; j += kBlock) s_sb[j] = s_fb[j] = j * A.tile.npix;
+    } else {   // the scanned histograms at each iteration's first entry (the previous producer's tiles)
         const int32_t* tb_in = SA.itb + (size_t)par * (kMaxSpp + 1);
-        for (int j = tid; j <= spp; j += kBlock) s_sb[j] = SA.offs[(size_t)tb_in[j] * nmats];
+        for (int j = tid; j <= spp; j += kBlock) {
+            s_sb[j] = SA.offs2[(size_t)tb_in[j] * nmats];
+            s_fb[j] = SA.offs[(size_t)tb_in[j] * nmats];
+        }
     }
     __syncthreads();
     {   // this launch's tiles: iteration it owns ceil(n_it / 256) of them, from s_tb[it]
@@ -2270,7 +2302,7 @@ __global__ __launch_bounds__(kBlock, MESH ? 1 : PT_PRODUCE_WAVES) void k_sort_pr
         }
         int32_t* tb_out = SA.itb + (size_t)(par ^ 1) * (kMaxSpp + 1);
         for (int j = tid; j <= spp; j += kBlock) tb_out[j] = s_tb[j];
-        if (!FIRST) count_bounce(A, s_sb[spp]);   // the live paths of bounce b, shaded here
+        if (!FIRST) count_bounce(A, s_fb[spp]);   // the live paths of bounce b (with those that ended early)
     }
     if ((int)blockIdx.x >= T) return;
     if (!MESH) stage_geoms(A.S, s_geoms);
@@ -2284,40 +2316,45 @@ __global__ __launch_bounds__(kBlock, MESH ? 1 : PT_PRODUCE_WAVES) void k_sort_pr
         const int it = tile_iteration(s_tb, spp, t);
         const int t0 = s_tb[it], t1 = s_tb[it + 1];
         const int it_base = s_sb[it];
-        const int idx = it_base + (t - t0) * kBlock + tid;   // sorted position
+        const int idx = it_base + (t - t0) * kBlock + tid;   // work position
         const int iter = A.tile.iter_first + it;
         bool alive = false, emitted = false;
         PathReg p;
         Hit h;
+        bool ends = false;
         if (idx < s_sb[it + 1]) {
-            const int j = FIRST ? 0 : SA.perm[idx];   // j < 0: the path ended in the previous launch
             if (FIRST) {
                 raygen(A.cam, A.fl, A.tile, idx, p);
                 alive = true;
-            } else if (j >= 0) {
+            } else {
+                const int j = SA.perm[idx];
                 const v4f* r = srec(A.in, j);
-                // (plain loads: a gather of 64-byte records whose four 16-byte pieces share a line)
-                const v4f r0 = r[0], r1 = r[1], r2 = r[2], r3 = r[3];
-                p.o = F3(r0[0], r0[1], r0[2]);
-                p.d = F3(r0[3], r1[0], r1[1]);
-                p.c = F3(r1[2], r1[3], r2[0]);
-                p.slot = __float_as_int(r2[1]);
+                // (plain loads: a gather of 48-byte records whose 16-byte pieces share lines)
+                const v4f r0 = r[0], r1 = r[1], r2 = r[2];
+                const f3 hitp = F3(r0[0], r0[1], r0[2]);
+                p.c = F3(r0[3], r1[0], r1[1]);
+                p.slot = __float_as_int(r1[2]);
                 p.bounces = A.bounce;
-                h.t = r2[2];
-                h.mat = __float_as_int(r2[3]);
-                h.n = F3(r3[0], r3[1], r3[2]);
+                h.mat = __float_as_int(r1[3]);
+                h.n = F3(r2[0], r2[1], r2[2]);
                 h.u = h.v = 0.0f;
-                if (A.S.texs && h.t > 0.0f) {
+                p.d = F3(0, 0, 0);
+                if (lds_mats ? mat_needs_dir(s_mats[h.mat]) : mat_needs_dir(A.S.mats[h.mat])) {
+                    const v4f d = sdir(A.in, j)[0];
+                    p.d = F3(d[0], d[1], d[2]);
+                }
+                if (A.S.texs) {
                     const bool tex = lds_mats ? s_mats[h.mat].texture_id != -1 : A.S.mats[h.mat].texture_id != -1;
                     if (tex) {
                         h.u = A.hit.uv[2 * (size_t)j];
                         h.v = A.hit.uv[2 * (size_t)j + 1];
                     }
                 }
-                // key: sorted index within the path's own iteration
-                const int key = A.fl.rng_pixel ? slot_pixel(A.cam, A.tile, p.slot) : idx - it_base;
-                alive = lds_mats ? shade(A.S, A.fl, A.tile.depth, iter, key, p, h, s_mats)
-                                 : shade(A.S, A.fl, A.tile.depth, iter, key, p, h, A.S.mats);
+                // key: sorted index within the path's own iteration (paths that ended in the
+                // previous launch hold positions too: fpos)
+                const int key = A.fl.rng_pixel ? slot_pixel(A.cam, A.tile, p.slot) : SA.fpos[idx] - s_fb[it];
+                alive = lds_mats ? shade_from(A.S, A.fl, A.tile.depth, iter, key, p, h, hitp, s_mats)
+                                 : shade_from(A.S, A.fl, A.tile.depth, iter, key, p, h, hitp, A.S.mats);
                 if (!alive) {
                     emitted = p.c.x != 0.0f || p.c.y != 0.0f || p.c.z != 0.0f;
                     retire<SPP1>(A, p);
@@ -2328,18 +2365,22 @@ __global__ __launch_bounds__(kBlock, MESH ? 1 : PT_PRODUCE_WAVES) void k_sort_pr
                 const int lp0 = __builtin_amdgcn_readfirstlane(idx - it_base);
                 gm = A.cmask[lp0 >> 6];
             }
-            if (alive) h = closest_hit<MESH, true, !FIRST>(A.S, A.fl, s_geoms, p.o, p.d, &A.stats->bound_mismatch, gm);
+            if (alive) {
+                h = closest_hit<MESH, true, !FIRST>(A.S, A.fl, s_geoms, p.o, p.d, &A.stats->bound_mismatch, gm);
+                PathReg e = p;   // (only the verdict here; the colour below)
+                ends = lds_mats ? shade_ends(h, s_mats, e) : shade_ends(h, A.S.mats, e);
+            }
         }
         const int key = alive ? (h.t == -1.0f ? 0 : h.mat) : -1;   // misses keep materialId 0 (pathtrace.cu:466)
         emit_cnt += (uint32_t)__popcll(__ballot(emitted));
-        const uint64_t m = __ballot(alive);
+        const uint64_t m = __ballot(alive), me = __ballot(ends);
         // this wave's row of per-material counts: cleared, then one ballot per material present ->
         // in-wave rank (lanes of that key) and the count (written by the first lane of the key).
         // Buffer k&1 was last read two tiles ago, before the previous barrier; a wave's LDS
         // writes land in order.
 #pragma unroll
         for (int q = 0; q < kSortMaxMats / 64; ++q)   // (fixed trip count: a dynamic loop here cost 34 VGPRs)
-            if (lane + 64 * q < nmats) KC(k & 1, wave, lane + 64 * q) = 0u;
+            if (lane + 64 * q < nmats) KC(k & 1, wave, lane + 64 * q) = KL(k & 1, wave, lane + 64 * q) = 0u;
         uint32_t krank = 0;
         uint64_t rem = m;
         while (rem) {
@@ -2347,7 +2388,10 @@ __global__ __launch_bounds__(kBlock, MESH ? 1 : PT_PRODUCE_WAVES) void k_sort_pr
             const int kk = __builtin_amdgcn_readlane(key, src);
             const uint64_t mk = __ballot(key == kk);
             if (key == kk) krank = (uint32_t)__popcll(mk & lt);
-            if (lane == src) KC(k & 1, wave, kk) = (uint32_t)__popcll(mk);
+            if (lane == src) {
+                KC(k & 1, wave, kk) = (uint32_t)__popcll(mk);
+                KL(k & 1, wave, kk) = (uint32_t)__popcll(mk & ~me);
+            }
             rem &= ~mk;
         }
         __syncthreads();
@@ -2365,6 +2409,7 @@ __global__ __launch_bounds__(kBlock, MESH ? 1 : PT_PRODUCE_WAVES) void k_sort_pr
                 s_base[mm] = bm;
                 const size_t e = sort_hidx(t0, t1, nmats, t, mm);
                 SA.hist[e] = (int32_t)cm;
+                SA.hist2[e] = (int32_t)((KL(k & 1, 0, mm) + KL(k & 1, 1, mm)) + (KL(k & 1, 2, mm) + KL(k & 1, 3, mm)));
                 SA.hslot[e] = t * kBlock + (int32_t)bm;
             }
         }
@@ -2375,23 +2420,26 @@ __global__ __launch_bounds__(kBlock, MESH ? 1 : PT_PRODUCE_WAVES) void k_sort_pr
             for (int w = 0; w < wave; ++w) kb += KC(k & 1, w, key);
             const int q = t * kBlock + (int)(s_base[key] + kb);
             // A path whose new ray misses or meets an emitter ends at the next shade without drawing
-            // a random number (shade_ends): it keeps its sorted position (the next launch's RNG keys
-            // count it), but ends here — retired with the colour that shade would give it, its slot
-            // flagged in SA.dead (k_hist_apply marks its perm entry), and no record written or read.
-            PathReg e = p;
-            const bool ends = lds_mats ? shade_ends(h, s_mats, e) : shade_ends(h, A.S.mats, e);
+            // a random number (shade_ends): it keeps its sorted position (hist counts it, so the
+            // next launch's RNG keys do), but ends here — retired with the colour that shade would
+            // give it, its slot flagged in SA.dead, no record written, and no work position in the
+            // next launch (hist2 leaves it out; k_hist_apply skips its slot).
             if (ends) {
+                PathReg e = p;
+                (void)(lds_mats ? shade_ends(h, s_mats, e) : shade_ends(h, A.S.mats, e));
                 atomicOr(&s_dead[k & 1][(q - t * kBlock) >> 5], 1u << (q & 31));
                 em_next = e.c.x != 0.0f || e.c.y != 0.0f || e.c.z != 0.0f;
                 retire<SPP1>(A, e);
             } else {
                 v4f* r = srec(A.out, q);
-                // (plain stores: each store instruction covers 16 of every 64 bytes, and L2 merges the
-                // four into whole lines; non-temporal ones halved config 3's rate)
-                r[0] = v4f{p.o.x, p.o.y, p.o.z, p.d.x};
-                r[1] = v4f{p.d.y, p.d.z, p.c.x, p.c.y};
-                r[2] = v4f{p.c.z, __int_as_float(p.slot), h.t, __int_as_float(key)};
-                r[3] = v4f{h.n.x, h.n.y, h.n.z, 0.0f};
+                // (plain stores: each store instruction covers 16 of every 48 bytes, and L2 merges the
+                // three into whole lines; non-temporal ones halved config 3's rate)
+                const f3 hitp = point_on_ray(p.o, p.d, h.t);
+                r[0] = v4f{hitp.x, hitp.y, hitp.z, p.c.x};
+                r[1] = v4f{p.c.y, p.c.z, __int_as_float(p.slot), __int_as_float(h.mat)};
+                r[2] = v4f{h.n.x, h.n.y, h.n.z, 0.0f};
+                if (lds_mats ? mat_needs_dir(s_mats[h.mat]) : mat_needs_dir(A.S.mats[h.mat]))
+                    sdir(A.out, q)[0] = v4f{p.d.x, p.d.y, p.d.z, 0.0f};
                 if (A.S.texs) {
                     SA.uv_out[2 * (size_t)q] = h.u;
                     SA.uv_out[2 * (size_t)q + 1] = h.v;
@@ -2406,6 +2454,7 @@ __global__ __launch_bounds__(kBlock, MESH ? 1 : PT_PRODUCE_WAVES) void k_sort_pr
     // (the camera rays' ends are bounce 0's; a later producer's are the next bounce's)
     flush_emissive2(A, emit_cnt, FIRST ? A.bounce : A.bounce + 1, emit_next, s_cnt);
 #undef KC
+#undef KL
 }
 
 // Exclusive scan of the sorted pipeline's histogram when two lanes share the GPU: reduce, scan of
@@ -2435,91 +2484,45 @@ __device__ __forceinline__ void hist_load(const int32_t* __restrict__ in, int64_
 __device__ __forceinline__ int64_t hist_n(int64_t n, const uint32_t* nlive) {
     return nlive ? (int64_t)min((uint64_t)n, (uint64_t)*nlive) : n;
 }
-__global__ __launch_bounds__(kBlock) void k_hist_sums(const int32_t* __restrict__ in, int64_t n, const uint32_t* nlive,
-                                                      uint32_t* __restrict__ sums) {
-    __shared__ uint32_t s_w[4];
+// The two histograms (hist: every survivor, the sorted positions; hist2: those that did not end in
+// the producer, the next producer's work positions) are scanned side by side: sums[2 b] and
+// sums[2 b + 1] are workgroup b's totals.
+__global__ __launch_bounds__(kBlock) void k_hist_sums(const int32_t* __restrict__ in, const int32_t* __restrict__ in2,
+                                                      int64_t n, const uint32_t* nlive, uint32_t* __restrict__ sums) {
+    __shared__ uint32_t s_w[4], s_w2[4];
     n = hist_n(n, nlive);
     const int64_t base = (int64_t)blockIdx.x * kHistTile + (int64_t)threadIdx.x * kHistPer;
-    uint32_t x[kHistPer], v = 0;
+    uint32_t x[kHistPer], y[kHistPer], v = 0, v2 = 0;
     hist_load(in, n, base, x);
+    hist_load(in2, n, base, y);
 #pragma unroll
-    for (int k = 0; k < kHistPer; ++k) v += x[k];
-    uint32_t total;
+    for (int k = 0; k < kHistPer; ++k) { v += x[k]; v2 += y[k]; }
+    uint32_t total, total2;
     (void)block_excl_scan(v, s_w, &total);
-    if (threadIdx.x == 0) sums[blockIdx.x] = total;
+    (void)block_excl_scan(v2, s_w2, &total2);
+    if (threadIdx.x == 0) { sums[2 * blockIdx.x] = total; sums[2 * blockIdx.x + 1] = total2; }
 }
 
 __global__ __launch_bounds__(kBlock) void k_hist_scan_sums(uint32_t* __restrict__ sums, int64_t n, const uint32_t* nlive) {
-    __shared__ uint32_t s_w[4];
+    __shared__ uint32_t s_w[4], s_w2[4];
     const int tiles = (int)((hist_n(n, nlive) + kHistTile - 1) / kHistTile);
     const int per = (tiles + kBlock - 1) / kBlock;
     const int j0 = (int)threadIdx.x * per;
-    uint32_t v = 0;
-    for (int j = j0; j < j0 + per && j < tiles; ++j) v += sums[j];
-    uint32_t total;
-    uint32_t run = block_excl_scan(v, s_w, &total);
+    uint32_t v = 0, v2 = 0;
+    for (int j = j0; j < j0 + per && j < tiles; ++j) { v += sums[2 * j]; v2 += sums[2 * j + 1]; }
+    uint32_t total, total2;
+    uint32_t run = block_excl_scan(v, s_w, &total), run2 = block_excl_scan(v2, s_w2, &total2);
     for (int j = j0; j < j0 + per && j < tiles; ++j) {
-        const uint32_t x = sums[j];
-        sums[j] = run;
-        run += x;
+        const uint32_t a = sums[2 * j], b = sums[2 * j + 1];
+        sums[2 * j] = run;
+        sums[2 * j + 1] = run2;
+        run += a;
+        run2 += b;
     }
 }
 
-// perm (sorted pipeline): the entries' runs, perm[offs[e] + r] = hslot[e] + r for r < in[e], for
-// the live entries but the last (the end offset, whose count is not written).
-__global__ __launch_bounds__(kBlock) void k_hist_apply(const int32_t* __restrict__ in, int32_t* __restrict__ out,
-                                                       int64_t n, const uint32_t* nlive, const uint32_t* __restrict__ sums,
-                                                       const int32_t* __restrict__ hslot, int32_t* __restrict__ perm,
-                                                       const uint32_t* __restrict__ dead) {
-    __shared__ uint32_t s_w[4];
-    n = hist_n(n, nlive);
-    const int64_t base = (int64_t)blockIdx.x * kHistTile + (int64_t)threadIdx.x * kHistPer;
-    uint32_t x[kHistPer], v = 0;
-    hist_load(in, n, base, x);
-#pragma unroll
-    for (int k = 0; k < kHistPer; ++k) v += x[k];
-    uint32_t total;
-    uint32_t run = block_excl_scan(v, s_w, &total) + sums[blockIdx.x];
-    if (perm) {   // the wave writes its entries' runs one after the other, 64 consecutive slots per store
-        // Each live entry's tile's 8 SA.dead words go to LDS first (all loads in flight at once),
-        // so the stores below do not wait on a load per run.
-        __shared__ uint32_t s_dm[kHistTile * (kBlock / 32)];
-        const int lane = (int)threadIdx.x & 63;
-        int32_t s0[kHistPer];
-#pragma unroll
-        for (int k = 0; k < kHistPer; ++k) {
-            const bool live = base + k < n - 1 && x[k] != 0u;
-            s0[k] = live ? hslot[base + k] : 0;
-        }
-#pragma unroll
-        for (int k = 0; k < kHistPer; ++k) {
-            if (base + k < n - 1 && x[k] != 0u) {
-                const v4i_h* d = reinterpret_cast<const v4i_h*>(dead + (size_t)((uint32_t)s0[k] >> 8) * (kBlock / 32));
-                v4i_h* l = reinterpret_cast<v4i_h*>(s_dm + ((int)threadIdx.x * kHistPer + k) * (kBlock / 32));
-                l[0] = d[0];
-                l[1] = d[1];
-            }
-        }
-        wave_sync();   // (each wave reads only its own entries' rows)
-        uint32_t o = run;
-#pragma unroll
-        for (int k = 0; k < kHistPer; ++k) {
-            const bool live = base + k < n - 1 && x[k] != 0u;
-            uint64_t rem = __ballot(live);
-            while (rem) {
-                const int src = __builtin_ctzll(rem);
-                const uint32_t ro = __builtin_amdgcn_readlane(o, src), rc = __builtin_amdgcn_readlane(x[k], src);
-                const uint32_t rs = (uint32_t)__builtin_amdgcn_readlane(s0[k], src);
-                const uint32_t* dm = s_dm + (((int)threadIdx.x & ~63) + src) * kHistPer * (kBlock / 32) + k * (kBlock / 32);
-                for (uint32_t r = (uint32_t)lane; r < rc; r += 64) {   // (slots whose path ended: sign bit set)
-                    const uint32_t b = (rs & (kBlock - 1)) + r;   // (a run lies inside its tile's 256 slots)
-                    perm[ro + r] = (int32_t)((rs + r) | (((dm[b >> 5] >> (b & 31)) & 1u) << 31));
-                }
-                rem &= rem - 1;
-            }
-            o += x[k];
-        }
-    }
+__device__ __forceinline__ void hist_store(int32_t* __restrict__ out, int64_t n, int64_t base, uint32_t run,
+                                           const uint32_t (&x)[kHistPer]) {
     if (base + kHistPer <= n) {
 #pragma unroll
         for (int q = 0; q < kHistPer / 4; ++q) {
@@ -2535,6 +2538,82 @@ __global__ __launch_bounds__(kBlock) void k_hist_apply(const int32_t* __restrict
             run += x[k];
         }
     }
+}
+
+// The scans (out: sorted positions, out2: work positions) and the next producer's work list: for
+// the live entries but the last (the end offset, whose count is not written), the run's slots
+// hslot[e] + r whose path did not end (SA.dead bit clear), in order, at work positions out2[e] + i:
+// perm = the slot, fpos = its sorted position out[e] + r.
+__global__ __launch_bounds__(kBlock) void k_hist_apply(const int32_t* __restrict__ in, int32_t* __restrict__ out,
+                                                       const int32_t* __restrict__ in2, int32_t* __restrict__ out2,
+                                                       int64_t n, const uint32_t* nlive, const uint32_t* __restrict__ sums,
+                                                       const int32_t* __restrict__ hslot, int32_t* __restrict__ perm,
+                                                       int32_t* __restrict__ fpos, const uint32_t* __restrict__ dead) {
+    __shared__ uint32_t s_w[4], s_w2[4];
+    // each entry's tile's 8 SA.dead words (entries with ended paths only), all loads in flight at
+    // once, so the stores below wait on no load per run
+    __shared__ uint32_t s_dm[kHistTile * (kBlock / 32)];
+    n = hist_n(n, nlive);
+    const int64_t base = (int64_t)blockIdx.x * kHistTile + (int64_t)threadIdx.x * kHistPer;
+    uint32_t x[kHistPer], y[kHistPer], v = 0, v2 = 0;
+    hist_load(in, n, base, x);
+    hist_load(in2, n, base, y);
+#pragma unroll
+    for (int k = 0; k < kHistPer; ++k) { v += x[k]; v2 += y[k]; }
+    uint32_t total, total2;
+    const uint32_t run = block_excl_scan(v, s_w, &total) + sums[2 * blockIdx.x];
+    const uint32_t run2 = block_excl_scan(v2, s_w2, &total2) + sums[2 * blockIdx.x + 1];
+    const int lane = (int)threadIdx.x & 63;
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    int32_t s0[kHistPer];
+#pragma unroll
+    for (int k = 0; k < kHistPer; ++k) s0[k] = (base + k < n - 1 && y[k] != 0u) ? hslot[base + k] : 0;
+#pragma unroll
+    for (int k = 0; k < kHistPer; ++k) {
+        if (base + k < n - 1 && y[k] != 0u && y[k] != x[k]) {
+            const v4i_h* d = reinterpret_cast<const v4i_h*>(dead + (size_t)((uint32_t)s0[k] >> 8) * (kBlock / 32));
+            v4i_h* l = reinterpret_cast<v4i_h*>(s_dm + ((int)threadIdx.x * kHistPer + k) * (kBlock / 32));
+            l[0] = d[0];
+            l[1] = d[1];
+        }
+    }
+    wave_sync();   // (each wave reads only its own entries' rows)
+    uint32_t o = run, o2 = run2;
+#pragma unroll
+    for (int k = 0; k < kHistPer; ++k) {   // the wave writes its entries' runs one after the other
+        uint64_t rem = __ballot(base + k < n - 1 && y[k] != 0u);
+        while (rem) {
+            const int src = __builtin_ctzll(rem);
+            const uint32_t ro = __builtin_amdgcn_readlane(o, src), ro2 = __builtin_amdgcn_readlane(o2, src);
+            const uint32_t rc = __builtin_amdgcn_readlane(x[k], src), rl = __builtin_amdgcn_readlane(y[k], src);
+            const uint32_t rs = (uint32_t)__builtin_amdgcn_readlane(s0[k], src);
+            if (rl == rc) {   // no path of the run ended: 64 consecutive positions per store
+                for (uint32_t r = (uint32_t)lane; r < rc; r += 64) {
+                    perm[ro2 + r] = (int32_t)(rs + r);
+                    fpos[ro2 + r] = (int32_t)(ro + r);
+                }
+            } else {
+                const uint32_t* dm = s_dm + (((int)threadIdx.x & ~63) + src) * kHistPer * (kBlock / 32) + k * (kBlock / 32);
+                uint32_t i0 = 0;
+                for (uint32_t r0 = 0; r0 < rc; r0 += 64) {
+                    const uint32_t r = r0 + (uint32_t)lane, b = (rs & (kBlock - 1)) + r;   // (a run lies inside its tile)
+                    const bool keep = r < rc && ((dm[(b >> 5) & 7] >> (b & 31)) & 1u) == 0u;
+                    const uint64_t km = __ballot(keep);
+                    if (keep) {
+                        const uint32_t i = i0 + (uint32_t)__popcll(km & lt);
+                        perm[ro2 + i] = (int32_t)(rs + r);
+                        fpos[ro2 + i] = (int32_t)(ro + r);
+                    }
+                    i0 += (uint32_t)__popcll(km);
+                }
+            }
+            rem &= rem - 1;
+        }
+        o += x[k];
+        o2 += y[k];
+    }
+    hist_store(out, n, base, run, x);
+    hist_store(out2, n, base, run2, y);
 }
 
 // spp > 1: add the per-slot colours in sample order (finalGather as `spp` sequential iterations).
@@ -2663,6 +2742,7 @@ struct pt_ctx {
     hipEvent_t ev_fork = nullptr, ev_join[kMaxLanes] = {};
     struct SortSet {   // material-sort buffers of one lane (k_sort_produce / k_hist_*)
         int32_t *hslot = nullptr, *hist = nullptr, *offs = nullptr, *perm = nullptr, *itb = nullptr;
+        int32_t *hist2 = nullptr, *offs2 = nullptr, *fpos = nullptr;
         uint32_t* dead = nullptr;   // (k_sort_produce -> k_hist_apply: slots whose path ended)
         float* uv[2] = {nullptr, nullptr};   // (u, v) of the records in buf[0] / buf[1]
         uint32_t* sums = nullptr;            // histogram scan: tile sums
@@ -3016,7 +3096,8 @@ int build_cmask(pt_ctx* c) {
 }
 
 // One block of 4P planes per parity: the fused / split pipelines use the first three as the
-// a, b, c planes; the sorted pipeline uses the block as P 64-byte records (srec).
+// a, b, c planes; the sorted pipeline uses the first three as P 48-byte records (srec) and the
+// fourth for the ray directions of specular hits (sdir).
 int alloc_paths(pt_ctx* c, PathSoA& B, size_t P) {
     if (int rc = c->alloc(&B.a, 4 * P)) return rc;
     B.b = B.a + P;
@@ -3673,10 +3754,13 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
         if (int rc = c->alloc(&ss.hslot, (size_t)ss.hist_cap)) return bail(rc);
         if (int rc = c->alloc(&ss.perm, paths)) return bail(rc);
         if (int rc = c->alloc(&ss.dead, (cap / kBlock + 2) * (kBlock / 32))) return bail(rc);
+        if (int rc = c->alloc(&ss.fpos, paths)) return bail(rc);
+        if (int rc = c->alloc(&ss.hist2, (size_t)ss.hist_cap)) return bail(rc);
+        if (int rc = c->alloc(&ss.offs2, (size_t)ss.hist_cap)) return bail(rc);
         if (int rc = c->alloc(&ss.hist, (size_t)ss.hist_cap)) return bail(rc);
         if (int rc = c->alloc(&ss.offs, (size_t)ss.hist_cap)) return bail(rc);
         if (int rc = c->alloc(&ss.itb, 2 * ((size_t)kMaxSpp + 1))) return bail(rc);
-        if (int rc = c->alloc(&ss.sums, tiles)) return bail(rc);
+        if (int rc = c->alloc(&ss.sums, 2 * tiles)) return bail(rc);
         if (!S.textures.empty())
             for (int h = 0; h < 2; ++h)
                 if (int rc = c->alloc(&ss.uv[h], 2 * cap)) return bail(rc);
@@ -3737,9 +3821,9 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
             a.in = bufs[lcur];
             a.out = bufs[lcur ^ 1];
             a.hit.uv = ss.uv[lcur];
-            const SortArgs sa{ss.hslot, ss.hist, ss.offs, ss.perm, ss.itb, ss.uv[lcur ^ 1], ss.dead};
+            const SortArgs sa{ss.hslot, ss.hist, ss.offs, ss.hist2, ss.offs2, ss.perm, ss.fpos, ss.itb, ss.uv[lcur ^ 1], ss.dead};
             hipLaunchKernelGGL(produce_kernel(first, spp1, mesh), dim3(c->grid_bounce[0]), dim3(kBlock),
-                               (size_t)8 * c->nmats * sizeof(uint32_t), s, a, sa);
+                               (size_t)16 * c->nmats * sizeof(uint32_t), s, a, sa);
             HIP_TRY(hipGetLastError());
             ++lc;
             lcur ^= 1;
@@ -3754,10 +3838,12 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
         a.parity = (int)(lc & 1);
         const uint32_t* nlive = &a.ctl[a.parity].hist_live;
         const int tiles = (int)((ss.hist_cap + kHistTile - 1) / kHistTile);
-        hipLaunchKernelGGL(k_hist_sums, dim3(tiles), dim3(kBlock), 0, s, (const int32_t*)ss.hist, ss.hist_cap, nlive, ss.sums);
+        hipLaunchKernelGGL(k_hist_sums, dim3(tiles), dim3(kBlock), 0, s, (const int32_t*)ss.hist, (const int32_t*)ss.hist2,
+                           ss.hist_cap, nlive, ss.sums);
         hipLaunchKernelGGL(k_hist_scan_sums, dim3(1), dim3(kBlock), 0, s, ss.sums, ss.hist_cap, nlive);
-        hipLaunchKernelGGL(k_hist_apply, dim3(tiles), dim3(kBlock), 0, s, (const int32_t*)ss.hist, ss.offs, ss.hist_cap,
-                           nlive, (const uint32_t*)ss.sums, (const int32_t*)ss.hslot, ss.perm, (const uint32_t*)ss.dead);
+        hipLaunchKernelGGL(k_hist_apply, dim3(tiles), dim3(kBlock), 0, s, (const int32_t*)ss.hist, ss.offs,
+                           (const int32_t*)ss.hist2, ss.offs2, ss.hist_cap, nlive, (const uint32_t*)ss.sums,
+                           (const int32_t*)ss.hslot, ss.perm, ss.fpos, (const uint32_t*)ss.dead);
         HIP_TRY(hipGetLastError());
         if (int rc = produce(false)) return rc;
         return prof_end(ev, s);
