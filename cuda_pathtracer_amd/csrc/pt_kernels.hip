@@ -2194,16 +2194,21 @@ __global__ __launch_bounds__(kBlock) void k_compact_paths(const KArgs A) {
 // Batched passes sort every iteration on its own (stable sort by (iteration, material), as `spp`
 // sequential pathtrace() calls would): tiles never span two iterations, and an iteration's tiles
 // form one block of the histogram.
-// Path j of the sorted pipeline is ONE 48-byte record (only paths that go on to be shaded have one:
-// a miss or an emitter ends in the producer), so the gather reads one 48-byte span:
-//   r0 = (hit point.xyz, c.r)   r1 = (c.gb, slot, material)   r2 = (n.xyz, 0)
-// The hit point (getPointOnRay, as shade computes it) replaces the ray's origin and length; the
-// ray's direction, which only a refractive or possibly reflective material reads (mat_needs_dir),
-// goes to a side plane (the block's fourth) for those paths alone.  `bounces` is not stored: every
-// path entering bounce b has b bounces behind it.  Texture coordinates (textured scenes only) go to
-// a side array, double-buffered like the records.
-__device__ __forceinline__ v4f* srec(const PathSoA& B, int j) { return B.a + 3 * (size_t)(uint32_t)j; }
-__device__ __forceinline__ v4f* sdir(const PathSoA& B, int j) { return B.c + (B.b - B.a) + (size_t)(uint32_t)j; }
+// Path j of the sorted pipeline is ONE 32-byte record (only paths that go on to be shaded have one:
+// a miss or an emitter ends in the producer), so the gather reads one 32-byte span:
+//   r0 = (hit point.xyz, c.r)   r1 = (c.gb, slot, code)
+// The hit point (getPointOnRay, as shade computes it) replaces the ray's origin and length.  code
+// >= 0: a cube hit, geom * 6 + slab code (Hit::frame): the material is the geom's, the normal its
+// precomputed slab normal (box_normal, which is how the hit's normal was made) and the tangent
+// frame its precomputed one.  code < 0: -(material + 1), the normal in a side plane.  The ray's
+// direction, which only a refractive or possibly reflective material reads (mat_needs_dir), goes
+// to a second side plane for those paths alone.  Block of 4P planes: records in the first two,
+// directions in the third, normals in the fourth.  `bounces` is not stored: every path entering
+// bounce b has b bounces behind it.  Texture coordinates (textured scenes only) go to a side
+// array, double-buffered like the records.
+__device__ __forceinline__ v4f* srec(const PathSoA& B, int j) { return B.a + 2 * (size_t)(uint32_t)j; }
+__device__ __forceinline__ v4f* sdir(const PathSoA& B, int j) { return B.c + (size_t)(uint32_t)j; }
+__device__ __forceinline__ v4f* snrm(const PathSoA& B, int j) { return B.c + (B.b - B.a) + (size_t)(uint32_t)j; }
 
 struct SortArgs {
     int32_t* hslot;     // per (iteration, material, tile): first slot of its run (sort_hidx)
@@ -2257,6 +2262,7 @@ __global__ __launch_bounds__(kBlock, MESH ? 1 : (FIRST ? PT_PRODUCE_WAVES_FIRST 
 void k_sort_produce(const KArgs A, const SortArgs SA) {
     __shared__ DMaterial s_mats[kLdsMats];
     __shared__ LGeom s_geoms[MESH ? 1 : kLdsGeoms];
+    __shared__ float s_frm[MESH || FIRST ? 1 : kLdsGeoms * 36];   // the cubes' tangent frames (stage_frames)
     __shared__ int32_t s_sb[kMaxSpp + 1];      // work start of every iteration (first bounce: j * npix)
     __shared__ int32_t s_fb[kMaxSpp + 1];      // sorted start of every iteration (RNG key base)
     __shared__ int32_t s_tb[kMaxSpp + 1];      // first tile of every iteration ([spp] = all tiles)
@@ -2306,9 +2312,11 @@ void k_sort_produce(const KArgs A, const SortArgs SA) {
     }
     if ((int)blockIdx.x >= T) return;
     if (!MESH) stage_geoms(A.S, s_geoms);
+    if (!MESH && !FIRST) stage_frames(A.S, s_frm);
     if (tid < 2 * (kBlock / 32)) s_dead[tid / (kBlock / 32)][tid % (kBlock / 32)] = 0u;
     stage_materials(A, s_mats);   // (its barrier also orders s_dead's clearing)
     const bool lds_mats = nmats <= kLdsMats;
+    const bool lds_geoms = !MESH && A.S.ngeoms <= kLdsGeoms;   // (stage_geoms / stage_frames ran)
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     uint32_t emit_cnt = 0, emit_next = 0;
     int k = 0;
@@ -2329,14 +2337,28 @@ void k_sort_produce(const KArgs A, const SortArgs SA) {
             } else {
                 const int j = SA.perm[idx];
                 const v4f* r = srec(A.in, j);
-                // (plain loads: a gather of 48-byte records whose 16-byte pieces share lines)
-                const v4f r0 = r[0], r1 = r[1], r2 = r[2];
+                // (plain loads: a gather of 32-byte records)
+                const v4f r0 = r[0], r1 = r[1];
                 const f3 hitp = F3(r0[0], r0[1], r0[2]);
                 p.c = F3(r0[3], r1[0], r1[1]);
                 p.slot = __float_as_int(r1[2]);
                 p.bounces = A.bounce;
-                h.mat = __float_as_int(r1[3]);
-                h.n = F3(r2[0], r2[1], r2[2]);
+                const int code = __float_as_int(r1[3]);
+                if (code >= 0) {   // a cube's slab: the geom's material, normal and frame
+                    const int g = code / 6, f = code - 6 * g;
+                    if (lds_geoms) {
+                        h.mat = s_geoms[g].material;
+                        h.n = F3(s_geoms[g].nrm[f][0], s_geoms[g].nrm[f][1], s_geoms[g].nrm[f][2]);
+                    } else {
+                        h.mat = A.S.geoms[g].material;
+                        h.n = F3(A.S.geoms[g].nrm[f][0], A.S.geoms[g].nrm[f][1], A.S.geoms[g].nrm[f][2]);
+                    }
+                    h.frame = code;
+                } else {
+                    h.mat = -code - 1;
+                    const v4f nv = snrm(A.in, j)[0];
+                    h.n = F3(nv[0], nv[1], nv[2]);
+                }
                 h.u = h.v = 0.0f;
                 p.d = F3(0, 0, 0);
                 if (lds_mats ? mat_needs_dir(s_mats[h.mat]) : mat_needs_dir(A.S.mats[h.mat])) {
@@ -2353,8 +2375,9 @@ void k_sort_produce(const KArgs A, const SortArgs SA) {
                 // key: sorted index within the path's own iteration (paths that ended in the
                 // previous launch hold positions too: fpos)
                 const int key = A.fl.rng_pixel ? slot_pixel(A.cam, A.tile, p.slot) : SA.fpos[idx] - s_fb[it];
-                alive = lds_mats ? shade_from(A.S, A.fl, A.tile.depth, iter, key, p, h, hitp, s_mats)
-                                 : shade_from(A.S, A.fl, A.tile.depth, iter, key, p, h, hitp, A.S.mats);
+                const float* frames = lds_geoms ? s_frm : nullptr;
+                alive = lds_mats ? shade_from(A.S, A.fl, A.tile.depth, iter, key, p, h, hitp, s_mats, frames)
+                                 : shade_from(A.S, A.fl, A.tile.depth, iter, key, p, h, hitp, A.S.mats, frames);
                 if (!alive) {
                     emitted = p.c.x != 0.0f || p.c.y != 0.0f || p.c.z != 0.0f;
                     retire<SPP1>(A, p);
@@ -2432,12 +2455,13 @@ void k_sort_produce(const KArgs A, const SortArgs SA) {
                 retire<SPP1>(A, e);
             } else {
                 v4f* r = srec(A.out, q);
-                // (plain stores: each store instruction covers 16 of every 48 bytes, and L2 merges the
-                // three into whole lines; non-temporal ones halved config 3's rate)
+                // (plain stores: each store instruction covers 16 of every 32 bytes, and L2 merges the
+                // two into whole lines; non-temporal ones halved config 3's rate)
                 const f3 hitp = point_on_ray(p.o, p.d, h.t);
+                const int code = h.frame >= 0 ? h.frame : -(h.mat + 1);
                 r[0] = v4f{hitp.x, hitp.y, hitp.z, p.c.x};
-                r[1] = v4f{p.c.y, p.c.z, __int_as_float(p.slot), __int_as_float(h.mat)};
-                r[2] = v4f{h.n.x, h.n.y, h.n.z, 0.0f};
+                r[1] = v4f{p.c.y, p.c.z, __int_as_float(p.slot), __int_as_float(code)};
+                if (code < 0) snrm(A.out, q)[0] = v4f{h.n.x, h.n.y, h.n.z, 0.0f};
                 if (lds_mats ? mat_needs_dir(s_mats[h.mat]) : mat_needs_dir(A.S.mats[h.mat]))
                     sdir(A.out, q)[0] = v4f{p.d.x, p.d.y, p.d.z, 0.0f};
                 if (A.S.texs) {
@@ -3096,8 +3120,8 @@ int build_cmask(pt_ctx* c) {
 }
 
 // One block of 4P planes per parity: the fused / split pipelines use the first three as the
-// a, b, c planes; the sorted pipeline uses the first three as P 48-byte records (srec) and the
-// fourth for the ray directions of specular hits (sdir).
+// a, b, c planes; the sorted pipeline uses the first two as P 32-byte records (srec), the third
+// for the ray directions of specular hits (sdir) and the fourth for normals not held by a code.
 int alloc_paths(pt_ctx* c, PathSoA& B, size_t P) {
     if (int rc = c->alloc(&B.a, 4 * P)) return rc;
     B.b = B.a + P;
