@@ -8,5 +8,5 @@ mkdir -p $B/$N
 /opt/rocm/bin/hipcc -x hip --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off $FLAGS -I $R/include \
     -c $R/cuda_pathtracer_amd/csrc/pt_kernels.hip -o $B/$N/pt_kernels.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $B/libpt_amd_$N.so $B/$N/pt_kernels.o \
-    $B/sc_kernels.hip.o $B/pt_scene.cpp.o $B/pt_mesh.cpp.o $B/pt_image.cpp.o $B/pt_jpeg.cpp.o -lz
+    $B/sc_kernels.hip.o $B/bvh_build.hip.o $B/pt_scene.cpp.o $B/pt_mesh.cpp.o $B/pt_image.cpp.o $B/pt_jpeg.cpp.o -lz
 echo $B/libpt_amd_$N.so
