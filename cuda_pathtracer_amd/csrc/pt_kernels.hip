@@ -2515,16 +2515,20 @@ __global__ __launch_bounds__(kBlock) void k_hist_sums(const int32_t* __restrict_
                                                       int64_t n, const uint32_t* nlive, uint32_t* __restrict__ sums) {
     __shared__ uint32_t s_w[4], s_w2[4];
     n = hist_n(n, nlive);
-    const int64_t base = (int64_t)blockIdx.x * kHistTile + (int64_t)threadIdx.x * kHistPer;
-    uint32_t x[kHistPer], y[kHistPer], v = 0, v2 = 0;
-    hist_load(in, n, base, x);
-    hist_load(in2, n, base, y);
+    // (a grid-stride loop over blocks of kHistTile entries: the grid is sized for the capacity, the
+    // live length is read here, and later bounces use a few blocks)
+    for (int64_t blk = blockIdx.x; blk * kHistTile < n; blk += gridDim.x) {
+        const int64_t base = blk * kHistTile + (int64_t)threadIdx.x * kHistPer;
+        uint32_t x[kHistPer], y[kHistPer], v = 0, v2 = 0;
+        hist_load(in, n, base, x);
+        hist_load(in2, n, base, y);
 #pragma unroll
-    for (int k = 0; k < kHistPer; ++k) { v += x[k]; v2 += y[k]; }
-    uint32_t total, total2;
-    (void)block_excl_scan(v, s_w, &total);
-    (void)block_excl_scan(v2, s_w2, &total2);
-    if (threadIdx.x == 0) { sums[2 * blockIdx.x] = total; sums[2 * blockIdx.x + 1] = total2; }
+        for (int k = 0; k < kHistPer; ++k) { v += x[k]; v2 += y[k]; }
+        uint32_t total, total2;
+        (void)block_excl_scan(v, s_w, &total);
+        (void)block_excl_scan(v2, s_w2, &total2);
+        if (threadIdx.x == 0) { sums[2 * blk] = total; sums[2 * blk + 1] = total2; }
+    }
 }
 
 __global__ __launch_bounds__(kBlock) void k_hist_scan_sums(uint32_t* __restrict__ sums, int64_t n, const uint32_t* nlive) {
@@ -2575,69 +2579,72 @@ __global__ __launch_bounds__(kBlock) void k_hist_apply(const int32_t* __restrict
                                                        int32_t* __restrict__ fpos, const uint32_t* __restrict__ dead) {
     __shared__ uint32_t s_w[4], s_w2[4];
     // each entry's tile's 8 SA.dead words (entries with ended paths only), all loads in flight at
-    // once, so the stores below wait on no load per run
+    // once, so the stores below wait on no load per run (rows are per wave: no block barrier)
     __shared__ uint32_t s_dm[kHistTile * (kBlock / 32)];
     n = hist_n(n, nlive);
-    const int64_t base = (int64_t)blockIdx.x * kHistTile + (int64_t)threadIdx.x * kHistPer;
-    uint32_t x[kHistPer], y[kHistPer], v = 0, v2 = 0;
-    hist_load(in, n, base, x);
-    hist_load(in2, n, base, y);
-#pragma unroll
-    for (int k = 0; k < kHistPer; ++k) { v += x[k]; v2 += y[k]; }
-    uint32_t total, total2;
-    const uint32_t run = block_excl_scan(v, s_w, &total) + sums[2 * blockIdx.x];
-    const uint32_t run2 = block_excl_scan(v2, s_w2, &total2) + sums[2 * blockIdx.x + 1];
     const int lane = (int)threadIdx.x & 63;
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    int32_t s0[kHistPer];
+    for (int64_t blk = blockIdx.x; blk * kHistTile < n; blk += gridDim.x) {   // (as k_hist_sums)
+        const int64_t base = blk * kHistTile + (int64_t)threadIdx.x * kHistPer;
+        uint32_t x[kHistPer], y[kHistPer], v = 0, v2 = 0;
+        hist_load(in, n, base, x);
+        hist_load(in2, n, base, y);
 #pragma unroll
-    for (int k = 0; k < kHistPer; ++k) s0[k] = (base + k < n - 1 && y[k] != 0u) ? hslot[base + k] : 0;
+        for (int k = 0; k < kHistPer; ++k) { v += x[k]; v2 += y[k]; }
+        uint32_t total, total2;
+        const uint32_t run = block_excl_scan(v, s_w, &total) + sums[2 * blk];
+        const uint32_t run2 = block_excl_scan(v2, s_w2, &total2) + sums[2 * blk + 1];
+        int32_t s0[kHistPer];
 #pragma unroll
-    for (int k = 0; k < kHistPer; ++k) {
-        if (base + k < n - 1 && y[k] != 0u && y[k] != x[k]) {
-            const v4i_h* d = reinterpret_cast<const v4i_h*>(dead + (size_t)((uint32_t)s0[k] >> 8) * (kBlock / 32));
-            v4i_h* l = reinterpret_cast<v4i_h*>(s_dm + ((int)threadIdx.x * kHistPer + k) * (kBlock / 32));
-            l[0] = d[0];
-            l[1] = d[1];
-        }
-    }
-    wave_sync();   // (each wave reads only its own entries' rows)
-    uint32_t o = run, o2 = run2;
+        for (int k = 0; k < kHistPer; ++k) s0[k] = (base + k < n - 1 && y[k] != 0u) ? hslot[base + k] : 0;
 #pragma unroll
-    for (int k = 0; k < kHistPer; ++k) {   // the wave writes its entries' runs one after the other
-        uint64_t rem = __ballot(base + k < n - 1 && y[k] != 0u);
-        while (rem) {
-            const int src = __builtin_ctzll(rem);
-            const uint32_t ro = __builtin_amdgcn_readlane(o, src), ro2 = __builtin_amdgcn_readlane(o2, src);
-            const uint32_t rc = __builtin_amdgcn_readlane(x[k], src), rl = __builtin_amdgcn_readlane(y[k], src);
-            const uint32_t rs = (uint32_t)__builtin_amdgcn_readlane(s0[k], src);
-            if (rl == rc) {   // no path of the run ended: 64 consecutive positions per store
-                for (uint32_t r = (uint32_t)lane; r < rc; r += 64) {
-                    perm[ro2 + r] = (int32_t)(rs + r);
-                    fpos[ro2 + r] = (int32_t)(ro + r);
-                }
-            } else {
-                const uint32_t* dm = s_dm + (((int)threadIdx.x & ~63) + src) * kHistPer * (kBlock / 32) + k * (kBlock / 32);
-                uint32_t i0 = 0;
-                for (uint32_t r0 = 0; r0 < rc; r0 += 64) {
-                    const uint32_t r = r0 + (uint32_t)lane, b = (rs & (kBlock - 1)) + r;   // (a run lies inside its tile)
-                    const bool keep = r < rc && ((dm[(b >> 5) & 7] >> (b & 31)) & 1u) == 0u;
-                    const uint64_t km = __ballot(keep);
-                    if (keep) {
-                        const uint32_t i = i0 + (uint32_t)__popcll(km & lt);
-                        perm[ro2 + i] = (int32_t)(rs + r);
-                        fpos[ro2 + i] = (int32_t)(ro + r);
-                    }
-                    i0 += (uint32_t)__popcll(km);
-                }
+        for (int k = 0; k < kHistPer; ++k) {
+            if (base + k < n - 1 && y[k] != 0u && y[k] != x[k]) {
+                const v4i_h* d = reinterpret_cast<const v4i_h*>(dead + (size_t)((uint32_t)s0[k] >> 8) * (kBlock / 32));
+                v4i_h* l = reinterpret_cast<v4i_h*>(s_dm + ((int)threadIdx.x * kHistPer + k) * (kBlock / 32));
+                l[0] = d[0];
+                l[1] = d[1];
             }
-            rem &= rem - 1;
         }
-        o += x[k];
-        o2 += y[k];
+        wave_sync();   // (each wave reads only its own entries' rows)
+        uint32_t o = run, o2 = run2;
+#pragma unroll
+        for (int k = 0; k < kHistPer; ++k) {   // the wave writes its entries' runs one after the other
+            uint64_t rem = __ballot(base + k < n - 1 && y[k] != 0u);
+            while (rem) {
+                const int src = __builtin_ctzll(rem);
+                const uint32_t ro = __builtin_amdgcn_readlane(o, src), ro2 = __builtin_amdgcn_readlane(o2, src);
+                const uint32_t rc = __builtin_amdgcn_readlane(x[k], src), rl = __builtin_amdgcn_readlane(y[k], src);
+                const uint32_t rs = (uint32_t)__builtin_amdgcn_readlane(s0[k], src);
+                if (rl == rc) {   // no path of the run ended: 64 consecutive positions per store
+                    for (uint32_t r = (uint32_t)lane; r < rc; r += 64) {
+                        perm[ro2 + r] = (int32_t)(rs + r);
+                        fpos[ro2 + r] = (int32_t)(ro + r);
+                    }
+                } else {
+                    const uint32_t* dm = s_dm + (((int)threadIdx.x & ~63) + src) * kHistPer * (kBlock / 32) + k * (kBlock / 32);
+                    uint32_t i0 = 0;
+                    for (uint32_t r0 = 0; r0 < rc; r0 += 64) {
+                        const uint32_t r = r0 + (uint32_t)lane, b = (rs & (kBlock - 1)) + r;   // (a run lies inside its tile)
+                        const bool keep = r < rc && ((dm[(b >> 5) & 7] >> (b & 31)) & 1u) == 0u;
+                        const uint64_t km = __ballot(keep);
+                        if (keep) {
+                            const uint32_t i = i0 + (uint32_t)__popcll(km & lt);
+                            perm[ro2 + i] = (int32_t)(rs + r);
+                            fpos[ro2 + i] = (int32_t)(ro + r);
+                        }
+                        i0 += (uint32_t)__popcll(km);
+                    }
+                }
+                rem &= rem - 1;
+            }
+            o += x[k];
+            o2 += y[k];
+        }
+        hist_store(out, n, base, run, x);
+        hist_store(out2, n, base, run2, y);
+        wave_sync();   // (this wave's s_dm rows are rewritten by the next block)
     }
-    hist_store(out, n, base, run, x);
-    hist_store(out2, n, base, run2, y);
 }
 
 // spp > 1: add the per-slot colours in sample order (finalGather as `spp` sequential iterations).
@@ -2780,6 +2787,7 @@ struct pt_ctx {
     uint32_t* tq = nullptr;              // k_traverse ray tickets: [lane][bounce], zeroed per pass
     int grid_traverse = 0;               // k_traverse: one resident wave of workgroups
     int grid_traverse4 = 0;              // k_traverse4 (4-wide layout): the same for its footprint
+    int cus = 256;                       // compute units of the device
     int quad_occ = 0;                    // k_traverse4: bound on its stack occupancy (build_quads)
     bool trav_quads = false;             // mesh mode 2 walks the 4-wide layout (PT_AMD_TRAV=pairs: off)
     hipStream_t fin_stream = nullptr;
@@ -3649,6 +3657,7 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
     // occupancy API's answer, which can over-report by one for SGPR-heavy kernels).
     int cus = 256;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
+    c->cus = cus;
     c->grid_trace = std::max(1, std::min({(int)((P + kBlock - 1) / kBlock), cus * 8, A.emit_stride}));
     c->grid_compact = std::max(1, std::min((int)((P + kCompactTile - 1) / kCompactTile), cus * resident_per_cu((const void*)k_compact_paths)));
     for (int f = 0; f < 2; ++f) {   // k_bounce: any grid is correct; one full wave of equal-work
@@ -3865,10 +3874,11 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
         a.parity = (int)(lc & 1);
         const uint32_t* nlive = &a.ctl[a.parity].hist_live;
         const int tiles = (int)((ss.hist_cap + kHistTile - 1) / kHistTile);
-        hipLaunchKernelGGL(k_hist_sums, dim3(tiles), dim3(kBlock), 0, s, (const int32_t*)ss.hist, (const int32_t*)ss.hist2,
+        const int hgrid = std::min(tiles, 4 * c->cus);   // (grid-stride over the live blocks)
+        hipLaunchKernelGGL(k_hist_sums, dim3(hgrid), dim3(kBlock), 0, s, (const int32_t*)ss.hist, (const int32_t*)ss.hist2,
                            ss.hist_cap, nlive, ss.sums);
         hipLaunchKernelGGL(k_hist_scan_sums, dim3(1), dim3(kBlock), 0, s, ss.sums, ss.hist_cap, nlive);
-        hipLaunchKernelGGL(k_hist_apply, dim3(tiles), dim3(kBlock), 0, s, (const int32_t*)ss.hist, ss.offs,
+        hipLaunchKernelGGL(k_hist_apply, dim3(hgrid), dim3(kBlock), 0, s, (const int32_t*)ss.hist, ss.offs,
                            (const int32_t*)ss.hist2, ss.offs2, ss.hist_cap, nlive, (const uint32_t*)ss.sums,
                            (const int32_t*)ss.hslot, ss.perm, ss.fpos, (const uint32_t*)ss.dead);
         HIP_TRY(hipGetLastError());
