@@ -501,7 +501,7 @@ def main() -> None:
     avg_ms = k_ms / max(k_n, 1)
     achieved = per_launch_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     # pt_kernels.hip pt_create: 3 lanes for large sorted passes (kThreeLanePaths), 1 with the BVH walk
-    default_lanes = 3 if sorted_ and pt.npaths >= (48 << 20) else (1 if walk else 2)
+    default_lanes = 3 if sorted_ and pt.npaths >= (48 << 20) else (1 if quads else 2)
     lanes = min(int(os.environ.get("PT_AMD_LANES", str(default_lanes))), spp, 4) \
         if (spp > 1 and (sorted_ or os.environ.get("PT_PIPELINE") != "split")) else 1
     # every bounce's algorithmic bytes (184 B per segment) of one step over the step time: the

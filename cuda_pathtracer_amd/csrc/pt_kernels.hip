@@ -3745,7 +3745,8 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
         const bool three = c->flags.sort_by_material != 0 && P >= kThreeLanePaths;
         // (the BVH walk's persistent grid fills the GPU, so a second lane's bounce kernel only waits
         // for it: config 5 at one lane 794.6 vs 784.8 Mray/s, same box, two alternations)
-        const bool walk = c->flags.sort_by_material == 0 && mesh_mode(c) == kMeshPre;
+        const bool walk = c->flags.sort_by_material == 0 && mesh_mode(c) == kMeshPre && c->trav_quads &&
+                          c->flags.bvh_cull == 0;   // (the pair walk with bvh_cull: 790 at two lanes vs 730 at one)
         const int want = lv ? std::max(1, std::min(kMaxLanes, std::atoi(lv))) : (three ? 3 : (walk ? 1 : 2));
         const int L = std::min(want, sh.spp);
         if (L >= 2) {
