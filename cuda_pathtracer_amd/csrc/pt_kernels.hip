@@ -79,6 +79,7 @@ struct SceneDev {
     v4f root_lo, root_hi;  // root box
     const struct DQuad* __restrict__ quads;   // 4-wide collapse of the pair tree (k_traverse4), or null
     int32_t root_qcode;    // root's code in the quad layout (quad index or leaf code)
+    const float* __restrict__ tpack;   // the triangles again as packed 36-byte (v0, e1, e2): k_traverse4's task loads
 };
 struct CamDev {
     float pos[3], view[3], up[3], right[3], pl[2];
@@ -1815,9 +1816,21 @@ __global__ __launch_bounds__(kBlock, PT_T4_WAVES) void k_traverse4(const KArgs A
 #endif
         }
         v4f t0, t1, t2;
+#ifndef PT_T4_TRI_PACK
+#define PT_T4_TRI_PACK 1
+#endif
         auto load_tri = [&]() {
+#if PT_T4_TRI_PACK
+            // 36 bytes per triangle: a leaf's consecutive triangles cover fewer cache lines
+            typedef float v3f __attribute__((ext_vector_type(3)));
+            const float* p = S.tpack + 9 * (size_t)tidx;
+            const v3f a = *reinterpret_cast<const v3f*>(p), b = *reinterpret_cast<const v3f*>(p + 3),
+                      c = *reinterpret_cast<const v3f*>(p + 6);
+            t0 = v4f{a[0], a[1], a[2], 0.f}; t1 = v4f{b[0], b[1], b[2], 0.f}; t2 = v4f{c[0], c[1], c[2], 0.f};
+#else
             const v4f* tsrc = reinterpret_cast<const v4f*>(S.tris + tidx);   // (non-task lanes: triangle 0)
             t0 = tsrc[0]; t1 = tsrc[1]; t2 = tsrc[2];
+#endif
         };
 #if PT_T4_LOADS == 1
         load_tri();
@@ -3553,8 +3566,20 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
             std::memcpy(at[i].n, t.n, sizeof at[i].n);
             std::memcpy(at[i].uv, t.uv, sizeof at[i].uv);
         }
+        std::vector<float> pack(9 * tr.size());
+        for (size_t i = 0; i < tr.size(); ++i)
+            for (int k = 0; k < 3; ++k) {
+                pack[9 * i + k] = tr[i].a[k];
+                pack[9 * i + 3 + k] = tr[i].b[k];
+                pack[9 * i + 6 + k] = tr[i].c[k];
+            }
         DTri* d_tr;
         DTriAttr* d_at;
+        float* d_pack;
+        if (int rc = c->alloc(&d_pack, pack.size())) return bail(rc);
+        if ((e = hipMemcpy(d_pack, pack.data(), pack.size() * sizeof(float), hipMemcpyHostToDevice)) != hipSuccess)
+            return bail(pt::fail(PT_ERR_HIP, std::string("triangle upload: ") + hipGetErrorString(e)));
+        A.S.tpack = d_pack;
         if (int rc = c->alloc(&d_tr, tr.size())) return bail(rc);
         if (int rc = c->alloc(&d_at, at.size())) return bail(rc);
         if ((e = hipMemcpy(d_tr, tr.data(), tr.size() * sizeof(DTri), hipMemcpyHostToDevice)) != hipSuccess ||
