@@ -833,3 +833,26 @@ def test_config5_100k_triangles_bitexact(tmp_path, kw):
     g, r, st, live = _run(Scene(path), O.OracleScene.from_json(path), _gui(**kw), iters=2, spp=2)
     _assert_bitexact(g, r, f"config 5 100k triangles {kw}")
     assert st["bounce_live"] == live and r.sum() > 0
+
+
+@pytest.mark.parametrize("spp", [1, 3])
+@pytest.mark.parametrize("look", ["away", "light"])
+def test_sorted_paths_that_all_end_early(cornell_path, spp, look):
+    """Material-sorted shading when the producer retires (almost) every path itself: a camera
+    facing away from the box (every camera ray misses: the next producer gets no work positions)
+    and one looking straight up at the light (most camera rays meet the emitter).  Live-path and
+    emission counts and the image equal the oracle's (shade_ends, pathtrace.cu:318-330)."""
+    from cuda_pathtracer_amd import Scene
+    eye, at, up = ((0, 5, 10.5), (0, 5, 30), (0, 1, 0)) if look == "away" else ((0, 6, 2.5), (0, 10, 0), (0, 1, 0))
+    s = Scene(cornell_path)
+    s.set_camera((48, 32), 45.0, eye, at, up)
+    s.finalize()
+    o = O.OracleScene.from_json(cornell_path)
+    o.set_camera((48, 32), 45.0, eye, at, up)
+    g, r, st, live = _run(s, o, _gui(sortbyMaterial=True), iters=3, spp=spp)
+    _assert_bitexact(g, r, f"sorted, camera {look}, spp {spp}")
+    assert list(st["bounce_live"][:len(live)]) == live
+    if look == "away":
+        assert live[0] == 3 * 48 * 32 and sum(live[1:]) == 0 and r.sum() == 0
+    else:
+        assert r.sum() > 0 and live[1] < live[0]
