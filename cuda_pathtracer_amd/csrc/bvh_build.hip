@@ -16,8 +16,9 @@
 //     host recursion's own order;
 //   * subtree sizes and inner boxes (left || right) bottom-up, preorder indices top-down (traverse_bvh :138-154: DFS, left child
 //     at i + 1), then the flattened nodes and the reordered triangles are written (k_bvh_emit).
-// Scenes whose triangle boxes or centres hold a NaN (the fold is then order-dependent in a way the
-// block reductions do not reproduce) are built on the host (pt::build_bvh_device returns 1).
+// Triangles whose boxes or centres hold a NaN (the fold is then order-dependent in a way the block
+// reductions do not reproduce) are handed to the host build (pt::build_bvh_device returns 1) — a
+// guard only: the mesh loader rejects non-finite vertices (pt_mesh.cpp append_mesh_impl).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -84,8 +85,8 @@ __device__ __forceinline__ int longest_axis(const Box& b) {
 __device__ __forceinline__ int region_of(const Box& cb, const float* c, int axis) {
     float o = c[axis] - cb.mn[axis];   // getOffsetBoxes (boundingbox.h:94-105)
     if (cb.mx[axis] > cb.mn[axis]) o /= (cb.mx[axis] - cb.mn[axis]);
-    const int idx = (int)(kRegions * o);
-    return idx == kRegions ? kRegions - 1 : idx;
+    const float f = kRegions * o;   // (int)(7 o), 7 -> 6; undefined cases clamped as pt_mesh.cpp region_of
+    return !(f >= 0.0f) ? 0 : (f >= (float)kRegions ? kRegions - 1 : (int)f);
 }
 __device__ __forceinline__ Box prim_box(const PrimD& p) {
     Box b;

@@ -189,7 +189,11 @@ void tri_bounds(const pt_triangle& t, float* mn, float* mx) {   // Triangle::cal
 }
 
 // Fan-triangulate faces into world-space triangles of a new mesh geom.  Returns the geom id, or
-// a negated PT_ERR_* code (the scene is left unchanged on error).
+// a negated PT_ERR_* code (the scene is left unchanged on error).  World vertices must be finite
+// and below 2^126 in magnitude: beyond, the SAH build (BVH_tree.cpp:27-126) meets NaN or infinite
+// centres or extents, puts every triangle in one bucket and recurses on the same range without end
+// (the reference's behaviour there is undefined: an unbounded recursion); tinyobj reads no NaN, so
+// only a programmatic mesh or an extreme transform gets here.
 int append_mesh_impl(Scene& S, int32_t mat, const float* t, const float* r, const float* s, const float* pos, int32_t npos,
                 const float* nrm, int32_t nnrm, const float* uv, int32_t nuv, const int32_t* face_sizes, int32_t nfaces,
                 const ObjCorner* corners, int64_t ncorners) {
@@ -221,6 +225,10 @@ int append_mesh_impl(Scene& S, int32_t mat, const float* t, const float* r, cons
                     tri.uv[j][1] = uv[2 * (size_t)c[j]->vt + 1];
                 }
             }
+            for (int j = 0; j < 3; ++j)   // (see below)
+                for (int a = 0; a < 3; ++a)
+                    if (!(std::fabs(tri.v[j][a]) < 0x1p126f))
+                        return -fail(PT_ERR_ARG, "mesh vertex not finite, or beyond 2^126, after the transform");
             tri_bounds(tri, tri.bmin, tri.bmax);
             for (int a = 0; a < 3; ++a) {   // std::min / std::max (scene.cpp:146-160)
                 mn[a] = mn[a] < tri.bmin[a] ? mn[a] : tri.bmin[a];
@@ -306,9 +314,12 @@ struct BuildNode {
 
 constexpr int kRegions = 7;   // MAX_AREAS - 1
 
+// getOffsetBoxes -> bucket (BVH_tree.cpp:75-84): (int)(7 * offset), 7 -> 6.  Offsets outside
+// [0, 7] — where the reference's int conversion is undefined (NaN or infinite centres) or indexes
+// outside its buckets — are clamped; every defined case is unchanged (bvh_build.hip: the same).
 int region_of(const Box& cb, const Prim& p, int axis) {
-    int idx = (int)(kRegions * box_offset(cb, p.center, axis));
-    return idx == kRegions ? kRegions - 1 : idx;
+    const float f = kRegions * box_offset(cb, p.center, axis);
+    return !(f >= 0.0f) ? 0 : (f >= (float)kRegions ? kRegions - 1 : (int)f);
 }
 
 struct Builder {

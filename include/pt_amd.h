@@ -184,7 +184,8 @@ int pt_scene_add_geom(pt_scene* s, int32_t type, int32_t material_id, const floa
                       const float r[3], const float sc[3], int32_t* id_out);
 /* Mesh: object-space polygon soup, fan-triangulated (tinyobj triangulate=true), pre-transformed
  * to world space (scene.cpp:94-173).  face_sizes[f] vertices per face; idx_* per face-vertex
- * (-1 = absent), positions/normals (xyz), uvs (uv). */
+ * (-1 = absent), positions/normals (xyz), uvs (uv).  PT_ERR_ARG for a world vertex that is not
+ * finite or beyond 2^126 in magnitude (the SAH build would recurse without end on it). */
 int pt_scene_add_mesh(pt_scene* s, int32_t material_id, const float t[3], const float r[3],
                       const float sc[3], const float* positions, int32_t npos,
                       const float* normals, int32_t nnorm, const float* uvs, int32_t nuv,

@@ -118,3 +118,40 @@ def test_render_with_device_bvh_equals_oracle(gpu_device):
     o.set_camera((40, 40), 45.0, (0, 5, 10.5), (0, 5, 0), (0, 1, 0))
     ref = O.render_pass(o, O.flags(), 1, spp=2)[0]
     assert np.array_equal(img, ref)
+
+
+def _api_mesh_scene(verts, device):
+    """The same triangles through pt_scene_add_mesh (the OBJ parser, like tinyobj's, reads no
+    'nan'), the BVH built on the host or the device."""
+    from cuda_pathtracer_amd import Scene
+    sc = Scene()
+    m = sc.add_material(rgb=(0.9, 0.9, 0.9))
+    pos = np.ascontiguousarray(verts.reshape(-1), np.float32)
+    n = len(verts)
+    fs = np.full(n, 3, np.int32)
+    ip = np.arange(3 * n, dtype=np.int32)
+    gid = C.c_int32()
+    f3 = lambda v: (C.c_float * 3)(*v)  # noqa: E731
+    assert N.lib().pt_scene_add_mesh(sc.handle, m, f3([0, 0, 0]), f3([0, 0, 0]), f3([1, 1, 1]),
+                                     pos.ctypes.data_as(N._FP), 3 * n, None, 0, None, 0,
+                                     fs.ctypes.data_as(N._IP), n, ip.ctypes.data_as(N._IP), None, None,
+                                     C.byref(gid)) == 0
+    sc.set_camera((16, 16), 45.0, (0, 0, 10), (0, 0, 0))
+    sc.set_bvh_builder(device)
+    sc.finalize()
+    return sc
+
+
+@pytest.mark.parametrize("value", [1e30, -2e37])
+def test_large_coordinates_device_bvh_equals_host(gpu_device, value):
+    """Coordinates far from the rest (the loader accepts up to 2^126): bucket offsets of the
+    other centres collapse towards 0 and the SAH splits peel the far triangles off; both builds
+    agree."""
+    rng = np.random.default_rng(11)
+    v = rng.uniform(-3, 3, size=(300, 3, 3)).astype(np.float32)
+    v[17, :, 2] = value
+    v[200, 1, 0] = -value
+    h = _api_mesh_scene(v, False)
+    d = _api_mesh_scene(v, True)
+    assert not h.bvh_build_info()[0] and d.bvh_build_info()[0]
+    assert _tables(h) == _tables(d)

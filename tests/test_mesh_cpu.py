@@ -172,3 +172,20 @@ def test_random_triangles_100k_bvh_matches_oracle(tmp_path):
     s, o, pt, pn = _assert_same(path)
     assert len(pt) == 100_000
     assert int(pn[pn["sub_areas"] > 0]["sub_areas"].sum()) == 100_000
+
+
+@pytest.mark.parametrize("value", [np.nan, np.inf, 3e38])
+def test_non_finite_mesh_vertices_are_rejected(value):
+    """A world vertex that is not finite or beyond 2^126 would give the SAH build NaN or infinite
+    centres and extents, every triangle in one bucket and an unbounded recursion (the reference's
+    build has no defined result there); pt_scene_add_mesh refuses it with PT_ERR_ARG and leaves the
+    scene unchanged."""
+    sc = P.Scene()
+    m = sc.add_material(rgb=(1, 1, 1))
+    pos = np.array([0, 0, 0, 1, 0, 0, 0, 1, value], np.float32)
+    f3 = lambda v: (C.c_float * 3)(*v)  # noqa: E731
+    rc = N.lib().pt_scene_add_mesh(sc.handle, m, f3([0, 0, 0]), f3([0, 0, 0]), f3([1, 1, 1]),
+                                   pos.ctypes.data_as(N._FP), 3, None, 0, None, 0, (C.c_int32 * 1)(3), 1,
+                                   (C.c_int32 * 3)(0, 1, 2), None, None, None)
+    assert rc == 1   # PT_ERR_ARG (include/pt_amd.h)
+    assert sc.counts()[0] == 0 and sc.counts()[2] == 0
