@@ -44,8 +44,12 @@ constexpr int kBlock = 256;
 
 // Path state: three 16-byte planes (one dwordx4 load/store each, a wave moving 1 KiB contiguous
 // per instruction): a = (o.xyz, d.x), b = (d.yz, c.rg), c = (c.b, slot, bounces, 0).
+typedef float v2f __attribute__((ext_vector_type(2)));
+// a = (o, d.x), b = (d.yz, colour.rg), c = (colour.b, slot): every path of a launch has the same
+// number of bounces behind it (KArgs::bounce), so it is not stored.
 struct PathSoA {
-    v4f *a, *b, *c;
+    v4f *a, *b;
+    v2f* c;
 };
 struct HitSoA {   // sorted pipeline, textured scenes: texture coordinates of physical path j
     float* uv;    // [2 * P]
@@ -1041,18 +1045,19 @@ __device__ __forceinline__ void raygen(const CamDev& cam, const FlagsDev& fl, co
 #define PT_LD(p) __builtin_nontemporal_load(p)
 #define PT_ST(v, p) __builtin_nontemporal_store((v), (p))
 #endif
-__device__ __forceinline__ void load_path(const PathSoA& B, int i, PathReg& p) {
-    const v4f a = PT_LD(B.a + i), b = PT_LD(B.b + i), c = PT_LD(B.c + i);
+__device__ __forceinline__ void load_path(const PathSoA& B, int i, int bounce, PathReg& p) {
+    const v4f a = PT_LD(B.a + i), b = PT_LD(B.b + i);
+    const v2f c = PT_LD(B.c + i);
     p.o = F3(a[0], a[1], a[2]);
     p.d = F3(a[3], b[0], b[1]);
     p.c = F3(b[2], b[3], c[0]);
     p.slot = __float_as_int(c[1]);
-    p.bounces = __float_as_int(c[2]);
+    p.bounces = bounce;
 }
 __device__ __forceinline__ void store_path(const PathSoA& B, int i, const PathReg& p) {
     PT_ST((v4f{p.o.x, p.o.y, p.o.z, p.d.x}), B.a + i);
     PT_ST((v4f{p.d.y, p.d.z, p.c.x, p.c.y}), B.b + i);
-    PT_ST((v4f{p.c.z, __int_as_float(p.slot), __int_as_float(p.bounces), 0.0f}), B.c + i);
+    PT_ST((v2f{p.c.z, __int_as_float(p.slot)}), B.c + i);
 }
 
 // A path that terminated this bounce: its colour is final (finalGather, pathtrace.cu:347-356).
@@ -1128,7 +1133,7 @@ __device__ __forceinline__ void store_survivor(const PathSoA& B, int i, const Pa
     (void)with_slot;
     B.a[i] = v4f{p.o.x, p.o.y, p.o.z, p.d.x};
     B.b[i] = v4f{p.d.y, p.d.z, p.c.x, p.c.y};
-    B.c[i] = v4f{p.c.z, __int_as_float(p.slot), __int_as_float(p.bounces), 0.0f};
+    B.c[i] = v2f{p.c.z, __int_as_float(p.slot)};
 }
 
 // Trace one bounce: [raygen] -> intersect -> shade, one path per lane, no barriers and no
@@ -1153,7 +1158,7 @@ __global__ __launch_bounds__(kBlock) void k_trace(const KArgs A) {
         if (i < N) {
             PathReg p;
             if (FIRST) raygen(A.cam, A.fl, A.tile, i, p);
-            else load_path(A.in, i, p);
+            else load_path(A.in, i, A.bounce, p);
             uint32_t gm = ~0u;
             if (FIRST && A.cmask) {   // the wave's 64 consecutive slots: up to two pixel blocks, or four
                 const int np = A.tile.npix;   // when they wrap into the next iteration
@@ -2014,7 +2019,7 @@ __global__ __launch_bounds__(kBlock, FIRST || MESH ? 1 : PT_LATER_WAVES) void k_
             } else {
                 const int s = seg_walk(s_pre, nseg_in, seg, i);
                 q = s * chunk_in + (i - s_pre[s]);
-                load_path(A.in, q, p);
+                load_path(A.in, q, A.bounce, p);
             }
             STAMP(t1);
             Hit h;
@@ -2220,8 +2225,8 @@ __global__ __launch_bounds__(kBlock) void k_compact_paths(const KArgs A) {
 // bounce b has b bounces behind it.  Texture coordinates (textured scenes only) go to a side
 // array, double-buffered like the records.
 __device__ __forceinline__ v4f* srec(const PathSoA& B, int j) { return B.a + 2 * (size_t)(uint32_t)j; }
-__device__ __forceinline__ v4f* sdir(const PathSoA& B, int j) { return B.c + (size_t)(uint32_t)j; }
-__device__ __forceinline__ v4f* snrm(const PathSoA& B, int j) { return B.c + (B.b - B.a) + (size_t)(uint32_t)j; }
+__device__ __forceinline__ v4f* sdir(const PathSoA& B, int j) { return B.a + 2 * (B.b - B.a) + (size_t)(uint32_t)j; }
+__device__ __forceinline__ v4f* snrm(const PathSoA& B, int j) { return B.a + 3 * (B.b - B.a) + (size_t)(uint32_t)j; }
 
 struct SortArgs {
     int32_t* hslot;     // per (iteration, material, tile): first slot of its run (sort_hidx)
@@ -3146,7 +3151,7 @@ int build_cmask(pt_ctx* c) {
 int alloc_paths(pt_ctx* c, PathSoA& B, size_t P) {
     if (int rc = c->alloc(&B.a, 4 * P)) return rc;
     B.b = B.a + P;
-    B.c = B.a + 2 * P;
+    B.c = reinterpret_cast<v2f*>(B.a + 2 * P);
     return PT_OK;
 }
 
