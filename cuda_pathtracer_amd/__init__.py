@@ -10,10 +10,11 @@ from .pathtrace import (  # noqa: F401
     CUBE, MESH, SPHERE, GuiDataContainer, InitDataContainer, PathTracer, Scene, pathtrace, pathtraceFree,
     pathtraceInit, render, save_image, save_image_hdr, encode_hdr, tonemap)
 from . import distributed  # noqa: F401
-from .stream_compaction import (Efficient, compact_device, live_indices_device, partition_device,  # noqa: F401
-                                scan_device)
+from .stream_compaction import (CPU, Efficient, Naive, Thrust, compact_device, live_indices_device,  # noqa: F401
+                                naive_scan_device, partition_device, scan_device, thrust_scan_device)
 
-__all__ = ["Scene", "PathTracer", "GuiDataContainer", "Efficient", "scan_device", "compact_device",
+__all__ = ["Scene", "PathTracer", "GuiDataContainer", "Efficient", "CPU", "Naive", "Thrust", "scan_device",
+           "compact_device", "naive_scan_device", "thrust_scan_device",
            "partition_device", "live_indices_device", "render", "save_image", "save_image_hdr", "encode_hdr", "tonemap", "pathtraceInit",
            "pathtraceFree", "pathtrace",
            "InitDataContainer", "lib", "LIB_PATH", "NativeLibraryError", "PtError"]

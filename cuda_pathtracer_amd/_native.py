@@ -94,6 +94,13 @@ SIGNATURES = {
     "sc_efficient_scan": (_I, [C.c_int, _P, _P]),
     "sc_efficient_compact": (_I, [C.c_int, _P, _P, _IP]),
     "sc_timer_gpu_ms": (C.c_float, []),
+    "sc_cpu_scan": (_I, [C.c_int, _P, _P]),
+    "sc_cpu_compact_without_scan": (_I, [C.c_int, _P, _P, _IP]),
+    "sc_cpu_compact_with_scan": (_I, [C.c_int, _P, _P, _IP]),
+    "sc_naive_scan_i32": (_I, [_P, _P, C.c_int64, _P, _P]),
+    "sc_thrust_scan_i32": (_I, [_P, _P, C.c_int64, _P]),
+    "sc_naive_scan": (_I, [C.c_int, _P, _P]),
+    "sc_thrust_scan": (_I, [C.c_int, _P, _P]),
     "sc_set_tile_schedule": (_I, [_I]),
     "sc_workspace_check": (_I, [_P]),
     "sc_workspace_error_word": (_P, [_P]),

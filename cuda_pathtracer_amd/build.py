@@ -26,7 +26,7 @@ ARCH = "gfx950"
 # -ffp-contract=off: the evaluation contract — every multiply-add is two
 # correctly-rounded operations unless the source writes fmaf(); keeps GPU == oracle bitwise.
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall", "-Wno-unused-function"]
-DEVICE_SRCS = ["sc_kernels.hip", "pt_kernels.hip", "bvh_build.hip"]
+DEVICE_SRCS = ["sc_kernels.hip", "sc_variants.hip", "pt_kernels.hip", "bvh_build.hip"]
 # pt_kernels.hip: no SLP vectorisation.  Packing independent f32 ops into v_pk_* pairs needed
 # register pairs and moves: k_bounce took 79 VGPRs (6 waves/SIMD) instead of 60 (8 waves), and
 # measured 30.8k vs 32.7k Mray/s on the bench (same box, alternating runs; same bits).

@@ -654,6 +654,13 @@ int host_op(int n, int* odata, const int* idata, int* count_out) {
 
 }  // namespace
 
+// Shared with sc_variants.hip (the CPU / Naive / Thrust entry points): one error message and one
+// "previous operation" timer per thread for the whole sc_* ABI.
+namespace sc_internal {
+int fail(int code, const std::string& msg) { return ::fail(code, msg); }
+void set_timer_ms(float ms) { g_timer_ms = ms; }
+}  // namespace sc_internal
+
 extern "C" {
 
 const char* sc_last_error(void) { return g_err.c_str(); }

@@ -1,4 +1,4 @@
-// StreamCompaction::Efficient over the C ABI (see stream_compaction.h).
+// StreamCompaction::{Efficient, CPU, Naive, Thrust} over the C ABI (see stream_compaction.h).
 #include "stream_compaction.h"
 
 #include <hip/hip_runtime.h>
@@ -80,4 +80,66 @@ int compact(int n, int* odata, const int* idata) {
 }
 
 }  // namespace Efficient
+
+namespace CPU {
+
+Common::PerformanceTimer& timer() {
+    static Common::PerformanceTimer t;
+    return t;
+}
+
+void scan(int n, int* odata, const int* idata) {
+    timer().startCpuTimer();
+    const int rc = sc_cpu_scan(n, odata, idata);
+    timer().endCpuTimer();
+    check(rc, "CPU::scan");
+}
+
+int compactWithoutScan(int n, int* odata, const int* idata) {
+    int count = 0;
+    timer().startCpuTimer();
+    const int rc = sc_cpu_compact_without_scan(n, odata, idata, &count);
+    timer().endCpuTimer();
+    check(rc, "CPU::compactWithoutScan");
+    return count;
+}
+
+int compactWithScan(int n, int* odata, const int* idata) {
+    int count = 0;
+    timer().startCpuTimer();
+    const int rc = sc_cpu_compact_with_scan(n, odata, idata, &count);
+    timer().endCpuTimer();
+    check(rc, "CPU::compactWithScan");
+    return count;
+}
+
+}  // namespace CPU
+
+namespace Naive {
+
+Common::PerformanceTimer& timer() {
+    static Common::PerformanceTimer t;
+    return t;
+}
+
+void scan(int n, int* odata, const int* idata) {
+    check(sc_naive_scan(n, odata, idata), "Naive::scan");
+    timer().setGpuElapsed(sc_timer_gpu_ms());
+}
+
+}  // namespace Naive
+
+namespace Thrust {
+
+Common::PerformanceTimer& timer() {
+    static Common::PerformanceTimer t;
+    return t;
+}
+
+void scan(int n, int* odata, const int* idata) {
+    check(sc_thrust_scan(n, odata, idata), "Thrust::scan");
+    timer().setGpuElapsed(sc_timer_gpu_ms());
+}
+
+}  // namespace Thrust
 }  // namespace StreamCompaction

@@ -2,9 +2,13 @@
 // include/sc_amd.h (libpt_amd.so).  Same names, argument meaning and error behaviour as
 //   path_tracer/stream_compaction/efficient.h:5-13   (Efficient::timer / scan / compact)
 //   path_tracer/stream_compaction/common.h:46-130    (Common::PerformanceTimer)
+//   path_tracer/stream_compaction/cpu.h:7-14         (CPU::timer / scan / compactWithoutScan / compactWithScan)
+//   path_tracer/stream_compaction/naive.h:7-10       (Naive::timer / scan)
+//   path_tracer/stream_compaction/thrust.h:7-10      (Thrust::timer / scan)
 //   path_tracer/stream_compaction/common.cu:3-15     (checkCUDAError: print and exit(1))
-// Only Efficient is on the path tracer's hot path; CPU:: is the test oracle (oracle/), and the
-// Naive/Thrust teaching variants are out of scope.
+// Only Efficient is on the path tracer's hot path; the other three let the reference's self-test
+// (stream_compaction/src/main.cpp) compare the four implementations.  CPU:: runs the library's
+// own host loops (sc_cpu_*), not the test oracle.
 //
 // Pointers may be host or device memory, like the reference (pathtrace.cu:397 hands device
 // pointers to Efficient::scan through UVA): device pointers run on the null stream without
@@ -49,6 +53,28 @@ private:
 };
 
 }  // namespace Common
+
+namespace CPU {
+StreamCompaction::Common::PerformanceTimer& timer();
+// Exclusive scan on the host (wrapping int32); odata may equal idata.
+void scan(int n, int* odata, const int* idata);
+// The non-zero elements of idata in order; returns how many.
+int compactWithoutScan(int n, int* odata, const int* idata);
+// Map to 0/1, exclusive scan, scatter; returns how many were kept.
+int compactWithScan(int n, int* odata, const int* idata);
+}  // namespace CPU
+
+namespace Naive {
+StreamCompaction::Common::PerformanceTimer& timer();
+// Hillis & Steele exclusive scan on the device (ceil(log2 n) launches, then the shift).
+void scan(int n, int* odata, const int* idata);
+}  // namespace Naive
+
+namespace Thrust {
+StreamCompaction::Common::PerformanceTimer& timer();
+// rocThrust's exclusive_scan.
+void scan(int n, int* odata, const int* idata);
+}  // namespace Thrust
 
 namespace Efficient {
 StreamCompaction::Common::PerformanceTimer& timer();

@@ -1,14 +1,18 @@
 """Python mirror of the reference's StreamCompaction API, backed by the HIP kernels.
 
-Reference: path_tracer/stream_compaction/{efficient,common}.{h,cu}.
+Reference: path_tracer/stream_compaction/{efficient,cpu,naive,thrust,common}.{h,cu}.
   StreamCompaction::Efficient::scan(n, odata, idata)     -> Efficient.scan
   StreamCompaction::Efficient::compact(n, odata, idata)  -> Efficient.compact
   StreamCompaction::Efficient::timer()                   -> Efficient.timer()
+  StreamCompaction::CPU::{scan, compactWithoutScan, compactWithScan}, CPU::timer()  -> CPU
+  StreamCompaction::Naive::scan, Naive::timer()          -> Naive
+  StreamCompaction::Thrust::scan, Thrust::timer()        -> Thrust
 The host-array calls keep the reference semantics (host arrays in, host arrays out, GPU time of
 the device work only).  The device-tensor functions (scan_device, compact_device,
-partition_device) take torch tensors already resident on the GPU and never synchronise.
-StreamCompaction::CPU is deliberately absent: the CPU version is the test oracle (oracle/), and
-this package has no CPU fallback.
+partition_device, naive_scan_device, thrust_scan_device) take torch tensors already resident on
+the GPU and never synchronise.  CPU's functions are the library's own host loops (sc_cpu_*), the
+reference's CPU namespace; they are not a fallback of any device path and not the test oracle
+(oracle/ checks them).
 """
 from __future__ import annotations
 
@@ -27,6 +31,19 @@ class _Timer:
 
 
 _TIMER = _Timer()
+
+
+class _CpuTimer:
+    """PerformanceTimer's CPU side (common.h:63-80): wall time of the previous CPU:: call."""
+
+    def __init__(self):
+        self._ms = 0.0
+
+    def getCpuElapsedTimeForPreviousOperation(self) -> float:  # noqa: N802 (reference name)
+        return self._ms
+
+
+_CPU_TIMER = _CpuTimer()
 
 
 def _i32(a: np.ndarray, name: str) -> np.ndarray:
@@ -57,6 +74,73 @@ class Efficient:
         cnt = C.c_int32(0)
         check_sc(lib().sc_efficient_compact(n, odata.ctypes.data, idata.ctypes.data, C.byref(cnt)))
         return int(cnt.value)
+
+
+def _host_args(n, odata, idata):
+    _i32(odata, "odata"); _i32(idata, "idata")
+    if n < 0 or n > len(idata) or n > len(odata):
+        raise ValueError("n out of range")
+
+
+class CPU:
+    """StreamCompaction::CPU (cpu.h:9-13): sequential host loops in libpt_amd.so (sc_cpu_*)."""
+
+    @staticmethod
+    def timer() -> _CpuTimer:
+        return _CPU_TIMER
+
+    @staticmethod
+    def _timed(fn, *args):
+        import time
+        t0 = time.perf_counter()
+        rc = fn(*args)
+        _CPU_TIMER._ms = (time.perf_counter() - t0) * 1e3
+        check_sc(rc)
+
+    @staticmethod
+    def scan(n: int, odata: np.ndarray, idata: np.ndarray) -> None:
+        _host_args(n, odata, idata)
+        CPU._timed(lib().sc_cpu_scan, n, odata.ctypes.data, idata.ctypes.data)
+
+    @staticmethod
+    def compactWithoutScan(n: int, odata: np.ndarray, idata: np.ndarray) -> int:  # noqa: N802
+        _host_args(n, odata, idata)
+        cnt = C.c_int32(0)
+        CPU._timed(lib().sc_cpu_compact_without_scan, n, odata.ctypes.data, idata.ctypes.data, C.byref(cnt))
+        return int(cnt.value)
+
+    @staticmethod
+    def compactWithScan(n: int, odata: np.ndarray, idata: np.ndarray) -> int:  # noqa: N802
+        _host_args(n, odata, idata)
+        cnt = C.c_int32(0)
+        CPU._timed(lib().sc_cpu_compact_with_scan, n, odata.ctypes.data, idata.ctypes.data, C.byref(cnt))
+        return int(cnt.value)
+
+
+class Naive:
+    """StreamCompaction::Naive (naive.h:9): Hillis & Steele on the device (sc_naive_scan)."""
+
+    @staticmethod
+    def timer() -> _Timer:
+        return _TIMER
+
+    @staticmethod
+    def scan(n: int, odata: np.ndarray, idata: np.ndarray) -> None:
+        _host_args(n, odata, idata)
+        check_sc(lib().sc_naive_scan(n, odata.ctypes.data, idata.ctypes.data))
+
+
+class Thrust:
+    """StreamCompaction::Thrust (thrust.h:9): rocThrust's exclusive_scan (sc_thrust_scan)."""
+
+    @staticmethod
+    def timer() -> _Timer:
+        return _TIMER
+
+    @staticmethod
+    def scan(n: int, odata: np.ndarray, idata: np.ndarray) -> None:
+        _host_args(n, odata, idata)
+        check_sc(lib().sc_thrust_scan(n, odata.ctypes.data, idata.ctypes.data))
 
 
 def _stream_ptr(stream) -> int:
@@ -138,3 +222,25 @@ def live_indices_device(d_flags, d_idx=None, stream=None, check: bool = False):
                                         _stream_ptr(stream)))
     _checked(stream, check)
     return d_idx, cnt
+
+
+def naive_scan_device(d_in, d_out=None, d_tmp=None, stream=None):
+    """Naive::scan on device tensors (sc_naive_scan_i32): d_in unchanged, d_tmp = n int32 of scratch."""
+    import torch
+    _check_dev_i32(d_in, "d_in")
+    d_out = torch.empty_like(d_in) if d_out is None else d_out
+    d_tmp = torch.empty_like(d_in) if d_tmp is None else d_tmp
+    _check_dev_i32(d_out, "d_out"); _check_dev_i32(d_tmp, "d_tmp")
+    check_sc(lib().sc_naive_scan_i32(d_in.data_ptr(), d_out.data_ptr(), d_in.numel(), d_tmp.data_ptr(),
+                                     _stream_ptr(stream)))
+    return d_out
+
+
+def thrust_scan_device(d_in, d_out=None, stream=None):
+    """Thrust::scan on device tensors (sc_thrust_scan_i32: rocThrust exclusive_scan)."""
+    import torch
+    _check_dev_i32(d_in, "d_in")
+    d_out = torch.empty_like(d_in) if d_out is None else d_out
+    _check_dev_i32(d_out, "d_out")
+    check_sc(lib().sc_thrust_scan_i32(d_in.data_ptr(), d_out.data_ptr(), d_in.numel(), _stream_ptr(stream)))
+    return d_out

@@ -8,8 +8,14 @@
  *   Common::kernMapToBoolean / kernScatter  common.cu:25-46       -> fused into sc_compact_i32
  *   mark_valid + scan + keep  path_tracer/src/pathtrace.cu:359-407 -> sc_partition_i32 (stable partition)
  *                                                                    and sc_partition_indices (live index list)
- * The reference's CPU:: functions (cpu.h:9-13) are the test ORACLE (oracle/sc_oracle.cpp), not part
- * of this product library: there is no CPU fallback here.
+ * The reference's other three namespaces (sc_variants.hip; not on the path tracer's hot path, which
+ * calls Efficient only — they let the reference's self-test, stream_compaction/src/main.cpp:31-85,
+ * compare the four implementations against the C++ mirror):
+ *   CPU::scan / compactWithoutScan / compactWithScan  cpu.h:9-13 / cpu.cu:16-79 -> sc_cpu_*
+ *   Naive::scan                                       naive.h:9 / naive.cu:14-66 -> sc_naive_scan(_i32)
+ *   Thrust::scan                                      thrust.h:9 / thrust.cu:14-28 -> sc_thrust_scan(_i32)
+ * sc_cpu_* are host loops of their own, not the test oracle (oracle/sc_oracle.cpp checks them) and
+ * not a fallback of the device entry points: nothing here falls back to the CPU.
  *
  * Differences from the reference, by design:
  *   - every entry point returns a status code (SC_OK / SC_ERR_*) instead of exit()ing
@@ -91,6 +97,26 @@ const uint32_t* sc_workspace_error_word(const void* workspace);
  * 1: tiles claimed in order from a ticket — correct whatever else runs on the GPU, ~15% slower.
  * The environment variable PT_AMD_SCHEDULE=claim selects 1 at load time. */
 int sc_set_tile_schedule(int32_t claimed);
+
+/* ---- the reference's CPU / Naive / Thrust namespaces (sc_variants.hip) ----------------------- */
+
+/* CPU::scan (cpu.cu:16-33): exclusive prefix sum on the host, wrapping; odata may equal idata. */
+int sc_cpu_scan(int n, int* odata, const int* idata);
+/* CPU::compactWithoutScan (cpu.cu:40-52): the non-zero elements in order; *count_out = how many. */
+int sc_cpu_compact_without_scan(int n, int* odata, const int* idata, int* count_out);
+/* CPU::compactWithScan (cpu.cu:59-79): map to 0/1, exclusive scan, scatter; *count_out = kept. */
+int sc_cpu_compact_with_scan(int n, int* odata, const int* idata, int* count_out);
+
+/* Naive::scan (naive.cu:14-66): Hillis & Steele, ceil(log2 n) launches ping-ponging between d_out
+ * and d_tmp (n int32 of device scratch), then the inclusive -> exclusive shift.  d_in is left
+ * unchanged; d_in, d_out and d_tmp must not alias (SC_ERR_ARG).  Asynchronous on `stream`. */
+int sc_naive_scan_i32(const int32_t* d_in, int32_t* d_out, int64_t n, int32_t* d_tmp, void* stream);
+/* Thrust::scan (thrust.cu:14-28): rocThrust's exclusive_scan on `stream` (d_out may equal d_in). */
+int sc_thrust_scan_i32(const int32_t* d_in, int32_t* d_out, int64_t n, void* stream);
+/* Host-array forms with the reference's signatures (upload, device work timed by sc_timer_gpu_ms,
+ * download), like sc_efficient_scan. */
+int sc_naive_scan(int n, int* odata, const int* idata);
+int sc_thrust_scan(int n, int* odata, const int* idata);
 
 /* Elapsed device time (ms) of the previous host-pointer operation
  * (PerformanceTimer::getGpuElapsedTimeForPreviousOperation, common.h:98-101). */

@@ -1,8 +1,9 @@
 // C++ restatement of the reference's own stream-compaction self-test
 // (stream_compaction/src/main.cpp:14-146 + testing_helpers.hpp) against the C++ host mirror
 // (cuda_pathtracer_amd/host/stream_compaction.h -> libpt_amd.so).  The expected values come
-// from the CPU oracle (oracle/sc_oracle.cpp, test infrastructure) instead of CPU:: — same roles:
-// b = CPU result, c = device result, printCmpResult after each case.  Exit status != 0 on any
+// from the CPU oracle (oracle/sc_oracle.cpp, test infrastructure), and all four namespaces of the
+// mirror (CPU, Naive, Efficient, Thrust) are checked against it: b = expected, c = result,
+// printCmpResult after each case.  Exit status != 0 on any
 // mismatch.  Inputs are seeded (the reference uses time()).
 //
 //   test_stream_compaction [SIZE_LOG2=20]
@@ -14,6 +15,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <random>
 #include <vector>
 
@@ -97,6 +99,42 @@ int main(int argc, char** argv) {
     printElapsedTime(Efficient::timer().getGpuElapsedTimeForPreviousOperation(), "(HIP Measured)");
     printCmpResult(NPOT, b, c);
 
+    // the other three namespaces (main.cpp:31-85), each against the oracle
+    for (int npot = 0; npot < 2; ++npot) {
+        const int n = npot ? NPOT : SIZE;
+        oracle_scan(n, b, a);
+        const char* tag = npot ? "non-power-of-two" : "power-of-two";
+        char desc[96];
+        zeroArray(SIZE, c);
+        std::snprintf(desc, sizeof desc, "cpu scan, %s", tag);
+        printDesc(desc);
+        CPU::scan(n, c, a);
+        printElapsedTime(CPU::timer().getCpuElapsedTimeForPreviousOperation(), "(std::chrono Measured)");
+        printCmpResult(n, b, c);
+        zeroArray(SIZE, c);
+        std::snprintf(desc, sizeof desc, "naive scan, %s", tag);
+        printDesc(desc);
+        Naive::scan(n, c, a);
+        printElapsedTime(Naive::timer().getGpuElapsedTimeForPreviousOperation(), "(HIP Measured)");
+        printCmpResult(n, b, c);
+        zeroArray(SIZE, c);
+        std::snprintf(desc, sizeof desc, "thrust scan, %s", tag);
+        printDesc(desc);
+        Thrust::scan(n, c, a);
+        printElapsedTime(Thrust::timer().getGpuElapsedTimeForPreviousOperation(), "(HIP Measured)");
+        printCmpResult(n, b, c);
+    }
+    for (int n : {1, 2, 3, 5, 64, 65, 1000}) {   // naive: ceil(log2 n) passes, odd and even
+        if (n > SIZE) continue;
+        oracle_scan(n, b, a);
+        zeroArray(n, c);
+        Naive::scan(n, c, a);
+        char desc[64];
+        std::snprintf(desc, sizeof desc, "naive scan, n = %d", n);
+        printDesc(desc);
+        printCmpResult(n, b, c);
+    }
+
     // small sizes the reference's padded scan could not do
     for (int n : {1, 2, 3, 7, 64, 65, 8191, 8193}) {
         if (n > SIZE) continue;
@@ -122,6 +160,21 @@ int main(int argc, char** argv) {
         printCmpLenResult(k, expectedCount, b, w.data());
     }
     std::vector<int> bn(c, c + SIZE);
+    for (int npot = 0; npot < 2; ++npot) {   // CPU::compactWithoutScan / compactWithScan (main.cpp:103-126)
+        const int n = npot ? NPOT : SIZE;
+        const int* expect = npot ? bn.data() : b;
+        const int ecount = npot ? expectedNPOT : expectedCount;
+        std::vector<int> w(SIZE, 0);
+        printDesc(npot ? "cpu compact without scan, non-power-of-two" : "cpu compact without scan, power-of-two");
+        int k = CPU::compactWithoutScan(n, w.data(), a);
+        printElapsedTime(CPU::timer().getCpuElapsedTimeForPreviousOperation(), "(std::chrono Measured)");
+        printCmpLenResult(k, ecount, expect, w.data());
+        std::fill(w.begin(), w.end(), 0);
+        printDesc(npot ? "cpu compact with scan, non-power-of-two" : "cpu compact with scan, power-of-two");
+        k = CPU::compactWithScan(n, w.data(), a);
+        printElapsedTime(CPU::timer().getCpuElapsedTimeForPreviousOperation(), "(std::chrono Measured)");
+        printCmpLenResult(k, ecount, expect, w.data());
+    }
 
     zeroArray(SIZE, c);
     printDesc("work-efficient compact, power-of-two");
