@@ -1337,6 +1337,9 @@ constexpr int kFoldBatch = PT_FOLD_BATCH;   // k_traverse4: task results read pe
 #ifndef PT_T4_OVERLAP
 #define PT_T4_OVERLAP 1  // k_traverse4: a leaf sent out whole and the node after it in one trip
 #endif
+#ifndef PT_T4_PUSH
+#define PT_T4_PUSH 1     // k_traverse4: branch-free pushes in trips whose stack is LDS-only
+#endif
 #ifndef PT_T4_ASSIGN
 #define PT_T4_ASSIGN 0   // k_traverse4 leaf tasks: 0 owner tag + ballot + ds_bpermute; 1 task slots written by owners
 #endif
@@ -1869,13 +1872,29 @@ __global__ __launch_bounds__(kBlock, PT_T4_WAVES) void k_traverse4(const KArgs A
                 hm = ((hm & 3u) << 2) | (hm >> 2);
             }
             // push the later hits (farthest first), continue with the first
-            int nx = 0;
-            bool got = false;
-            if (hm & 8u) { nx = c3; got = true; }
-            if (hm & 4u) { if (got) push(nx); nx = c2; got = true; }
-            if (hm & 2u) { if (got) push(nx); nx = c1; got = true; }
-            if (hm & 1u) { if (got) push(nx); nx = c0; got = true; }
-            next = got ? nx : pop();
+#if PT_T4_PUSH
+            if (fast) {   // (wave-uniform) LDS rows only: the pushes without branches
+                // hit slot k after the first hit goes to top + (hit slots above k): the farthest
+                // deepest, as the sequential pushes below place them
+                const uint32_t m = (uint32_t)__builtin_popcount(hm);
+                const int f = __builtin_ctz(hm | 16u);   // first hit (4: none)
+                if (((hm >> 1) & 1u) && f < 1) col[(top + __builtin_popcount(hm >> 2)) * kBlock] = c1;
+                if (((hm >> 2) & 1u) && f < 2) col[(top + __builtin_popcount(hm >> 3)) * kBlock] = c2;
+                if (((hm >> 3) & 1u) && f < 3) col[top * kBlock] = c3;
+                const int pn = top > 0 ? col[max(top - 1, 0) * kBlock] : kWalkDone;   // (m == 0: pop)
+                next = m == 0 ? pn : (f == 0 ? c0 : (f == 1 ? c1 : (f == 2 ? c2 : c3)));
+                top += m > 0 ? (int)m - 1 : (top > 0 ? -1 : 0);
+            } else
+#endif
+            {
+                int nx = 0;
+                bool got = false;
+                if (hm & 8u) { nx = c3; got = true; }
+                if (hm & 4u) { if (got) push(nx); nx = c2; got = true; }
+                if (hm & 2u) { if (got) push(nx); nx = c1; got = true; }
+                if (hm & 1u) { if (got) push(nx); nx = c0; got = true; }
+                next = got ? nx : pop();
+            }
         }
         // ---- triangle tests ----
         if (is_task) {

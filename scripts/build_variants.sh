@@ -14,6 +14,6 @@ wait
 for v in $VARIANTS; do
   name=${v%%:*}
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $B/libpt_amd_$name.so $B/pt_kernels_$name.o \
-      $B/sc_kernels.hip.o $B/bvh_build.hip.o $B/pt_scene.cpp.o $B/pt_mesh.cpp.o $B/pt_image.cpp.o $B/pt_jpeg.cpp.o -lz
+      $B/sc_kernels.hip.o $B/sc_variants.hip.o $B/bvh_build.hip.o $B/pt_scene.cpp.o $B/pt_mesh.cpp.o $B/pt_image.cpp.o $B/pt_jpeg.cpp.o -lz
   echo $B/libpt_amd_$name.so
 done
