@@ -2685,10 +2685,22 @@ __global__ __launch_bounds__(kBlock) void k_hist_apply(const int32_t* __restrict
 }
 
 // spp > 1: add the per-slot colours in sample order (finalGather as `spp` sequential iterations).
+#ifndef PT_FIN_BATCH
+#define PT_FIN_BATCH 16
+#endif
 __global__ void k_finalize_spp(float* __restrict__ image, const v4f* __restrict__ col, int npix, int spp) {
     for (int lp = blockIdx.x * blockDim.x + threadIdx.x; lp < npix; lp += gridDim.x * blockDim.x) {
         float r = image[3 * (size_t)lp], g = image[3 * (size_t)lp + 1], b = image[3 * (size_t)lp + 2];
-        for (int s = 0; s < spp; ++s) {
+        int s = 0;
+        // the loads of a batch of samples issued together (independent), the adds in sample order
+        for (; s + PT_FIN_BATCH <= spp; s += PT_FIN_BATCH) {
+            v4f c[PT_FIN_BATCH];
+#pragma unroll
+            for (int k = 0; k < PT_FIN_BATCH; ++k) c[k] = PT_LD(col + (size_t)(s + k) * npix + lp);
+#pragma unroll
+            for (int k = 0; k < PT_FIN_BATCH; ++k) { r += c[k][0]; g += c[k][1]; b += c[k][2]; }
+        }
+        for (; s < spp; ++s) {
             const v4f c = PT_LD(col + (size_t)s * npix + lp);
             r += c[0]; g += c[1]; b += c[2];
         }
