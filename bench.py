@@ -3,8 +3,8 @@
 Workload (BASELINE.json configs[1]): path_tracer/scenes/cornell.json as-is — 800x800, DEPTH 8,
 default flags.  A step renders a FIXED 256 samples per pixel of the whole image (strong scaling,
 the default): on N GPUs (one process per GPU, torchrun) rank r owns the image rows y % N == r and
-traces its rows' 256 iterations as passes of `--spp` iterations (default 128 at N = 1: 2 passes;
-one pass of 256 from N = 2), so the work per step is the same at every N and the driver's 1/2/4/8
+traces its rows' 256 iterations as passes of `--spp` iterations (default: one pass of 256 at every
+N; 2 x 128 at N = 1 measured 0.5% slower), so the work per step is the same at every N and the driver's 1/2/4/8
 values measure speed-up.  Batching iterations into one pass is bit-identical to tracing them one
 pass at a time (tests/test_render_gpu.py::test_batched_pass_equals_sequential_passes); --spp 1
 --samples 1 is exactly the reference's pathtrace() per step.  --scaling weak: a step is one pass of
@@ -340,7 +340,7 @@ def main() -> None:
     ap.add_argument("--samples", type=int, default=256, help="strong scaling: samples per pixel per step")
     args = ap.parse_args()
     if args.spp is None:   # iterations per pass, measured per workload
-        args.spp = {"cornell": 128, "cornell_hd_sorted": 256, "multi_object_4k": 64, "random_triangles_100k": 32}[args.config]
+        args.spp = {"cornell": 256, "cornell_hd_sorted": 256, "multi_object_4k": 128, "random_triangles_100k": 128}[args.config]
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -11,8 +11,8 @@ run() {   # name, extra args
 }
 run cornell_hd_sorted --steps 10 || exit 1
 run multi_object_4k --steps 5 || exit 1
-run random_triangles_100k --steps 2 --spp 32 --samples 32 || exit 1
-run random_triangles_100k --steps 2 --spp 32 --samples 32 --bvh-cull || exit 1
+run random_triangles_100k --steps 2 --spp 128 --samples 128 || exit 1
+run random_triangles_100k --steps 2 --spp 128 --samples 128 --bvh-cull || exit 1
 python3 - <<'PY'
 import json
 for line in open("gpurun_out/configs.jsonl"):
