@@ -23,8 +23,8 @@ hit read 28 + path read 48 + write 48 + compaction 8) x the segments that launch
 (DESIGN.md §4).  roofline.frac = those bytes / the average launch duration / 8 TB/s, per launch;
 roofline.step_frac = the same bytes of every bounce of a step / ms_per_step / 8 TB/s.  Batched
 passes run two lanes of iterations whose launches overlap; the bytes over the union of the launch
-intervals are reported separately (roofline.aggregate).  The fused kernel itself needs only 44 B in
-+ 44 B per survivor + 24 B per emissive hit (kernel_min_bytes).
+intervals are reported separately (roofline.aggregate).  The fused kernel itself needs only 40 B in
++ 40 B per survivor + 24 B per emissive hit (kernel_min_bytes; path planes of 16 + 16 + 8 B).
 Measured in the same run (N = 1): rocprofv3 --pmc passes over the same workload (scripts/pmc.py)
 give the kernel's fabric traffic per launch (roofline.traffic, FETCH_SIZE x 2 + WRITE_SIZE) and its
 VALU wave-instructions (roofline.valu_issue: against the chip's VALU issue rate, 256 CUs x 4 SIMDs x
@@ -50,9 +50,10 @@ sys.path.insert(0, str(ROOT))
 
 METRIC = "Mray/s (paths×bounces/s) on Cornell scene + scan GB/s vs HBM peak, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+HBM_COPY_GBS = 6290.0          # same guide: measured float4 copy, the achievable streaming rate (79%)
 VALU_PEAK = 256 * 4 * 2.4e9 / 2   # wave64 VALU instructions/s: 4 SIMD-32 per CU, 2 cycles each (same guide)
 SEGMENT_BYTES = 184            # SURVEY.md §8d algorithmic bytes per traced segment
-PATH_BYTES = 44                # fused kernel's path state: o(12) d(12) c(12) slot(4) bounces(4)
+PATH_BYTES = 40                # fused kernel's path state: planes (o, d.x) 16 + (d.yz, c.rg) 16 + (c.b, slot) 8
 FB_RMW_BYTES = 24              # float3 read + write
 
 
@@ -174,7 +175,9 @@ def scan_bench(torch, dev, n: int, reps: int) -> dict:
     gbs = 8.0 * n / (ms * 1e-3) / 1e9
     return {"n": n, "ms": ms, "ms_min": times[0], "GB/s": gbs, "verified": ok,
             "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": gbs / HBM_PEAK_GBS}}
+                         "frac": gbs / HBM_PEAK_GBS, "copy_ceiling": HBM_COPY_GBS,
+                         "frac_of_copy_ceiling": gbs / HBM_COPY_GBS,
+                         "copy_ceiling_source": "MI355X_MICROARCH.md: float4 copy measured at 6.29 TB/s"}}
 
 
 def compact_bench(torch, dev, n: int, reps: int) -> dict:
@@ -200,6 +203,27 @@ def compact_bench(torch, dev, n: int, reps: int) -> dict:
     ok = kept == int((a != 0).sum().item()) and bool(torch.equal(out[:kept], a[a != 0]))
     gbs = (4.0 * n + 4.0 * kept) / (ms * 1e-3) / 1e9
     return {"n": n, "kept": kept, "ms": ms, "GB/s": gbs, "frac": gbs / HBM_PEAK_GBS, "verified": ok}
+
+
+def dropin_bench(scene_path: str, iters: int = 50, warmup: int = 3) -> dict:
+    """The drop-in call sequence a reference caller gets: `iters` calls of the C++ mirror's
+    pathtrace(nullptr, 0, it) (host/pathtrace.cpp: the per-call pt_set_flags of pathtrace.cu:438-463,
+    one iteration, and the synchronous image copy of pathtrace.cu:524), as main.cpp:114-168's loop
+    issues them (host/dropin_bench.cpp through libpt_dropin.so)."""
+    import ctypes as C
+    lib = C.CDLL(str(ROOT / "cuda_pathtracer_amd" / "libpt_dropin.so"))
+    fn = lib.pt_dropin_bench
+    fn.restype = C.c_int
+    fn.argtypes = [C.c_char_p, C.c_int, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+    ms, seg, syncs = C.c_double(), C.c_uint64(), C.c_uint64()
+    rc = fn(str(scene_path).encode(), warmup, iters, C.byref(ms), C.byref(seg), C.byref(syncs))
+    if rc != 0:
+        return {"error": f"pt_dropin_bench rc={rc}"}
+    return {"value": seg.value / (ms.value * 1e-3) / 1e6, "unit": "Mray/s", "calls": iters,
+            "ms_per_call": ms.value / iters, "segments": seg.value, "flag_syncs": syncs.value,
+            "definition": f"{iters} calls of the C++ mirror's pathtrace(nullptr, 0, it) on the same scene (one "
+                          "iteration each: per-call pt_set_flags, pt_render_pass, synchronous 7.7 MB image copy "
+                          "to the host, as pathtrace.cu:438-524), after {warmup} warm-up calls; segments / wall time"}
 
 
 def _pmc_leg(args, scene_path, spp_pass, sorted_, avg_ms, kernel_prefix, seg_per_launch, busy_ms, launches,
@@ -328,14 +352,16 @@ def main() -> None:
                     help="BASELINE.json workload: cornell (configs[1], the default line) or configs 3-5 "
                          "generated by cuda_pathtracer_amd.scenes")
     ap.add_argument("--bvh-cull", action="store_true", help="pt_flags.bvh_cull extension (mesh scenes)")
+    ap.add_argument("--no-dropin", action="store_true",
+                    help="skip the drop-in leg (50 per-iteration pathtrace() calls of the C++ mirror, N = 1)")
     ap.add_argument("--spp", type=int, default=None,
                     help="iterations per pass and GPU-share: a pass traces spp x N iterations of the rank's rows "
                          "(so every GPU's pass has the 1-GPU pass's size); results are bit-identical to one "
-                         "iteration per pass (default: 128 for cornell, 256 for config 3, 64 for config 4, 32 for config 5)")
+                         "iteration per pass (default: 256 for cornell and config 3, 128 for configs 4 and 5)")
     ap.add_argument("--scaling", choices=["strong", "weak"], default="strong",
                     help="strong (default): a step renders a FIXED batch of --samples samples per pixel of the "
-                         "whole image, split over the N GPUs by rows (cornell: 2 passes of 128 iterations at N=1, "
-                         "one pass of 256 from N=2); "
+                         "whole image, split over the N GPUs by rows (cornell: one pass of 256 iterations of the "
+                         "rank's rows at every N); "
                          "weak: a step is one pass of spp x N iterations of the rank's rows")
     ap.add_argument("--samples", type=int, default=256, help="strong scaling: samples per pixel per step")
     args = ap.parse_args()
@@ -574,6 +600,10 @@ def main() -> None:
             "roofline": roofline,
             "segments": seg_all,
             "bounce_live_per_step": [x / args.steps for x in live],
+            # SURVEY.md §8d's nominal rate: every path of every sample traced to full depth
+            "nominal_mrays": scene.camera().res[0] * scene.camera().res[1] * (args.samples if strong else spp * world)
+            * depth / (t_max / args.steps) / 1e6,
+            "nominal_definition": "W x H x samples per step x DEPTH / ms_per_step (no early termination counted)",
             "first_bounce_avg_ms": f_ms / max(f_n, 1),
             "gather_ms": gather_ms,
             "gather_ms_last_rank": gather_ms_min,
@@ -594,6 +624,12 @@ def main() -> None:
         dist.barrier()
         dist.destroy_process_group()
     pt.free()
+    if rank == 0 and world == 1 and not args.no_dropin and not shard_of and args.config == "cornell":
+        try:
+            result["dropin"] = dropin_bench(scene_path)
+            result["dropin"]["vs_batched"] = result["dropin"]["value"] / result["value"]
+        except Exception as e:   # a reported side leg: never fail the bench line
+            result["dropin"] = {"error": repr(e)}
     if rank == 0 and world == 1 and not args.no_pmc:
         try:
             extra = _pmc_leg(args, scene_path, spp, sorted_, avg_ms, kprefix, seg_bounce / max(k_n, 1), k_busy, k_n,

@@ -133,6 +133,7 @@ SIGNATURES = {
     "pt_create": (_I, [_P, C.POINTER(Flags), C.POINTER(Shard), C.POINTER(_P)]),
     "pt_destroy": (_I, [_P]),
     "pt_set_flags": (_I, [_P, C.POINTER(Flags)]),
+    "pt_ctx_counters": (_I, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "pt_render_pass": (_I, [_P, _I, _P]),
     "pt_preview_rgba": (_I, [_P, _I, _P, _P]),
     "pt_tile_info": (_I, [_P, _IP, _IP, _IP, _IP]),

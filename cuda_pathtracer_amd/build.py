@@ -16,6 +16,7 @@ ROOT = PKG.parent
 CSRC = PKG / "csrc"
 LIB = PKG / "libpt_amd.so"
 CLI = PKG / "pathtracer_amd"
+DROPIN_LIB = PKG / "libpt_dropin.so"
 HOST = PKG / "host"
 HOST_LIB = PKG / "build" / "libpt_amd_host.a"
 ORACLE_DIR = ROOT / "oracle"
@@ -70,7 +71,7 @@ def build_native(verbose: bool = False, force: bool = False) -> Path:
         _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(LIB), *map(str, objs), "-lz"], verbose)
     # C++ host mirror of the reference interface (host/) and the headless CLI over it
     host_srcs = [HOST / "pathtrace.cpp", HOST / "stream_compaction.cpp"]
-    host_hdrs = list(HOST.glob("*.h"))
+    host_hdrs = list(HOST.glob("*.h")) + list(HOST.glob("stream_compaction/*.h"))
     host_objs = []
     for s in host_srcs:
         o = objdir / ("host_" + s.name + ".o")
@@ -86,6 +87,12 @@ def build_native(verbose: bool = False, force: bool = False) -> Path:
     if force or _stale(CLI, [cli_src, LIB, HOST_LIB] + host_hdrs + headers):
         _run([HIPCC, f"--offload-arch={ARCH}", *COMMON, "-I", str(ROOT / "include"), "-I", str(HOST), str(cli_src),
               "-x", "none", str(HOST_LIB), "-o", str(CLI), "-L", str(PKG), "-lpt_amd", "-Wl,-rpath,$ORIGIN"], verbose)
+    # bench harness: the drop-in call sequence over the C++ mirror (host/dropin_bench.cpp)
+    dsrc = HOST / "dropin_bench.cpp"
+    if force or _stale(DROPIN_LIB, [dsrc, LIB, HOST_LIB] + host_hdrs + headers):
+        _run([HIPCC, f"--offload-arch={ARCH}", *COMMON, "-shared", "-I", str(ROOT / "include"), "-I", str(HOST),
+              str(dsrc), "-x", "none", str(HOST_LIB), "-o", str(DROPIN_LIB), "-L", str(PKG), "-lpt_amd",
+              "-Wl,-rpath,$ORIGIN"], verbose)
     return LIB
 
 
@@ -94,7 +101,7 @@ def build_oracle(verbose: bool = False, force: bool = False) -> Path:
     srcs = [ORACLE_DIR / "sc_oracle.cpp", ORACLE_DIR / "pt_oracle.cpp", ORACLE_DIR / "mesh_oracle.cpp"]
     ORACLE_LIB.parent.mkdir(exist_ok=True)
     if force or _stale(ORACLE_LIB, srcs):
-        _run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-fno-fast-math",
+        _run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-fno-fast-math", "-pthread",
               "-o", str(ORACLE_LIB), *map(str, srcs)], verbose)
     return ORACLE_LIB
 
@@ -108,8 +115,10 @@ def build_cpp_tests(verbose: bool = False, force: bool = False) -> list[Path]:
         exe = tdir / "build" / src.stem
         exe.parent.mkdir(exist_ok=True)
         outs.append(exe)
-        if force or _stale(exe, [src, LIB, HOST_LIB, ORACLE_LIB] + list(HOST.glob("*.h"))):
-            _run([HIPCC, f"--offload-arch={ARCH}", *COMMON, "-I", str(ROOT / "include"), "-I", str(HOST), str(src),
+        if force or _stale(exe, [src, LIB, HOST_LIB, ORACLE_LIB] + list(HOST.glob("*.h")) +
+                           list(HOST.glob("stream_compaction/*.h"))):
+            # only -I host: the test includes <stream_compaction/...> as the reference's main.cpp does
+            _run([HIPCC, f"--offload-arch={ARCH}", *COMMON, "-I", str(HOST), str(src),
                   "-x", "none", str(HOST_LIB), "-o", str(exe), "-L", str(PKG), "-lpt_amd", "-L", str(ORACLE_LIB.parent),
                   "-loracle", "-Wl,-rpath,$ORIGIN/../../../cuda_pathtracer_amd:$ORIGIN/../../../oracle/build"], verbose)
     return outs

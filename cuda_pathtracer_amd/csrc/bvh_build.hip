@@ -53,8 +53,9 @@ struct Ctl {
     uint32_t nodes;       // node ids allocated
     uint32_t nbig;        // big tasks of the next level
     uint32_t nsmall;      // small tasks (built whole by k_bvh_small)
-    uint32_t err;
+    uint32_t err;         // bits: 1 NaN box, 2 stack, 4 empty range, 8 degenerate split, 16 node capacity
     uint32_t max_depth;
+    uint32_t cap;         // node ids available (2n: a binary tree over n >= 1 leaves has 2n - 1)
 };
 
 // ---- the reference's box arithmetic (boundingbox.h, as pt_mesh.cpp restates it) ---------------
@@ -145,7 +146,14 @@ __device__ __forceinline__ CFold cfold_cat(const CFold& a, const CFold& b) {
     return r;
 }
 
-__device__ __forceinline__ uint32_t alloc_nodes(Ctl* ctl, uint32_t n) { return atomicAdd(&ctl->nodes, n); }
+// Two node ids for the children of a split, or -1 (error bit 16) when the capacity is spent — which
+// a partition with both sides non-empty never reaches; the guard keeps a broken split from writing
+// past the node array.
+__device__ __forceinline__ int alloc_pair(Ctl* ctl) {
+    const uint32_t l = atomicAdd(&ctl->nodes, 2u);
+    if (l + 2u > ctl->cap) { atomicOr(&ctl->err, 16u); return -1; }
+    return (int)l;
+}
 
 __device__ void make_leaf(BNode* nodes, int id, const Box& b, int start, int end, int depth, Ctl* ctl) {
     BNode& N = nodes[id];
@@ -358,13 +366,20 @@ __global__ __launch_bounds__(kBB) void k_bvh_big(const Task* __restrict__ tasks,
         // 5. the node and its two ranges (:122-128)
         if (tid == 0) {
             const int split_at = (int)(float)mid;
-            const int l = (int)alloc_nodes(ctl, 2u), r = l + 1;
-            make_inner(nodes, T.node, s_bounds, axis, l, r, T.start, T.depth);
-            const Task L{T.start, split_at, l, T.depth + 1}, R{split_at, T.end, r, T.depth + 1};
-            if (L.end - L.start > kSmall) next_big[atomicAdd(&ctl->nbig, 1u)] = L;
-            else small[atomicAdd(&ctl->nsmall, 1u)] = L;
-            if (R.end - R.start > kSmall) next_big[atomicAdd(&ctl->nbig, 1u)] = R;
-            else small[atomicAdd(&ctl->nsmall, 1u)] = R;
+            // both children non-empty (the SAH split always makes them so; a NaN centre box would not,
+            // and the level loop would then queue the same range again without end)
+            const bool split_ok = split_at > T.start && split_at < T.end;
+            if (!split_ok) atomicOr(&ctl->err, 8u);
+            const int l = split_ok ? alloc_pair(ctl) : -1;
+            if (l >= 0) {
+                const int r = l + 1;
+                make_inner(nodes, T.node, s_bounds, axis, l, r, T.start, T.depth);
+                const Task L{T.start, split_at, l, T.depth + 1}, R{split_at, T.end, r, T.depth + 1};
+                if (L.end - L.start > kSmall) next_big[atomicAdd(&ctl->nbig, 1u)] = L;
+                else small[atomicAdd(&ctl->nsmall, 1u)] = L;
+                if (R.end - R.start > kSmall) next_big[atomicAdd(&ctl->nbig, 1u)] = R;
+                else small[atomicAdd(&ctl->nsmall, 1u)] = R;
+            }
         }
         __syncthreads();
     }
@@ -435,7 +450,9 @@ __global__ void k_bvh_small(const Task* __restrict__ tasks, int ntasks, PrimD* _
                 mid = (int)(float)first;
             }
             if (top + 2 > 64) { atomicOr(&ctl->err, 2u); break; }
-            const int l = (int)alloc_nodes(ctl, 2u), r = l + 1;
+            if (!(mid > start && mid < end)) { atomicOr(&ctl->err, 8u); break; }
+            const int l = alloc_pair(ctl), r = l + 1;
+            if (l < 0) break;
             make_inner(nodes, T.node, bounds, axis, l, r, start, T.depth);
             stack[top++] = Task{mid, end, r, T.depth + 1};
             stack[top++] = Task{start, mid, l, T.depth + 1};
@@ -551,7 +568,7 @@ int build_bvh_device(Scene& S, double* ms) {
     BVH_TRY(B.get(&d_ctl, 1), "alloc");
     BVH_TRY(B.get(&d_flat, max_nodes), "alloc");
     BVH_TRY(hipMemcpy(d_tris, S.tris_load.data(), (size_t)n * sizeof(pt_triangle), hipMemcpyHostToDevice), "upload");
-    Ctl c0{1u, 0u, 0u, 0u, 0u};   // node 0 = the root
+    Ctl c0{1u, 0u, 0u, 0u, 0u, (uint32_t)max_nodes};   // node 0 = the root
     BVH_TRY(hipMemcpy(d_ctl, &c0, sizeof c0, hipMemcpyHostToDevice), "upload");
     const Task root{0, n, 0, 0};
     const int grid = std::min((n + 255) / 256, 2048);
@@ -563,7 +580,7 @@ int build_bvh_device(Scene& S, double* ms) {
         nbig = 1;
     } else {
         BVH_TRY(hipMemcpy(d_small, &root, sizeof root, hipMemcpyHostToDevice), "upload");
-        Ctl c1{1u, 0u, 1u, 0u, 0u};
+        Ctl c1{1u, 0u, 1u, 0u, 0u, (uint32_t)max_nodes};
         BVH_TRY(hipMemcpy(d_ctl, &c1, sizeof c1, hipMemcpyHostToDevice), "upload");
     }
     Task *cur = d_ta, *nxt = d_tb;
@@ -574,6 +591,7 @@ int build_bvh_device(Scene& S, double* ms) {
         BVH_TRY(hipGetLastError(), "k_bvh_big");
         Ctl c;
         BVH_TRY(hipMemcpy(&c, d_ctl, sizeof c, hipMemcpyDeviceToHost), "control read");
+        if (c.err) return 1;   // NaN boxes, a degenerate split or the node capacity: the host builds
         nbig = (int)c.nbig;
         std::swap(cur, nxt);
     }

@@ -2783,6 +2783,7 @@ struct pt_ctx {
     int grid_bounce[2] = {};   // k_bounce (later, first bounce): one full wave of workgroups
     bool fused = true;   // pipeline: fused bounce kernel (default) or trace + compact
     uint64_t compact_launches = 0;   // parity of the look-back status / live-count words
+    uint64_t n_cmask_builds = 0, n_flag_syncs = 0;   // pt_ctx_counters
     // owned device allocations
     std::vector<void*> allocs;
     PathSoA buf[2]{};
@@ -3050,6 +3051,7 @@ static bool beam_meets_box(const double olo[3], const double ohi[3], const doubl
 int build_cmask(pt_ctx* c) {
     KArgs& A = c->args;
     A.cmask = nullptr;
+    ++c->n_cmask_builds;
     const int ng = A.S.ngeoms;
     const char* off = std::getenv("PT_AMD_NO_CMASK");
     if ((off && std::strcmp(off, "1") == 0) || ng <= 0 || ng > kLdsGeoms || A.S.ntris > 0) return PT_OK;
@@ -3877,10 +3879,21 @@ int pt_destroy(pt_ctx* c) {
     return PT_OK;
 }
 
+// The reference re-reads its GUI flags on every pathtrace() call (pathtrace.cu:438-463), so this is
+// called once per iteration by a drop-in caller (host/pathtrace.cpp).  Only the lens (aperture) and
+// the camera-ray shape (SSAA, DoF, aperture, focal distance) reach device data — the widened geom
+// bounds and the first-bounce camera masks; every other flag is copied into the launch arguments
+// by value at pt_render_pass.  So a call that changes none of those four returns without a device
+// synchronisation and without rebuilding the masks (pt_ctx_counters counts both).
 int pt_set_flags(pt_ctx* c, const pt_flags* f) {
     if (!c || !f) return pt::fail(PT_ERR_ARG, "null argument");
-    const bool lens = f->aperture != c->flags.aperture;
+    auto same = [](float a, float b) { return std::memcmp(&a, &b, sizeof a) == 0; };
+    const bool lens = !same(f->aperture, c->flags.aperture);
+    const bool rays = lens || f->ssaa != c->flags.ssaa || f->dof != c->flags.dof ||
+                      !same(f->focal_dist, c->flags.focal_dist);
     set_flags_dev(c, *f);
+    if (!rays) return PT_OK;
+    ++c->n_flag_syncs;
     if (lens) {   // the camera lens bounds the ray origins: re-derive the widened bounds
         update_bounds(c, f->aperture);
         HIP_TRY(hipDeviceSynchronize());
@@ -3889,6 +3902,13 @@ int pt_set_flags(pt_ctx* c, const pt_flags* f) {
     }
     HIP_TRY(hipDeviceSynchronize());   // (queued first bounces still read the old masks)
     return build_cmask(c);   // SSAA / DoF / aperture / focal distance bound the camera rays
+}
+
+int pt_ctx_counters(const pt_ctx* c, uint64_t* mask_builds, uint64_t* flag_syncs) {
+    if (!c) return pt::fail(PT_ERR_ARG, "null context");
+    if (mask_builds) *mask_builds = c->n_cmask_builds;
+    if (flag_syncs) *flag_syncs = c->n_flag_syncs;
+    return PT_OK;
 }
 
 int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
@@ -4220,7 +4240,28 @@ int pt_profile_enable(pt_ctx* c, int32_t on) {
     return PT_OK;
 }
 
+namespace {
+int profile_read(pt_ctx* c, int32_t nkinds, double* ms, double* busy_ms, uint64_t* launches, bool fold_walk);
+}
+
 int pt_profile_read_kinds(pt_ctx* c, int32_t nkinds, double* ms, double* busy_ms, uint64_t* launches) {
+    return profile_read(c, nkinds, ms, busy_ms, launches, false);
+}
+
+int pt_profile_read_busy(pt_ctx* c, double ms[4], double busy_ms[4], uint64_t launches[4]) {
+    return profile_read(c, 4, ms, busy_ms, launches, true);
+}
+
+int pt_profile_read(pt_ctx* c, double ms[4], uint64_t launches[4]) {
+    return profile_read(c, 4, ms, nullptr, launches, true);
+}
+
+}  // extern "C"
+
+namespace {
+// fold_walk: the four-kind calls count the BVH walk in the bounce kinds, as they did before the walk
+// had kinds of its own (TRAVERSE -> BOUNCE, FIRST_TRAVERSE -> FIRST_BOUNCE; busy = the union of both)
+int profile_read(pt_ctx* c, int32_t nkinds, double* ms, double* busy_ms, uint64_t* launches, bool fold_walk) {
     if (!c || !ms || !launches || nkinds < 0) return pt::fail(PT_ERR_ARG, "bad argument");
     std::vector<std::pair<double, double>> iv[PT_KIND_COUNT];   // per kind: [start, end) after the first event
     double m[PT_KIND_COUNT] = {}, busy[PT_KIND_COUNT] = {};
@@ -4231,9 +4272,11 @@ int pt_profile_read_kinds(pt_ctx* c, int32_t nkinds, double* ms, double* busy_ms
         float t = 0.f, t0 = 0.f;
         HIP_TRY(hipEventElapsedTime(&t, ev.a, ev.b));
         HIP_TRY(hipEventElapsedTime(&t0, c->events[0].a, ev.a));
-        m[ev.kind] += t;
-        n[ev.kind] += 1;
-        iv[ev.kind].push_back({(double)t0, (double)t0 + (double)t});
+        const int k = !fold_walk ? ev.kind : ev.kind == PT_KIND_TRAVERSE ? PT_KIND_BOUNCE
+                                             : ev.kind == PT_KIND_FIRST_TRAVERSE ? PT_KIND_FIRST_BOUNCE : ev.kind;
+        m[k] += t;
+        n[k] += 1;
+        iv[k].push_back({(double)t0, (double)t0 + (double)t});
     }
     // union of each kind's launch intervals: lanes run kernels of one kind concurrently
     for (int k = 0; k < PT_KIND_COUNT; ++k) {
@@ -4253,12 +4296,4 @@ int pt_profile_read_kinds(pt_ctx* c, int32_t nkinds, double* ms, double* busy_ms
     return PT_OK;
 }
 
-int pt_profile_read_busy(pt_ctx* c, double ms[4], double busy_ms[4], uint64_t launches[4]) {
-    return pt_profile_read_kinds(c, 4, ms, busy_ms, launches);
-}
-
-int pt_profile_read(pt_ctx* c, double ms[4], uint64_t launches[4]) {
-    return pt_profile_read_kinds(c, 4, ms, nullptr, launches);
-}
-
-}  // extern "C"
+}  // namespace

@@ -13,7 +13,9 @@
 // between two buffers, then a shift to the exclusive result — the reference's algorithm.  Each
 // thread handles 4 consecutive elements: 16-byte loads of its own four and, when the distance is
 // a multiple of 4, of the four `distance` before them.
-// Thrust: rocThrust's exclusive_scan (the reference calls thrust::exclusive_scan).
+// Thrust: rocThrust's exclusive_scan (the reference calls thrust::exclusive_scan).  rocThrust
+// allocates and frees its temporary storage on every call, which synchronises the device: unlike
+// the Efficient and Naive entry points, the Thrust one is not asynchronous on its stream.
 // Sums wrap in int32 like the reference's (two's complement; computed in uint32 here, so the
 // wrap is defined behaviour).
 #include <hip/hip_runtime.h>
@@ -53,10 +55,11 @@ typedef int v4i __attribute__((ext_vector_type(4)));
 
 // out[i] = in[i] + in[i - dist] (i >= dist), in[i] otherwise, for i in [4t, 4t + 4) of thread t.
 __global__ __launch_bounds__(kNaiveThreads) void k_naive_pass(const int32_t* __restrict__ in,
-                                                            int32_t* __restrict__ out, int64_t n, int64_t dist) {
+                                                            int32_t* __restrict__ out, int64_t n, int64_t dist,
+                                                            bool vec) {
     const int64_t stride = (int64_t)gridDim.x * kNaiveThreads * 4;
     for (int64_t i = ((int64_t)blockIdx.x * kNaiveThreads + threadIdx.x) * 4; i < n; i += stride) {
-        if (i + 4 <= n && i >= dist && (dist & 3) == 0) {
+        if (vec && i + 4 <= n && i >= dist && (dist & 3) == 0) {
             const v4i a = *reinterpret_cast<const v4i*>(in + i);
             const v4i b = *reinterpret_cast<const v4i*>(in + i - dist);
             v4i c;
@@ -87,6 +90,10 @@ int naive_device(const int32_t* d_in, int32_t* d_out, int64_t n, int32_t* d_tmp,
     if (n == 0) return SC_OK;
     if (!d_in || !d_out || (n > 1 && !d_tmp)) return fail(SC_ERR_ARG, "null pointer");
     if (d_out == d_in || d_tmp == d_in || d_tmp == d_out) return fail(SC_ERR_ARG, "buffers must not alias");
+    // 16-byte vector loads and stores only when every base is 16-byte aligned (a torch view with a
+    // storage offset is only 4-byte aligned); the scalar path otherwise
+    const bool vec = ((reinterpret_cast<uintptr_t>(d_in) | reinterpret_cast<uintptr_t>(d_out) |
+                       reinterpret_cast<uintptr_t>(d_tmp)) & 15) == 0;
     int passes = 0;
     while ((int64_t)1 << passes < n) ++passes;   // ilog2ceil(n) (common.h:24-26); 0 for n == 1
     // ping-pong so that the last pass writes d_tmp, from which the shift writes d_out
@@ -94,7 +101,7 @@ int naive_device(const int32_t* d_in, int32_t* d_out, int64_t n, int32_t* d_tmp,
     for (int p = 0; p < passes; ++p) {
         int32_t* dst = ((passes - 1 - p) & 1) ? d_out : d_tmp;
         hipLaunchKernelGGL(k_naive_pass, dim3(naive_grid(4, n)), dim3(kNaiveThreads), 0, st, src, dst, n,
-                           (int64_t)1 << p);
+                           (int64_t)1 << p, vec);
         src = dst;
     }
     hipLaunchKernelGGL(k_naive_shift, dim3(naive_grid(1, n)), dim3(kNaiveThreads), 0, st, src, d_out, n);

@@ -89,6 +89,8 @@ void pathtraceFree() {
     g_ctx = nullptr;
 }
 
+pt_ctx* pathtraceContext() { return g_ctx; }
+
 void pathtrace(uchar4* pbo, int frame, int iteration) {
     (void)frame;
     if (!g_ctx || !g_scene) {

@@ -70,3 +70,7 @@ void InitDataContainer(GuiDataContainer* guiData);
 void pathtraceInit(Scene* scene);
 void pathtraceFree();
 void pathtrace(uchar4* pbo, int frame, int iteration);
+
+// Extension (no reference counterpart): the context the four functions above drive (null before
+// pathtraceInit), for callers that also want pt_stats / pt_ctx_counters of the global render.
+pt_ctx* pathtraceContext();

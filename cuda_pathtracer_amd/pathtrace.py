@@ -125,8 +125,11 @@ class Scene:
     def _fill_non_jpeg_textures(self) -> None:
         """Texture files that are not JPEG (PNG, BMP, TGA: stbi_load reads them too) are left
         undecoded by the native loader (include/pt_amd.h); decode them here.  These formats are
-        lossless, so any decoder yields stbi_load(path, &w, &h, &comp, 0)'s texels; palette images
-        are expanded to RGB(A) as stb does."""
+        lossless, so a decoder yields stbi_load(path, &w, &h, &comp, 0)'s texels once the modes are
+        mapped as stb maps them: palette images expand to RGB, or RGBA with a tRNS chunk; a tRNS chunk
+        adds an alpha channel to grey and RGB images too; 16-bit samples keep their high byte; 1-bit
+        grey expands to 0/255.  A mode stb would not produce raises instead of converting silently
+        (non-JPEG texels are parity-unpinned: no reference fixture covers them)."""
         ntex = self.counts()[4]
         for tid in range(ntex):
             path = self.texture_path(tid)
@@ -136,11 +139,7 @@ class Scene:
                 continue
             from PIL import Image   # (host-side file IO only; not on the render path)
             with Image.open(path) as im:
-                if im.mode == "P":
-                    im = im.convert("RGBA" if "transparency" in im.info else "RGB")
-                elif im.mode not in ("L", "LA", "RGB", "RGBA"):
-                    im = im.convert("RGB")
-                px = np.ascontiguousarray(np.asarray(im, dtype=np.uint8))
+                px = _stb_texels(im, path)
             h, w = px.shape[:2]
             comps = 1 if px.ndim == 2 else px.shape[2]
             check_pt(lib().pt_scene_set_texture_pixels(self._h, tid, w, h, comps, px.ctypes.data_as(C.c_void_p)))
@@ -226,6 +225,30 @@ def _stream_ptr(stream):
     return int(getattr(stream, "cuda_stream", stream))
 
 
+def _stb_texels(im, path) -> np.ndarray:
+    """PIL image -> the (h, w[, c]) uint8 texels stbi_load(..., 0) returns for the same file."""
+    trans = "transparency" in im.info
+    mode = im.mode
+    if mode == "P":
+        return np.ascontiguousarray(np.asarray(im.convert("RGBA" if trans else "RGB"), dtype=np.uint8))
+    if mode == "1":
+        im, mode = im.convert("L"), "L"
+    if mode in ("I;16", "I;16B", "I;16L", "I"):   # 16-bit grey: stb keeps the high byte
+        g = (np.asarray(im).astype(np.uint32) >> 8).astype(np.uint8)
+        if trans:   # tRNS on grey: stb adds an alpha channel (opaque except the keyed value)
+            key = int(im.info["transparency"])
+            a = np.where(np.asarray(im).astype(np.uint32) == key, 0, 255).astype(np.uint8)
+            return np.ascontiguousarray(np.stack([g, a], axis=-1))
+        return np.ascontiguousarray(g)
+    if mode == "L" and trans:
+        return np.ascontiguousarray(np.asarray(im.convert("LA"), dtype=np.uint8))
+    if mode == "RGB" and trans:
+        return np.ascontiguousarray(np.asarray(im.convert("RGBA"), dtype=np.uint8))
+    if mode in ("L", "LA", "RGB", "RGBA"):
+        return np.ascontiguousarray(np.asarray(im, dtype=np.uint8))
+    raise ValueError(f"texture {path}: image mode {mode!r} has no stbi_load equivalent here")
+
+
 class PathTracer:
     """One render context (pathtraceInit ... pathtraceFree) for a pixel tile of the image.
 
@@ -259,6 +282,13 @@ class PathTracer:
     def set_flags(self, gui: GuiDataContainer) -> None:
         self.gui = gui
         check_pt(lib().pt_set_flags(self._h, C.byref(gui.to_c())))
+
+    def counters(self) -> dict:
+        """Host-side counters (pt_ctx_counters): camera-mask builds and device-synchronising
+        pt_set_flags calls."""
+        b, y = C.c_uint64(), C.c_uint64()
+        check_pt(lib().pt_ctx_counters(self._h, C.byref(b), C.byref(y)))
+        return {"mask_builds": int(b.value), "flag_syncs": int(y.value)}
 
     def render_pass(self, iter_first: int, stream=None) -> None:
         """pathtrace(): iterations [iter_first, iter_first + spp) for this tile, asynchronous."""
@@ -307,7 +337,8 @@ class PathTracer:
         return {"segments": int(s.segments), "passes": int(s.passes),
                 "bounce_live": [int(s.bounce_live[k]) for k in range(depth)],
                 "bounce_emit": [int(s.bounce_emit[k]) for k in range(depth)],
-                "emissive_hits": int(s.emissive_hits), "bound_mismatch": int(s.bound_mismatch)}
+                "emissive_hits": int(s.emissive_hits), "bound_mismatch": int(s.bound_mismatch),
+                "device_error": int(s.device_error)}
 
     def profile(self, on: bool = True) -> None:
         check_pt(lib().pt_profile_enable(self._h, int(on)))

@@ -9,8 +9,9 @@ Reference: path_tracer/stream_compaction/{efficient,cpu,naive,thrust,common}.{h,
   StreamCompaction::Thrust::scan, Thrust::timer()        -> Thrust
 The host-array calls keep the reference semantics (host arrays in, host arrays out, GPU time of
 the device work only).  The device-tensor functions (scan_device, compact_device,
-partition_device, naive_scan_device, thrust_scan_device) take torch tensors already resident on
-the GPU and never synchronise.  CPU's functions are the library's own host loops (sc_cpu_*), the
+partition_device, naive_scan_device) take torch tensors already resident on the GPU and never
+synchronise; thrust_scan_device synchronises the device (rocThrust allocates and frees its
+temporary storage on every call).  CPU's functions are the library's own host loops (sc_cpu_*), the
 reference's CPU namespace; they are not a fallback of any device path and not the test oracle
 (oracle/ checks them).
 """
@@ -224,6 +225,13 @@ def live_indices_device(d_flags, d_idx=None, stream=None, check: bool = False):
     return d_idx, cnt
 
 
+def _check_len(d_in, **bufs) -> None:
+    """Output and scratch tensors must hold at least d_in.numel() elements (the kernels write n)."""
+    for name, t in bufs.items():
+        if t.numel() < d_in.numel():
+            raise ValueError(f"{name} holds {t.numel()} elements < n = {d_in.numel()}")
+
+
 def naive_scan_device(d_in, d_out=None, d_tmp=None, stream=None):
     """Naive::scan on device tensors (sc_naive_scan_i32): d_in unchanged, d_tmp = n int32 of scratch."""
     import torch
@@ -231,16 +239,19 @@ def naive_scan_device(d_in, d_out=None, d_tmp=None, stream=None):
     d_out = torch.empty_like(d_in) if d_out is None else d_out
     d_tmp = torch.empty_like(d_in) if d_tmp is None else d_tmp
     _check_dev_i32(d_out, "d_out"); _check_dev_i32(d_tmp, "d_tmp")
+    _check_len(d_in, d_out=d_out, d_tmp=d_tmp)
     check_sc(lib().sc_naive_scan_i32(d_in.data_ptr(), d_out.data_ptr(), d_in.numel(), d_tmp.data_ptr(),
                                      _stream_ptr(stream)))
     return d_out
 
 
 def thrust_scan_device(d_in, d_out=None, stream=None):
-    """Thrust::scan on device tensors (sc_thrust_scan_i32: rocThrust exclusive_scan)."""
+    """Thrust::scan on device tensors (sc_thrust_scan_i32: rocThrust exclusive_scan).  Synchronises
+    the device (rocThrust's per-call temporary storage)."""
     import torch
     _check_dev_i32(d_in, "d_in")
     d_out = torch.empty_like(d_in) if d_out is None else d_out
     _check_dev_i32(d_out, "d_out")
+    _check_len(d_in, d_out=d_out)
     check_sc(lib().sc_thrust_scan_i32(d_in.data_ptr(), d_out.data_ptr(), d_in.numel(), _stream_ptr(stream)))
     return d_out

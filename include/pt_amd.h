@@ -222,7 +222,13 @@ int pt_scene_bvh_quads(const pt_scene* s, void* out, int32_t cap, int32_t* root_
  * rows_in_tile * width * spp paths.  shard may be NULL (= {0, 1, 1}). */
 int pt_create(const pt_scene* s, const pt_flags* flags, const pt_shard* shard, pt_ctx** out);
 int pt_destroy(pt_ctx* c);                                  /* pathtraceFree */
-int pt_set_flags(pt_ctx* c, const pt_flags* flags);         /* InitDataContainer / Settings */
+/* InitDataContainer / Settings.  Cheap when called every iteration with unchanged camera-ray flags:
+ * only a change of ssaa, dof, aperture or focal_dist synchronises the device and rebuilds the
+ * first-bounce camera masks (and, for the aperture, the widened geom bounds). */
+int pt_set_flags(pt_ctx* c, const pt_flags* flags);
+/* Host-side counters of a context: first-bounce camera-mask builds (pt_create builds one) and the
+ * pt_set_flags calls that synchronised the device. */
+int pt_ctx_counters(const pt_ctx* c, uint64_t* mask_builds, uint64_t* flag_syncs);
 /* One pass: iterations [iter_first, iter_first + spp) for this tile, accumulated into the tile
  * image.  Asynchronous on `stream`; no host synchronisation inside.  A batched pass (spp > 1)
  * runs its iterations in lanes on internal streams and adds their colours into the image on a
@@ -260,7 +266,9 @@ int pt_stats(pt_ctx* c, pt_stats_t* out);                   /* synchronises the 
 #define PT_KIND_FIRST_TRAVERSE 5 /* mesh scenes, bounce 0: the BVH walk of the camera rays       */
 #define PT_KIND_COUNT 6
 int pt_profile_enable(pt_ctx* c, int32_t on);
-/* The first four kinds (pt_profile_read_kinds returns all of them). */
+/* The first four kinds (pt_profile_read_kinds returns all of them).  These two calls count the BVH
+ * walk (kinds 4 and 5) in BOUNCE and FIRST_BOUNCE, as before the walk had kinds of its own.  In the
+ * material-sorted pipeline the camera-ray producer counts as FIRST_BOUNCE, not SORT (since round 3). */
 int pt_profile_read(pt_ctx* c, double ms[4], uint64_t launches[4]);
 /* Same, plus busy_ms[kind]: the length of the union of that kind's launch intervals.  Batched
  * passes of the fused pipeline run two lanes of iterations concurrently (pt_render_pass), so

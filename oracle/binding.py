@@ -98,6 +98,7 @@ def lib() -> C.CDLL:
                                     C.POINTER(OCamera), C.c_int, C.POINTER(OFlags), C.c_int, C.c_int, P, P]
         L.oracle_render.restype = C.c_double
         L.oracle_set_tap.argtypes = [C.c_int, P, P, C.c_int]
+        L.oracle_set_threads.argtypes = [C.c_int]
         L.oracle_tap_count.restype = C.c_int
         L.oracle_tonemap.argtypes = [P, C.c_int, C.c_int, C.c_float, P]
         L.oracle_preview.argtypes = [P, C.c_int, C.c_int, C.c_int, P]
@@ -259,7 +260,15 @@ class OracleScene:
         extension; the reference reads neither key, scene.cpp:46-56)."""
         data = json.loads(Path(path).read_text())
         ext = data.get("Extensions", {})
-        refraction = refraction or (ext.get("REFRACTION") is True if isinstance(ext, dict) else "REFRACTION" in ext)
+        # as the native loader (pt_scene.cpp file_wants_refraction): an object's boolean
+        # "REFRACTION": true, or the string "REFRACTION" inside an array; anything else is off
+        if isinstance(ext, dict):
+            wants = ext.get("REFRACTION") is True
+        elif isinstance(ext, list):
+            wants = any(isinstance(x, str) and x == "REFRACTION" for x in ext)
+        else:
+            wants = False
+        refraction = refraction or wants
         sc = cls()
         ids = {}
         base = Path(path).resolve().parent
@@ -310,6 +319,11 @@ def render_pass(sc: OracleScene, fl: OFlags, iter_first: int, spp: int = 1, rank
                              C.byref(sc.cam), d, C.byref(fl), iter_first, spp, rank, world,
                              image.ctypes.data, live.ctypes.data)
     return image, [int(x) for x in live[:d]]
+
+
+def set_threads(n: int) -> None:
+    """Worker threads of render_pass's per-path loops (the result does not depend on it)."""
+    lib().oracle_set_threads(int(n))
 
 
 def bounce_records(sc: OracleScene, fl: OFlags, iteration: int, bounce: int):

@@ -39,6 +39,7 @@
 #include <cstring>
 #include <algorithm>
 #include <chrono>
+#include <thread>
 #include <vector>
 
 extern "C" {
@@ -722,6 +723,34 @@ void oracle_set_tap(int bounce, int32_t* keys, int32_t* flags, int cap) {
 }
 int oracle_tap_count() { return g_tap.n; }
 
+// Worker threads of oracle_render_pass's per-path loops (raygen, intersection, shading): each
+// path's work is independent given its index, and the sort and the compaction stay sequential, so
+// the result is the same for every thread count (default 1).  Lets a test check a 4K frame
+// (BASELINE.json configs 4 and 5 at their benched size) in seconds on the host's cores.
+static int g_threads = 1;
+void oracle_set_threads(int n) { g_threads = n < 1 ? 1 : n; }
+}  // extern "C"
+
+template <class F>
+static void par_for(int n, F f) {
+    const int T = std::min(g_threads, std::max(1, n / 256));
+    if (T <= 1) {
+        for (int i = 0; i < n; ++i) f(i);
+        return;
+    }
+    std::vector<std::thread> ts;
+    ts.reserve((size_t)T);
+    for (int t = 0; t < T; ++t)
+        ts.emplace_back([=, &f] {
+            // interleaved 64-path chunks: the cost per path varies along the array
+            for (int c0 = t * 64; c0 < n; c0 += T * 64)
+                for (int i = c0, e = std::min(n, c0 + 64); i < e; ++i) f(i);
+        });
+    for (auto& th : ts) th.join();
+}
+
+extern "C" {
+
 int oracle_render_pass(const OGeom* geoms, int ngeoms, const OMaterial* mats, int nmats,
                        const OTriangle* tris, int ntris, const ONode* nodes, int nnodes,
                        const OTexture* texs, int ntexs,
@@ -734,14 +763,14 @@ int oracle_render_pass(const OGeom* geoms, int ngeoms, const OMaterial* mats, in
     const int npix = rows * W;
     const int P = npix * spp;
     std::vector<Path> paths((size_t)P);
-    for (int s = 0; s < spp; ++s)
-        for (int lp = 0; lp < npix; ++lp) {
-            int y = (lp / W) * world + rank, x = lp % W;
-            Path& p = paths[(size_t)s * npix + lp];
-            raygen(*cam, *fl, iter_first + s, depth, x, y, p);
-            p.slot = s * npix + lp;
-            p.iter = iter_first + s;
-        }
+    par_for(P, [&](int i) {
+        const int s = i / npix, lp = i % npix;
+        int y = (lp / W) * world + rank, x = lp % W;
+        Path& p = paths[(size_t)i];
+        raygen(*cam, *fl, iter_first + s, depth, x, y, p);
+        p.slot = s * npix + lp;
+        p.iter = iter_first + s;
+    });
     std::vector<Isect> isect((size_t)P);
     std::vector<int32_t> flags((size_t)P), perm((size_t)P);
     std::vector<Path> tmp((size_t)P);
@@ -749,7 +778,7 @@ int oracle_render_pass(const OGeom* geoms, int ngeoms, const OMaterial* mats, in
     while (N != 0) {
         if (bounce_live && bounce < depth) bounce_live[bounce] += (uint64_t)N;
         std::memset(isect.data(), 0, sizeof(Isect) * (size_t)P);          // pathtrace.cu:466
-        for (int i = 0; i < N; ++i) compute_isect(sc, *fl, paths[i].o, paths[i].d, isect[i]);
+        par_for(N, [&](int i) { compute_isect(sc, *fl, paths[i].o, paths[i].d, isect[i]); });
         const bool tap = bounce == g_tap.bounce && N <= g_tap.cap;
         if (tap) {
             g_tap.n = N;
@@ -769,9 +798,13 @@ int oracle_render_pass(const OGeom* geoms, int ngeoms, const OMaterial* mats, in
         // RNG key (pathtrace.cu:315): the index within the path's own iteration, i.e. what `spp`
         // sequential pathtrace() calls would use (the array is iteration-major: stable compaction
         // of slot-ordered paths, and the sort above keeps iterations apart)
-        for (int i = 0, base = 0; i < N; ++i) {
-            if (i > 0 && paths[i].iter != paths[i - 1].iter) base = i;
-            shade(sc, *fl, paths[i], isect[i], fl->rng_key_pixel ? paths[i].pixel : i - base);
+        {
+            std::vector<int32_t> base((size_t)N);
+            for (int i = 0, b = 0; i < N; ++i) {
+                if (i > 0 && paths[i].iter != paths[i - 1].iter) b = i;
+                base[(size_t)i] = b;
+            }
+            par_for(N, [&](int i) { shade(sc, *fl, paths[i], isect[i], fl->rng_key_pixel ? paths[i].pixel : i - base[(size_t)i]); });
         }
         // relocate_terminated_paths (pathtrace.cu:377-407) == thrust::stable_partition here
         for (int i = 0; i < N; ++i) flags[i] = paths[i].remaining == 0 ? 0 : 1;

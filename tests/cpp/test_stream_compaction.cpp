@@ -19,7 +19,12 @@
 #include <random>
 #include <vector>
 
-#include "stream_compaction.h"
+// the reference self-test's include block, as stream_compaction/src/main.cpp:2-5 writes it
+// (forwarding headers cuda_pathtracer_amd/host/stream_compaction/*.h; built with -I host only)
+#include <stream_compaction/cpu.h>
+#include <stream_compaction/naive.h>
+#include <stream_compaction/efficient.h>
+#include <stream_compaction/thrust.h>
 
 extern "C" {   // oracle/sc_oracle.cpp (CPU::scan / compactWithoutScan / compactWithScan)
 void oracle_scan(int64_t n, int32_t* out, const int32_t* in);

@@ -234,3 +234,47 @@ def test_refraction_keys_ignored_by_default(tmp_path):
         import ctypes as C
         h = C.c_void_p()
         N.check_pt(N.lib().pt_scene_load_json_ex(str(path).encode(), 0x80, C.byref(h)))
+
+
+@pytest.mark.parametrize("ext", ["REFRACTION", {"REFRACTION": "yes"}, 1, ["refraction"], [True]])
+def test_refraction_opt_in_forms_agree(tmp_path, ext):
+    """Only `"Extensions": {"REFRACTION": true}` or `["REFRACTION"]` opt a file in; any other form
+    (a bare string, a non-boolean value, other array items) loads with the extension off in both
+    the product's loader (pt_scene.cpp file_wants_refraction) and the oracle's."""
+    path = _cornell_with_refraction_keys(tmp_path, ext)
+    bundled = _mat_table(P.Scene(SCENES / "cornell.json"))
+    assert _mat_table(P.Scene(path)) == bundled
+    o = [(m.has_refractive, m.ior) for m in O.OracleScene.from_json(path).materials]
+    assert o == [(m[2], m[3]) for m in bundled]
+
+
+def test_non_jpeg_texture_modes_follow_stb(tmp_path):
+    """Non-JPEG textures are decoded on the host (pathtrace.py _stb_texels) with stbi_load's mode
+    mapping: 16-bit grey keeps the high byte, a tRNS chunk adds an alpha channel to grey and RGB,
+    palette images expand, 1-bit grey becomes 0/255, and an unmapped mode raises."""
+    from PIL import Image
+    from cuda_pathtracer_amd.pathtrace import _stb_texels
+    g16 = np.array([[0, 255, 256, 65535], [1000, 40000, 512, 300]], np.uint16)
+    im = Image.fromarray(g16.astype(np.int32), mode="I")
+    assert np.array_equal(_stb_texels(im, "g16"), (g16 >> 8).astype(np.uint8))
+    p = tmp_path / "g16.png"
+    Image.fromarray(g16).save(p)
+    with Image.open(p) as im2:
+        assert np.array_equal(_stb_texels(im2, p), (g16 >> 8).astype(np.uint8))
+    g8 = np.array([[0, 7, 255], [7, 9, 7]], np.uint8)
+    p = tmp_path / "gt.png"
+    Image.fromarray(g8).save(p, transparency=7)
+    with Image.open(p) as im3:
+        la = _stb_texels(im3, p)
+    assert la.shape == (2, 3, 2) and np.array_equal(la[..., 0], g8)
+    assert np.array_equal(la[..., 1], np.where(g8 == 7, 0, 255))
+    rgb = np.arange(2 * 2 * 3, dtype=np.uint8).reshape(2, 2, 3)
+    p = tmp_path / "rt.png"
+    Image.fromarray(rgb).save(p, transparency=(0, 1, 2))
+    with Image.open(p) as im4:
+        ra = _stb_texels(im4, p)
+    assert ra.shape == (2, 2, 4) and np.array_equal(ra[..., :3], rgb) and ra[0, 0, 3] == 0 and ra[1, 1, 3] == 255
+    bw = Image.fromarray(np.array([[0, 255], [255, 0]], np.uint8)).convert("1")
+    assert np.array_equal(_stb_texels(bw, "bw"), np.array([[0, 255], [255, 0]], np.uint8))
+    with pytest.raises(ValueError):
+        _stb_texels(Image.new("CMYK", (2, 2)), "cmyk")

@@ -228,6 +228,24 @@ def test_batched_pass_equals_sequential_iterations(kw):
     assert live_b == live_s
 
 
+@pytest.mark.parametrize("kw", [dict(), dict(sort_by_material=True)])
+def test_render_threads_do_not_change_the_result(kw):
+    """oracle_set_threads only splits the per-path loops (raygen, intersection, shading); the sort
+    and the compaction stay sequential, so the pass is bit-identical for every thread count (the
+    full-size GPU parity tests run the oracle on the host's cores)."""
+    sc = _small_scene()
+    fl = O.flags(**kw)
+    one, live1 = O.render_pass(sc, fl, iter_first=2, spp=3)
+    try:
+        for t in (3, 8):
+            O.set_threads(t)
+            img, live = O.render_pass(sc, fl, iter_first=2, spp=3)
+            np.testing.assert_array_equal(img, one)
+            assert live == live1
+    finally:
+        O.set_threads(1)
+
+
 def test_render_shards_tile_the_image():
     """Rank r of W owns rows y % W == r; shards are disjoint and cover the image,
     and the camera ray of a pixel does not depend on the sharding (raygen key = global pixel)."""

@@ -745,6 +745,37 @@ def test_first_bounce_camera_masks(cornell_path, monkeypatch, cam, kw, shard):
     _assert_bitexact(gi, img, f"masks after set_flags {kw2}")
 
 
+def test_set_flags_unchanged_is_cheap(cornell_path):
+    """The reference re-reads its GUI flags on every pathtrace() call (pathtrace.cu:438-463), so a
+    drop-in caller calls pt_set_flags once per iteration.  Unchanged flags — and flags that do not
+    shape the camera rays (Russian roulette here) — must not synchronise the device or rebuild the
+    first-bounce camera masks; a change of SSAA / DoF / aperture / focal distance must.  The image of
+    the per-iteration pathtrace() sequence stays bit-exact against the oracle throughout."""
+    from cuda_pathtracer_amd import PathTracer
+    s, o = _pair(cornell_path, (64, 48))
+    gui = _gui()
+    pt = PathTracer(s, gui)
+    assert pt.counters() == {"mask_builds": 1, "flag_syncs": 0}
+    ref = None
+    for it in range(1, 6):
+        pt.set_flags(_gui())                       # what pathtrace() does every iteration
+        pt.render_pass(it)
+        ref, _ = O.render_pass(o, _oflags(_gui()), it, image=ref)
+    assert pt.counters() == {"mask_builds": 1, "flag_syncs": 0}
+    _assert_bitexact(pt.image(), ref, "unchanged flags")
+    pt.set_flags(_gui(russianRoulette=False))      # not a camera-ray flag: no sync, no rebuild
+    pt.render_pass(6)
+    ref, _ = O.render_pass(o, _oflags(_gui(russianRoulette=False)), 6, image=ref)
+    assert pt.counters() == {"mask_builds": 1, "flag_syncs": 0}
+    for it, kw in ((7, dict(aperture=0.4)), (8, dict(aperture=0.4)), (9, dict(aperture=0.4, SSAA=False))):
+        pt.set_flags(_gui(**kw))
+        pt.render_pass(it)
+        ref, _ = O.render_pass(o, _oflags(_gui(**kw)), it, image=ref)
+    assert pt.counters() == {"mask_builds": 3, "flag_syncs": 2}
+    _assert_bitexact(pt.image(), ref, "flags changed between iterations")
+    pt.free()
+
+
 @pytest.mark.parametrize("sort", [False, True])
 def test_async_lanes_stream_ordered_reads(cornell_path, sort):
     """Async lanes: a batched pass does not make the caller's stream wait for every lane, so the
@@ -833,6 +864,49 @@ def test_config5_100k_triangles_bitexact(tmp_path, kw):
     g, r, st, live = _run(Scene(path), O.OracleScene.from_json(path), _gui(**kw), iters=2, spp=2)
     _assert_bitexact(g, r, f"config 5 100k triangles {kw}")
     assert st["bounce_live"] == live and r.sum() > 0
+
+
+def test_config5_full_size_bitexact(tmp_path):
+    """BASELINE.json config 5 at its benched size: 100k random triangles (OBJ + SAH BVH), 3840x2160,
+    DEPTH 32, one iteration — GPU == oracle bit for bit, with the same live-path count entering every
+    bounce (pathtrace.cu:423-528).  8.3 M camera rays, ~25 M traced segments: the largest index
+    ranges of the 4-wide walk's tickets and records at one iteration.  The oracle's per-path loops
+    run on the host's cores (oracle_set_threads; its result does not depend on the thread count)."""
+    import os
+    from cuda_pathtracer_amd import Scene, scenes
+    path = scenes.random_triangles(tmp_path, n=100_000, res=(3840, 2160), depth=32)
+    O.set_threads(min(16, os.cpu_count() or 1))
+    try:
+        g, r, st, live = _run(Scene(path), O.OracleScene.from_json(path), _gui(), iters=1)
+    finally:
+        O.set_threads(1)
+    _assert_bitexact(g, r, "config 5 full size")
+    assert st["bounce_live"] == live and live[0] == 3840 * 2160 and r.sum() > 0
+
+
+@pytest.mark.parametrize("config", ["multi_object_4k", "random_triangles_100k"])
+def test_benched_pass_size_equals_two_half_passes(tmp_path, config):
+    """Configs 4 and 5 at the pass size bench.py runs them: one pass of 128 iterations at 3840x2160
+    (1.06 G paths; ~120 GB of path state, walk records and colours for config 5) against two passes
+    of 64 — a size-independent property (batched passes equal sequential ones): the
+    same image bit for bit, the same live-path and emission counts per bounce, no device error."""
+    from cuda_pathtracer_amd import PathTracer, Scene, scenes
+    path = scenes.CONFIGS[config](tmp_path)
+    scene = Scene(path)
+    out = []
+    for spp, passes in ((128, 1), (64, 2)):
+        pt = PathTracer(scene, _gui(), spp=spp)
+        it = 1
+        for _ in range(passes):
+            pt.render_pass(it)
+            it += spp
+        st = pt.stats()
+        assert st["device_error"] == 0 and st["bounce_live"][0] == 128 * 3840 * 2160
+        out.append((pt.image(), st["bounce_live"], st["bounce_emit"]))
+        pt.free()
+    _assert_bitexact(out[0][0], out[1][0], f"{config}: one pass of 128 vs two of 64")
+    assert out[0][1:] == out[1][1:]
+    assert np.isfinite(out[0][0]).all() and out[0][0].sum() > 0
 
 
 @pytest.mark.parametrize("spp", [1, 3])
