@@ -1343,6 +1343,19 @@ constexpr int kFoldBatch = PT_FOLD_BATCH;   // k_traverse4: task results read pe
 #ifndef PT_T4_ASSIGN
 #define PT_T4_ASSIGN 0   // k_traverse4 leaf tasks: 0 owner tag + ballot + ds_bpermute; 1 task slots written by owners
 #endif
+#ifndef PT_T4_COOP
+#define PT_T4_COOP 0     // k_traverse4 quad fetch: 0 each interior lane loads its own 112 B (7 loads);
+                         // 1 the wave loads the quads cooperatively, 8 lanes per 128-B row, register-
+                         // staged into LDS; 2 the same by LDS-DMA (global_load_lds_dwordx4).
+                         // Measured on config 5 (round 4, profiles/r04_walk_coop_ab.txt): 0 845.8,
+                         // 2 with 16 / 32 / 64 rows 745.7 / 589.9 / 416.2, 1 (32 rows) 477.3 Mray/s —
+                         // the walk waits on its dependent loads (46% of wave cycles), and the LDS
+                         // hand-over, its waits and the lower occupancy cost more than the address
+                         // cycles saved; 0 ships
+#endif
+#ifndef PT_T4_COOP_ROWS
+#define PT_T4_COOP_ROWS 32   // quads fetched cooperatively per trip (interior lanes of rank >= this load their own)
+#endif
 
 // Exclusive prefix of the previous launch's segment survivor counts into s_pre[0..nseg]; returns
 // the total.  All threads of the block call it (barriers).
@@ -1617,6 +1630,14 @@ __global__ __launch_bounds__(kBlock, PT_T4_WAVES) void k_traverse4(const KArgs A
 #if PT_T4_ASSIGN == 0
     __shared__ int32_t s_own[kBlock];   // leaf tasks: tag << 6 | owner lane, at the owner's first task
 #endif
+#if PT_T4_COOP
+    // cooperative quad fetch: per wave, the quad indices of the trip's interior lanes by rank, and
+    // PT_T4_COOP_ROWS staged 128-B rows (row r = the quad of the rank-r interior lane; its 16-B
+    // column k holds chunk (k - (r >> 1)) & 7, so the owners' ds_read_b128 of one chunk hit 16
+    // distinct 16-B bank slots per lane group)
+    __shared__ int32_t s_qlist[kBlock];
+    __shared__ v4f s_stage[(kBlock / 64) * PT_T4_COOP_ROWS * 8];
+#endif
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const SceneDev& S = A.S;
     int N, nseg = 0, chunk = 0;
@@ -1628,6 +1649,10 @@ __global__ __launch_bounds__(kBlock, PT_T4_WAVES) void k_traverse4(const KArgs A
         chunk = (int)A.ctl[par].chunk;
         N = seg_prefix(reinterpret_cast<const uint32_t*>(A.seg) + (size_t)par * kMaxSeg, nseg, s_pre, s_wsum);
     }
+#if PT_T4_COOP
+    int32_t* const qlist = s_qlist + wave * 64;
+    v4f* const stage = s_stage + wave * (PT_T4_COOP_ROWS * 8);
+#endif
     auto ray = [&](int k, f3& o, f3& d) -> int {   // as k_traverse
         if (FIRST) {
             PathReg p;
@@ -1777,6 +1802,41 @@ __global__ __launch_bounds__(kBlock, PT_T4_WAVES) void k_traverse4(const KArgs A
         // ---- the quad of every interior lane ----
         v4f x0, x1, x2, x3, x4, x5, x6;
         uint32_t meta;
+#if PT_T4_COOP
+        // The address path costs about one cycle per cache line per load instruction, so a lane
+        // fetching its own 112 B costs 7 line-accesses; eight lanes fetching one 128-B row together
+        // cost one (scripts/probes/gather_lds.hip: 11.7 -> 5.2-5.4 ps per row from L2).  The rows
+        // go through LDS to their owners; interior lanes of rank >= PT_T4_COOP_ROWS load their own.
+        const uint64_t imask = __ballot(inner);
+        const int n_in = __popcll(imask);
+        const int irank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(imask >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)imask, 0u));
+        const int nst = min(n_in, PT_T4_COOP_ROWS);   // (wave-uniform)
+        const bool staged = inner && irank < PT_T4_COOP_ROWS;
+        if (nst > 0) {
+            if (staged) qlist[irank] = cur & kQuadIdxMask;
+            wave_sync();
+            for (int j = 0; j * 8 < nst; ++j) {   // (wave-uniform) 8 rows per instruction
+                const int srow = j * 8 + (lane >> 3);
+                const int qi = qlist[min(srow, nst - 1)];
+                const int ck = ((lane & 7) - (srow >> 1)) & 7;   // the chunk whose column is lane & 7
+                const v4f* src = reinterpret_cast<const v4f*>(S.quads + qi) + ck;
+#if PT_T4_COOP == 2
+                if (srow < nst)
+                    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src),
+                                                     reinterpret_cast<__attribute__((address_space(3))) void*>(
+                                                         reinterpret_cast<uintptr_t>(stage + j * 64)),
+                                                     16, 0, 0);
+#else
+                if (srow < nst) stage[j * 64 + lane] = *src;
+#endif
+            }
+        }
+        if (inner && !staged) {
+            const v4f* qsrc = reinterpret_cast<const v4f*>(S.quads + (cur & kQuadIdxMask));
+            x0 = qsrc[0]; x1 = qsrc[1]; x2 = qsrc[2]; x3 = qsrc[3]; x4 = qsrc[4]; x5 = qsrc[5]; x6 = qsrc[6];
+        }
+#else
 #if PT_T4_LOADS == 1   // every lane loads (idle and leaf lanes: their last quad, cached): static wait counts
         {
 #else
@@ -1785,6 +1845,7 @@ __global__ __launch_bounds__(kBlock, PT_T4_WAVES) void k_traverse4(const KArgs A
             const v4f* qsrc = reinterpret_cast<const v4f*>(S.quads + (cur & kQuadIdxMask));
             x0 = qsrc[0]; x1 = qsrc[1]; x2 = qsrc[2]; x3 = qsrc[3]; x4 = qsrc[4]; x5 = qsrc[5]; x6 = qsrc[6];
         }
+#endif
         meta = (uint32_t)cur >> kQuadMetaShift;   // (the code that led here carries the quad's meta)
         f3 to = F3(0, 0, 0), td = F3(0, 0, 0);
         int tidx = 0;
@@ -1852,6 +1913,21 @@ __global__ __launch_bounds__(kBlock, PT_T4_WAVES) void k_traverse4(const KArgs A
         }
 #endif
         // ---- interior step ----
+#if PT_T4_COOP
+        if (nst > 0) {   // (wave-uniform) the staged rows have landed: each owner reads its row
+#if PT_T4_COOP == 2
+            __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0): the LDS-DMA writes
+#endif
+            wave_sync();
+            if (staged) {
+                const v4f* row = stage + irank * 8;
+                const int rot = irank >> 1;
+                x0 = row[(0 + rot) & 7]; x1 = row[(1 + rot) & 7]; x2 = row[(2 + rot) & 7];
+                x3 = row[(3 + rot) & 7]; x4 = row[(4 + rot) & 7]; x5 = row[(5 + rot) & 7];
+                x6 = row[(6 + rot) & 7];
+            }
+        }
+#endif
         int next = kWalkNone;
         if (inner) {
             uint32_t hm = quad_hits(x0, x1, x2, x3, x4, x5, o, inv) & meta & 15u;
