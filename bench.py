@@ -271,6 +271,16 @@ def _pmc_leg(args, scene_path, spp_pass, sorted_, avg_ms, kernel_prefix, seg_per
     out = {"pmc": res["_passes"], "traffic": m["bytes_per_launch"],
            "traffic_per_segment": m["bytes_per_launch"] / max(seg_per_launch, 1.0),
            "traffic_frac": m["bytes_per_launch"] / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+    iso_ns = m.get("dur_ns_sq") or m.get("dur_ns_fetch")
+    if iso_ns:   # rocprofv3 --pmc serialises the dispatches: each launch alone on the GPU
+        iso_ms = iso_ns * 1e-6
+        out["isolated"] = {
+            "avg_launch_ms": iso_ms,
+            "achieved": SEGMENT_BYTES * seg_per_launch / (iso_ms * 1e-3) / 1e9,
+            "frac": SEGMENT_BYTES * seg_per_launch / (iso_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "definition": "the same 184 B x segments per launch over the launch's duration in the rocprofv3 --pmc "
+                          "passes, where dispatches run one at a time (the line's avg_launch_ms shares the GPU "
+                          "with the other lane's launches)"}
     if "SQ_INSTS_VALU" in m:
         valu = m["SQ_INSTS_VALU"]
         wc = max(m.get("SQ_WAVE_CYCLES", 0.0), 1.0)
@@ -637,6 +647,10 @@ def main() -> None:
         except Exception as e:   # profiling is evidence, not the measurement: never fail the bench line
             extra = {"pmc_error": repr(e)}
         roofline.update(extra)
+        if "isolated" in roofline and roofline.get("launches"):
+            lps = roofline["launches"] / max(prof_passes, 1) * passes_per_step   # launches per step
+            roofline["isolated"]["launches_per_step"] = lps
+            roofline["isolated"]["ms_per_step_if_serial"] = lps * roofline["isolated"]["avg_launch_ms"]
     if rank == 0 and world == 1 and walk and not args.no_walk_counters:
         roofline["walk_counters"] = _walk_counters(scene_path, spp)
     if rank == 0:
