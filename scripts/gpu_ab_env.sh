@@ -8,7 +8,7 @@ for k in $(seq 1 ${RUNS:-3}); do
   for v in ${VARIANTS:-base:}; do
     name=${v%%:*}; assigns=${v#*:}
     ( IFS=','; for a in $assigns; do export "$a"; done; unset IFS
-      timeout -k 10 300 python -u bench.py --steps ${STEPS:-20} --warmup 3 --no-cpu-baseline --no-scan --no-pmc ${BENCH_ARGS:-} \
+      timeout -k 10 300 python -u bench.py --steps ${STEPS:-20} --warmup 3 --no-cpu-baseline --no-scan --no-pmc --no-dropin ${BENCH_ARGS:-} \
           > $O/b_${name}_$k.json 2> $O/b_${name}_$k.err ) || { echo "bench $name failed"; tail -5 $O/b_${name}_$k.err; exit 1; }
     python -c "import json;d=json.load(open('$O/b_${name}_$k.json'));r=d['roofline'];print('$name', round(d['value'],1), round(d['ms_per_step'],3), 'k_bounce', round(r['avg_launch_ms']*1e3,1), 'us')"
   done
