@@ -358,7 +358,7 @@ def main() -> None:
     ap.add_argument("--pmc-timeout", type=int, default=150)
     ap.add_argument("--scene", default=str(ROOT / "tests" / "scenes" / "cornell.json"))
     ap.add_argument("--config", default="cornell", choices=["cornell", "cornell_hd_sorted", "multi_object_4k",
-                                                           "random_triangles_100k"],
+                                                           "random_triangles_100k", "tessellated_meshes_100k"],
                     help="BASELINE.json workload: cornell (configs[1], the default line) or configs 3-5 "
                          "generated by cuda_pathtracer_amd.scenes")
     ap.add_argument("--bvh-cull", action="store_true", help="pt_flags.bvh_cull extension (mesh scenes)")
@@ -376,7 +376,8 @@ def main() -> None:
     ap.add_argument("--samples", type=int, default=256, help="strong scaling: samples per pixel per step")
     args = ap.parse_args()
     if args.spp is None:   # iterations per pass, measured per workload
-        args.spp = {"cornell": 256, "cornell_hd_sorted": 256, "multi_object_4k": 128, "random_triangles_100k": 128}[args.config]
+        args.spp = {"cornell": 256, "cornell_hd_sorted": 256, "multi_object_4k": 128, "random_triangles_100k": 128,
+                    "tessellated_meshes_100k": 128}[args.config]
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -426,6 +427,8 @@ def main() -> None:
         workload = {"cornell_hd_sorted": "config 3: cornell geometry 1920x1080 DEPTH 16, material-sorted shading",
                     "multi_object_4k": "config 4: 4K multi-object (spheres+boxes; diffuse, mirror, glass) DEPTH 8",
                     "random_triangles_100k": "config 5: 100k random triangles via OBJ+BVH, 4K, DEPTH 32",
+                    "tessellated_meshes_100k": "not a BASELINE config: 100k small triangles (tessellated sphere "
+                                               "+ torus) via OBJ+BVH, 1920x1080, DEPTH 16 (the exact t-cull's case)",
                     }[args.config]
     gui.bvhCull = bool(args.bvh_cull)
     scene = P.Scene(scene_path)
@@ -447,6 +450,7 @@ def main() -> None:
     if spp > 256:   # pt_shard.spp limit (one thread of the bounce kernel's workgroup per iteration)
         raise SystemExit(f"{spp} iterations per pass > 256 (pt_shard.spp limit)")
     pt = P.PathTracer(scene, gui, rank=rank, world=sw, spp=spp)
+    walk_info = pt.walk_info() if scene.counts()[2] > 0 else None
     stream = torch.cuda.current_stream()
     _log(rank, f"[bench] {args.scaling} scaling: tile rows={pt.rows} npix={pt.npix} paths/pass={pt.npaths} "
                f"passes/step={passes_per_step} depth={st_r.traceDepth}")
@@ -570,6 +574,7 @@ def main() -> None:
             "frac": bb / (b_avg * 1e-3) / 1e9 / HBM_PEAK_GBS if b_avg > 0 else 0.0,
             "kernel_min_bytes_per_launch": kernel_min / max(b_n, 1)}
         roofline["walk_share_of_gpu_time"] = t_ms / max(t_ms + b_ms + f_ms + prof["first_traverse"][0], 1e-9)
+        roofline["walk_info"] = walk_info   # 4-wide walk, its exact t-cull on/off, share of slots it can cull
         roofline["first_traverse_avg_ms"] = prof["first_traverse"][0] / max(prof["first_traverse"][1], 1)
 
     result = None

@@ -130,10 +130,12 @@ SIGNATURES = {
     "pt_scene_get_triangles": (_I, [_P, C.POINTER(Triangle), _I]),
     "pt_scene_get_bvh": (_I, [_P, C.POINTER(BvhNode), _I]),
     "pt_scene_bvh_quads": (_I, [_P, _P, _I, _IP, _IP]),
+    "pt_scene_bvh_tcull": (_I, [_P, C.POINTER(C.c_uint32), _I, C.POINTER(C.c_double)]),
     "pt_create": (_I, [_P, C.POINTER(Flags), C.POINTER(Shard), C.POINTER(_P)]),
     "pt_destroy": (_I, [_P]),
     "pt_set_flags": (_I, [_P, C.POINTER(Flags)]),
     "pt_ctx_counters": (_I, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    "pt_ctx_walk_info": (_I, [_P, C.POINTER(_I), C.POINTER(_I), C.POINTER(C.c_double)]),
     "pt_render_pass": (_I, [_P, _I, _P]),
     "pt_preview_rgba": (_I, [_P, _I, _P, _P]),
     "pt_tile_info": (_I, [_P, _IP, _IP, _IP, _IP]),

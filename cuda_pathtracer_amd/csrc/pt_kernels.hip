@@ -84,6 +84,7 @@ struct SceneDev {
     const struct DQuad* __restrict__ quads;   // 4-wide collapse of the pair tree (k_traverse4), or null
     int32_t root_qcode;    // root's code in the quad layout (quad index or leaf code)
     const float* __restrict__ tpack;   // the triangles again as packed 36-byte (v0, e1, e2): k_traverse4's task loads
+    const uint32_t* __restrict__ qcull;   // exact t-cull margins of the quads' slots (build_qcull), or null: off
 };
 struct CamDev {
     float pos[3], view[3], up[3], right[3], pl[2];
@@ -1695,6 +1696,7 @@ __global__ __launch_bounds__(kBlock, PT_T4_WAVES) void k_traverse4(const KArgs A
     int q = 0, cur = 0, top = 0, ti = 0, te = 0;
     f3 o = F3(0, 0, 0), d = F3(0, 0, 0), inv = F3(0, 0, 0);
     uint32_t negm = 0;
+    bool cullok = false;   // exact t-cull (S.qcull): the ray's |d|^2 lies in the margins' range
     MeshHit r{false, -1, -1, kFLT_MAX, 0.f, 0.f};
     auto enter = [&](int code) {
         leaf = code < 0;
@@ -1738,6 +1740,10 @@ __global__ __launch_bounds__(kBlock, PT_T4_WAVES) void k_traverse4(const KArgs A
                     const bool finite = __builtin_isfinite(inv.x) && __builtin_isfinite(inv.y) &&
                                         __builtin_isfinite(inv.z) && __builtin_isfinite(o.x) &&
                                         __builtin_isfinite(o.y) && __builtin_isfinite(o.z);
+                    {   // |d|^2 within [1 - 2^-18, 1 + 2^-18] (its float value is within 3 ulp of exact)
+                        const float dd = dot(d, d);
+                        cullok = dd >= 1.0f - 0x1p-18f + 0x1p-22f && dd <= 1.0f + 0x1p-18f - 0x1p-22f;
+                    }
                     top = 0;
                     r = MeshHit{false, -1, -1, kFLT_MAX, 0.f, 0.f};
                     const float bmin[3] = {S.root_lo[0], S.root_lo[1], S.root_lo[2]};
@@ -1847,6 +1853,9 @@ __global__ __launch_bounds__(kBlock, PT_T4_WAVES) void k_traverse4(const KArgs A
         }
 #endif
         meta = (uint32_t)cur >> kQuadMetaShift;   // (the code that led here carries the quad's meta)
+        typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+        v4u cw = {0u, 0u, 0u, 0u};   // the quad's exact t-cull words (one per slot)
+        if (S.qcull && inner) cw = *reinterpret_cast<const v4u*>(S.qcull + 4 * (size_t)(cur & kQuadIdxMask));
         f3 to = F3(0, 0, 0), td = F3(0, 0, 0);
         int tidx = 0;
         if (T > 0) {   // (wave-uniform)
@@ -1931,6 +1940,24 @@ __global__ __launch_bounds__(kBlock, PT_T4_WAVES) void k_traverse4(const KArgs A
         int next = kWalkNone;
         if (inner) {
             uint32_t hm = quad_hits(x0, x1, x2, x3, x4, x5, o, inv) & meta & 15u;
+            // Exact t-cull: a slot whose box puts a lower bound on glm's computed t of
+            // every triangle below it above the best t found so far is not entered — none of them can
+            // replace the best or tie it, and the slots entered keep the reference's order.
+            if (S.qcull && cullok && r.t < kFLT_MAX) {
+                uint32_t cm = 0u;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const float sx = (negm & 1u) ? x1[k] : x0[k];   // the box corner nearest along d
+                    const float sy = (negm & 2u) ? x3[k] : x2[k];
+                    const float sz = (negm & 4u) ? x5[k] : x4[k];
+                    const float tx = (sx - o.x) * d.x, ty = (sy - o.y) * d.y, tz = (sz - o.z) * d.z;
+                    const float lo = ((tx + ty) + tz) - ((fabsf(tx) + fabsf(ty)) + fabsf(tz)) * 0x1p-20f;
+                    const float A = (float)__builtin_bit_cast(_Float16, (uint16_t)(cw[k] & 0xffffu));
+                    const float B = (float)__builtin_bit_cast(_Float16, (uint16_t)(cw[k] >> 16));
+                    if (lo > 0.0f && (A * lo) * (1.0f - 0x1p-20f) > (B + r.t) * (1.0f + 0x1p-20f)) cm |= 1u << k;
+                }
+                hm &= ~cm;
+            }
             int c0 = __float_as_int(x6[0]), c1 = __float_as_int(x6[1]);
             int c2 = __float_as_int(x6[2]), c3 = __float_as_int(x6[3]);
             // near-first order: within each group by its axis, then the groups by N's axis
@@ -2915,6 +2942,7 @@ struct pt_ctx {
     int grid_traverse4 = 0;              // k_traverse4 (4-wide layout): the same for its footprint
     int cus = 256;                       // compute units of the device
     int quad_occ = 0;                    // k_traverse4: bound on its stack occupancy (build_quads)
+    double tcull_frac = 0.0;             // share of quad slots whose exact t-cull margin can pay (build_qcull)
     bool trav_quads = false;             // mesh mode 2 walks the 4-wide layout (PT_AMD_TRAV=pairs: off)
     hipStream_t fin_stream = nullptr;
     hipEvent_t ev_pass[2] = {}, ev_fin[2] = {};
@@ -3399,9 +3427,11 @@ std::vector<DNode> to_dnodes(const std::vector<pt_bvh_node>& bvh) {
 }
 
 // Host part: fills `quads`, the root's code and the stack bound; false = no quad layout.
-bool make_quads(const std::vector<DNode>& nodes, std::vector<DQuad>& quads, int32_t& root_code, int32_t& root_occ) {
+bool make_quads(const std::vector<DNode>& nodes, std::vector<DQuad>& quads, int32_t& root_code, int32_t& root_occ,
+                std::vector<int32_t>* slot_node = nullptr) {
     const size_t n = nodes.size();
     quads.clear();
+    if (slot_node) slot_node->clear();
     if (n == 0) return false;
     auto meta = [&](size_t i) { return __float_as_int_host(nodes[i].lo[3]); };
     auto link = [&](size_t i) { return __float_as_int_host(nodes[i].hi[3]); };
@@ -3443,6 +3473,7 @@ bool make_quads(const std::vector<DNode>& nodes, std::vector<DQuad>& quads, int3
     }
     if (order.size() > (size_t)kQuadIdxMask) return false;
     quads.resize(std::max<size_t>(order.size(), 1));
+    if (slot_node) slot_node->assign(4 * quads.size(), -1);
     occ.assign(order.size(), 0);
     // each quad's meta first: the interior codes pointing at a quad carry it
     std::vector<uint32_t> qmeta(order.size(), 0);
@@ -3476,6 +3507,7 @@ bool make_quads(const std::vector<DNode>& nodes, std::vector<DQuad>& quads, int3
                 valid |= 1u << s;
                 box[s] = y;
                 codes[s] = meta(y) > 0 ? leaf_code(y) : qcode(y);
+                if (slot_node) (*slot_node)[4 * qi + (size_t)s] = (int32_t)y;
             };
             if (meta(x) <= 0 && inside(x + 1, x) && inside((size_t)link(x), x)) {
                 slot(2 * g, x + 1);
@@ -3515,16 +3547,105 @@ bool make_quads(const std::vector<DNode>& nodes, std::vector<DQuad>& quads, int3
     return root_occ <= 64;   // HybStack holds rows + 64 >= 64 entries
 }
 
-int build_quads(pt_ctx* c, const std::vector<DNode>& nodes) {
+// IEEE binary16 bits of x >= 0 rounded down (toward 0) or up (toward +inf; +inf past the range).
+uint16_t half_dir(double x, bool up) {
+    if (!(x >= 0.0)) return up ? (uint16_t)0x7c00 : (uint16_t)0;
+    auto val = [](uint16_t bits) {
+        _Float16 t;
+        std::memcpy(&t, &bits, 2);
+        return (double)t;
+    };
+    const _Float16 h = (_Float16)(float)x;
+    uint16_t b;
+    std::memcpy(&b, &h, 2);
+    if (up) {
+        while (b < 0x7c00 && val(b) < x) ++b;
+    } else {
+        while (b > 0 && val(b) > x) --b;
+    }
+    return b;
+}
+
+// Exact t-cull margins of the 4-wide walk (DESIGN.md §4.3 "exact t-cull").  For a triangle with
+// float edges e1, e2 that glm::intersectRayTriangle reports hit (gtx/intersect.inl:37-74: the
+// determinant a >= FLT_EPSILON, barycentrics in range), its computed t satisfies
+//     t >= (tau_min(B) - (g lambda + 4.8 u) diam / |d|) / (1 + g),   g = c (1 + u) / (1 - c),
+//     c = (1 + u)(9 |e1||e2| |d| + 1.74 u),  lambda = 1 + 3.01 u,  diam = max(|e1|, |e2|),
+// for every box B that holds the triangle, tau_min(B) = min over B of (X - o).d / |d|^2 (u = 2^-24).
+// Per quad slot (a node of the reference tree) with the maxima of |e1||e2| and diam over its
+// subtree: the slot's children are culled when A tau_lo > B + best (with relative slack), where
+// A = 1 / ((1 + g)(1 + 2^-18)) (|d|^2 in [1 - 2^-18, 1 + 2^-18], checked per ray) rounded down and
+// B = (g lambda + 4.8 u) diam / ((1 - 2^-19)(1 + g)) rounded up, both as binary16: one 32-bit word
+// per slot, A | B << 16.  c >= 1 (large triangles): A = 0, B = inf, never culled.
+// Returns the fraction of valid slots with A >= 1/2 (the share where the cull can pay).
+double build_qcull(const std::vector<DNode>& nodes, const std::vector<pt_triangle>& tris,
+                   const std::vector<int32_t>& slot_node, std::vector<uint32_t>& qcull) {
+    const size_t n = nodes.size();
+    std::vector<double> mmax(n, 0.0), dmax(n, 0.0);
+    for (size_t i = n; i-- > 0;) {
+        const int32_t meta = __float_as_int_host(nodes[i].lo[3]), link = __float_as_int_host(nodes[i].hi[3]);
+        if (meta > 0) {
+            for (int32_t k = link; k < link + meta && (size_t)k < tris.size(); ++k) {
+                const pt_triangle& t = tris[(size_t)k];
+                double l1 = 0.0, l2 = 0.0;
+                for (int a = 0; a < 3; ++a) {
+                    const float e1 = t.v[1][a] - t.v[0][a], e2 = t.v[2][a] - t.v[0][a];   // the device's e1, e2
+                    l1 += (double)e1 * e1;
+                    l2 += (double)e2 * e2;
+                }
+                l1 = std::sqrt(l1) * (1.0 + 1e-12);
+                l2 = std::sqrt(l2) * (1.0 + 1e-12);
+                mmax[i] = std::max(mmax[i], l1 * l2 * (1.0 + 1e-12));
+                dmax[i] = std::max(dmax[i], std::max(l1, l2));
+                if (!std::isfinite(l1 * l2)) mmax[i] = HUGE_VAL;
+            }
+        } else if ((size_t)link < n && i + 1 < n) {
+            mmax[i] = std::max(mmax[i + 1], mmax[(size_t)link]);
+            dmax[i] = std::max(dmax[i + 1], dmax[(size_t)link]);
+        }
+    }
+    const double u = std::ldexp(1.0, -24), lam = 1.0 + 3.01 * u;
+    const double dhi = 1.0 + std::ldexp(1.0, -19), dlo = 1.0 - std::ldexp(1.0, -19);
+    qcull.assign(slot_node.size(), 0x7c000000u);   // A = 0, B = inf
+    size_t valid = 0, good = 0;
+    for (size_t k = 0; k < slot_node.size(); ++k) {
+        const int32_t y = slot_node[k];
+        if (y < 0) continue;
+        ++valid;
+        const double c = (1.0 + u) * (9.0 * mmax[(size_t)y] * dhi + 1.74 * u);
+        if (!(c < 1.0)) continue;
+        const double g = c * (1.0 + u) / (1.0 - c);
+        const double A = 1.0 / ((1.0 + g) * (1.0 + std::ldexp(1.0, -18))) * (1.0 - 1e-12);
+        const double B = (g * lam + 4.8 * u) * dmax[(size_t)y] / (dlo * (1.0 + g)) * (1.0 + 1e-12);
+        qcull[k] = (uint32_t)half_dir(A, false) | ((uint32_t)half_dir(B, true) << 16);
+        if (A >= 0.5) ++good;
+    }
+    return valid ? (double)good / (double)valid : 0.0;
+}
+
+int build_quads(pt_ctx* c, const std::vector<DNode>& nodes, const std::vector<pt_triangle>& tris) {
     std::vector<DQuad> quads;
+    std::vector<int32_t> slot_node;
     int32_t root_code = 0, occ = 0;
-    if (!make_quads(nodes, quads, root_code, occ)) return PT_OK;
+    if (!make_quads(nodes, quads, root_code, occ, &slot_node)) return PT_OK;
     DQuad* d_quads;
     if (int rc = c->alloc(&d_quads, quads.size())) return rc;
     HIP_TRY(hipMemcpy(d_quads, quads.data(), quads.size() * sizeof(DQuad), hipMemcpyHostToDevice));
     c->args.S.quads = d_quads;
     c->args.S.root_qcode = root_code;
     c->quad_occ = occ;
+    // exact t-cull: on when at least a quarter of the slots can cull (A >= 1/2), PT_AMD_TCULL=0/1 forces
+    std::vector<uint32_t> qcull;
+    c->tcull_frac = build_qcull(nodes, tris, slot_node, qcull);
+    bool on = c->tcull_frac >= 0.25;
+    if (const char* e = std::getenv("PT_AMD_TCULL")) on = std::strcmp(e, "1") == 0;
+    c->args.S.qcull = nullptr;
+    if (on) {
+        uint32_t* d_q;
+        if (int rc = c->alloc(&d_q, qcull.size())) return rc;
+        HIP_TRY(hipMemcpy(d_q, qcull.data(), qcull.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        c->args.S.qcull = d_q;
+    }
     return PT_OK;
 }
 
@@ -3755,7 +3876,7 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
             A.S.pairs = d_pairs;
             A.S.root_code = code(0);
             for (int k = 0; k < 4; ++k) { A.S.root_lo[k] = nodes[0].lo[k]; A.S.root_hi[k] = nodes[0].hi[k]; }
-            if (int rc = build_quads(c, nodes)) return bail(rc);
+            if (int rc = build_quads(c, nodes, S.triangles)) return bail(rc);
         }
     }
     if (!S.textures.empty()) {
@@ -3978,6 +4099,14 @@ int pt_set_flags(pt_ctx* c, const pt_flags* f) {
     }
     HIP_TRY(hipDeviceSynchronize());   // (queued first bounces still read the old masks)
     return build_cmask(c);   // SSAA / DoF / aperture / focal distance bound the camera rays
+}
+
+int pt_ctx_walk_info(const pt_ctx* c, int32_t* quad_walk, int32_t* tcull_on, double* tcull_frac) {
+    if (!c) return pt::fail(PT_ERR_ARG, "null context");
+    if (quad_walk) *quad_walk = c->trav_quads ? 1 : 0;
+    if (tcull_on) *tcull_on = c->args.S.qcull != nullptr ? 1 : 0;
+    if (tcull_frac) *tcull_frac = c->tcull_frac;
+    return PT_OK;
 }
 
 int pt_ctx_counters(const pt_ctx* c, uint64_t* mask_builds, uint64_t* flag_syncs) {
@@ -4291,6 +4420,21 @@ int pt_scene_bvh_quads(const pt_scene* scene, void* out, int32_t cap, int32_t* r
     if (stack_bound) *stack_bound = occ;
     if (out && cap > 0) std::memcpy(out, quads.data(), std::min<size_t>((size_t)cap, quads.size()) * sizeof(DQuad));
     return (int)quads.size();
+}
+
+int pt_scene_bvh_tcull(const pt_scene* scene, uint32_t* words, int32_t cap, double* cullable_frac) {
+    if (!scene) return -PT_ERR_ARG;
+    const auto& S = *reinterpret_cast<const pt::Scene*>(scene);
+    std::vector<DQuad> quads;
+    std::vector<int32_t> slot_node;
+    int32_t rc = 0, occ = 0;
+    const std::vector<DNode> nodes = to_dnodes(S.bvh);
+    if (!make_quads(nodes, quads, rc, occ, &slot_node)) return 0;
+    std::vector<uint32_t> q;
+    const double frac = build_qcull(nodes, S.triangles, slot_node, q);
+    if (cullable_frac) *cullable_frac = frac;
+    if (words && cap > 0) std::memcpy(words, q.data(), std::min<size_t>((size_t)cap, q.size()) * sizeof(uint32_t));
+    return (int)q.size();
 }
 
 int pt_selftest_math(uint64_t n, uint32_t seed, uint64_t* mismatches) {

@@ -290,6 +290,13 @@ class PathTracer:
         check_pt(lib().pt_ctx_counters(self._h, C.byref(b), C.byref(y)))
         return {"mask_builds": int(b.value), "flag_syncs": int(y.value)}
 
+    def walk_info(self) -> dict:
+        """Mesh scenes: 4-wide walk on/off, its exact t-cull on/off and the share of slots whose
+        cull margin can pay (pt_ctx_walk_info)."""
+        qw, on, fr = C.c_int32(), C.c_int32(), C.c_double()
+        check_pt(lib().pt_ctx_walk_info(self._h, C.byref(qw), C.byref(on), C.byref(fr)))
+        return {"quad_walk": bool(qw.value), "tcull": bool(on.value), "tcull_frac": float(fr.value)}
+
     def render_pass(self, iter_first: int, stream=None) -> None:
         """pathtrace(): iterations [iter_first, iter_first + spp) for this tile, asynchronous."""
         check_pt(lib().pt_render_pass(self._h, int(iter_first), _stream_ptr(stream)))

@@ -123,6 +123,54 @@ def random_triangles(out_dir, n=100_000, res=(3840, 2160), depth=32, seed=5) -> 
     return _write(out_dir, name, scene)
 
 
+def _grid_mesh(pos, nu, nv, wrap_v):
+    """Quads of a (nu x nv) parametric grid (u wraps; v wraps when wrap_v) split into triangles."""
+    idx = lambda i, j: (i % nu) * nv + (j % nv)
+    faces = []
+    for i in range(nu):
+        for j in range(nv if wrap_v else nv - 1):
+            a, b, c, d = idx(i, j), idx(i + 1, j), idx(i + 1, j + 1), idx(i, j + 1)
+            faces += [(a, b, c), (a, c, d)]
+    return pos.reshape(-1, 3), faces
+
+
+def tessellated_meshes(out_dir, res=(1920, 1080), depth=16) -> str:
+    """Not a BASELINE workload: 100k small triangles on two closed surfaces (a UV sphere of 60k
+    triangles and a torus of 40k) in the lit box — the shape of a real tessellated model, where the
+    4-wide walk's exact t-cull pays, unlike config 5's large random triangles."""
+    out = Path(out_dir)
+    (out / "Models").mkdir(parents=True, exist_ok=True)
+    nu, nv = 200, 151
+    th = np.linspace(0.0, 2.0 * np.pi, nu, endpoint=False)[:, None]
+    ph = np.linspace(0.0, np.pi, nv)[None, :]
+    sph = np.stack([np.sin(ph) * np.cos(th), np.cos(ph) + 0.0 * th, np.sin(ph) * np.sin(th)], axis=-1)
+    sph = sph * 2.2 + np.array([-1.5, 3.2, -1.0])
+    v1, f1 = _grid_mesh(sph, nu, nv, False)
+    mu, mv = 200, 100
+    a = np.linspace(0.0, 2.0 * np.pi, mu, endpoint=False)[:, None]
+    b = np.linspace(0.0, 2.0 * np.pi, mv, endpoint=False)[None, :]
+    R, r = 1.6, 0.55
+    tor = np.stack([(R + r * np.cos(b)) * np.cos(a), r * np.sin(b) + 0.0 * a, (R + r * np.cos(b)) * np.sin(a)], axis=-1)
+    tor = tor + np.array([2.2, 1.2, 0.5])
+    v2, f2 = _grid_mesh(tor, mu, mv, True)
+    verts = np.concatenate([v1, v2])
+    faces = f1 + [(x + len(v1), y + len(v1), z + len(v1)) for x, y, z in f2]
+    fa = np.array(faces)
+    nrm = np.cross(verts[fa[:, 1]] - verts[fa[:, 0]], verts[fa[:, 2]] - verts[fa[:, 0]])
+    nrm /= np.maximum(np.linalg.norm(nrm, axis=1, keepdims=True), 1e-12)
+    lines = ["# tessellated sphere + torus (cuda_pathtracer_amd.scenes.tessellated_meshes)"]
+    lines += [f"v {x:.6f} {y:.6f} {z:.6f}" for x, y, z in verts]
+    lines += [f"vn {x:.6f} {y:.6f} {z:.6f}" for x, y, z in nrm]
+    lines += [f"f {x + 1}//{i + 1} {y + 1}//{i + 1} {z + 1}//{i + 1}" for i, (x, y, z) in enumerate(faces)]
+    name = f"tess{len(faces)}"
+    (out / "Models" / f"{name}.obj").write_text("\n".join(lines) + "\n")
+    objs = _room()
+    objs.append({"TYPE": "mesh", "MATERIAL": "diffuse_white", "OBJ_FILE": f"{name}.obj",
+                 "TRANS": [0.0, 0.0, 0.0], "ROTAT": [0.0, 0.0, 0.0], "SCALE": [1.0, 1.0, 1.0]})
+    scene = {"Materials": dict(CORNELL_MATERIALS), "Camera": _camera(res, depth, 5000, name), "Objects": objs}
+    return _write(out_dir, name, scene)
+
+
 def random_primitives(out_dir, n=24, res=(640, 480), depth=8, seed=7, extra_materials=0) -> str:
     """Stress scene for the bounded closest-hit pass (not a BASELINE workload): the Cornell shell
     plus n cubes and spheres with random rotations and strongly non-uniform scales (thin slabs,
@@ -158,4 +206,5 @@ CONFIGS = {
     "cornell_hd_sorted": cornell_hd,
     "multi_object_4k": multi_object,
     "random_triangles_100k": random_triangles,
+    "tessellated_meshes_100k": tessellated_meshes,   # (not a BASELINE workload: the exact t-cull's case)
 }

@@ -216,6 +216,11 @@ int pt_scene_get_bvh(const pt_scene* s, pt_bvh_node* out, int32_t cap);
  * codes in pt_kernels.hip DQuad).  Returns the entry count (0: no 4-wide layout for this tree; the
  * pair walk runs) and copies min(count, cap) entries; *root_code / *stack_bound as pt_create uses. */
 int pt_scene_bvh_quads(const pt_scene* s, void* out, int32_t cap, int32_t* root_code, int32_t* stack_bound);
+/* Inspection (host only): the 4-wide walk's exact t-cull words, 4 per quad in pt_scene_bvh_quads's
+ * order (slot k: binary16 A in bits 0-15, binary16 B in bits 16-31; a slot's children are not entered
+ * when A * tau_lo > B + best), and the share of slots with A >= 1/2.  Returns the word
+ * count (0: no 4-wide layout) and copies min(count, cap) words. */
+int pt_scene_bvh_tcull(const pt_scene* s, uint32_t* words, int32_t cap, double* cullable_frac);
 
 /* ---- render context -------------------------------------------------------------------- */
 /* pathtraceInit: uploads the scene to the current HIP device, allocates SoA path buffers for
@@ -229,6 +234,10 @@ int pt_set_flags(pt_ctx* c, const pt_flags* flags);
 /* Host-side counters of a context: first-bounce camera-mask builds (pt_create builds one) and the
  * pt_set_flags calls that synchronised the device. */
 int pt_ctx_counters(const pt_ctx* c, uint64_t* mask_builds, uint64_t* flag_syncs);
+/* Mesh scenes: whether the BVH walk runs on the 4-wide layout, whether its exact t-cull is on, and
+ * the share of the layout's slots whose cull margin can pay.  The cull is on when
+ * that share is >= 1/4 (PT_AMD_TCULL=0/1 forces it); it never changes a result. */
+int pt_ctx_walk_info(const pt_ctx* c, int32_t* quad_walk, int32_t* tcull_on, double* tcull_frac);
 /* One pass: iterations [iter_first, iter_first + spp) for this tile, accumulated into the tile
  * image.  Asynchronous on `stream`; no host synchronisation inside.  A batched pass (spp > 1)
  * runs its iterations in lanes on internal streams and adds their colours into the image on a

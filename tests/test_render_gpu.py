@@ -551,6 +551,53 @@ def test_bvh_walk_records_equal_reference_walk(room_path, config_scenes, tmp_pat
     assert total > 200_000
 
 
+@pytest.mark.parametrize("mode", ["auto", "forced"])
+def test_exact_tcull_records_equal_reference_walk(room_path, config_scenes, tmp_path, monkeypatch, mode):
+    """The 4-wide walk's exact t-cull changes no record: with PT_AMD_VERIFY_BOUNDS=1
+    the mesh bounce kernel re-runs the reference's node-at-a-time BVHIntersectionTest for every ray
+    and counts 0 differences in the closest triangle, t and barycentrics.  "auto": the cull is on
+    where the margins pay (the tessellated scene's 100k small triangles, room.json) and off on
+    config 5; "forced" (PT_AMD_TCULL=1): on everywhere, config 5's 100k large triangles included."""
+    from cuda_pathtracer_amd import PathTracer, Scene, scenes
+    monkeypatch.setenv("PT_AMD_VERIFY_BOUNDS", "1")
+    if mode == "forced":
+        monkeypatch.setenv("PT_AMD_TCULL", "1")
+    tess = scenes.tessellated_meshes(tmp_path / "t", res=(200, 112), depth=16)
+    big = scenes.random_triangles(tmp_path / "b", n=100_000, res=(320, 180), depth=32)
+    total = 0
+    for path, spp, expect in ((tess, 4, True), (room_path, 4, True), (config_scenes["random_triangles"], 4, None),
+                              (big, 2, mode == "forced")):
+        s = Scene(path)
+        if path == room_path:
+            s.set_camera((96, 72), 45.0, (0, 5, 10.5), (0, 5, 0), (0, 1, 0))
+            s.finalize()
+        pt = PathTracer(s, _gui(), spp=spp)
+        info = pt.walk_info()
+        assert info["quad_walk"]
+        if expect is not None:
+            assert info["tcull"] == expect, (path, info)
+        for k in range(2):
+            pt.render_pass(1 + spp * k)
+        st = pt.stats()
+        pt.free()
+        assert st["bound_mismatch"] == 0, (path, st["bound_mismatch"])
+        total += st["segments"]
+    assert total > 400_000
+
+
+def test_tessellated_meshes_bitexact_with_tcull(tmp_path):
+    """The exact t-cull's own workload (100k small triangles on a sphere and a torus): the GPU image
+    equals the oracle's (which walks the whole reference tree, no cull) bit for bit, batched and not."""
+    from cuda_pathtracer_amd import PathTracer, Scene, scenes
+    path = scenes.tessellated_meshes(tmp_path, res=(160, 90), depth=16)
+    s = Scene(path)
+    assert PathTracer(s, _gui()).walk_info()["tcull"]
+    for spp in (1, 2):
+        g, r, st, live = _run(Scene(path), O.OracleScene.from_json(path), _gui(), iters=2, spp=spp)
+        _assert_bitexact(g, r, f"tessellated meshes spp={spp}")
+        assert st["bounce_live"] == live and r.sum() > 0
+
+
 def test_refraction_keys_render_like_bundled_scene(cornell_path, tmp_path):
     """A reference scene file carrying REFRACTIVE / IOR (keys scene.cpp:46-56 never reads) renders
     bit-identically to the bundled cornell.json when the loader extension is off (the default),

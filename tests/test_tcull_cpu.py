@@ -83,3 +83,95 @@ def test_grazing_ray_computed_t_far_before_the_box(tmp_path):
     n = np.cross((v[1] - v[0]).astype(np.float64), (v[2] - v[0]).astype(np.float64))
     t_geo = np.dot(v[0].astype(np.float64) - o, n) / np.dot(d.astype(np.float64), n)
     assert t_geo > 1.2
+
+
+def _tcull_tables(path):
+    import ctypes as C
+    s = P.Scene(path)
+    fr = C.c_double()
+    n = N.lib().pt_scene_bvh_tcull(s.handle, None, 0, C.byref(fr))
+    words = (C.c_uint32 * n)()
+    assert N.lib().pt_scene_bvh_tcull(s.handle, words, n, C.byref(fr)) == n
+    w = np.frombuffer(bytes(words), np.uint32).reshape(-1, 4)
+    nq = N.lib().pt_scene_bvh_quads(s.handle, None, 0, None, None)
+    buf = (C.c_uint8 * (128 * nq))()
+    assert N.lib().pt_scene_bvh_quads(s.handle, buf, nq, None, None) == nq == len(w)
+    q = np.frombuffer(bytes(buf), np.dtype([("b", "<f4", (6, 4)), ("code", "<i4", 4), ("meta", "<i4", 4)]))
+    nt = s.counts()[2]
+    arr = (N.Triangle * nt)()
+    assert N.lib().pt_scene_get_triangles(s.handle, arr, nt) == nt
+    tv = np.array([[list(t.v[k]) for k in range(3)] for t in arr], f32)   # BVH order
+    return s, fr.value, w, q, tv
+
+
+def _leaf_range(code):
+    c = -int(code) - 1
+    return c >> 8, (c >> 8) + (c & 255)
+
+
+import pytest   # noqa: E402
+
+
+@pytest.mark.parametrize("scene", ["tessellated", "config5"])
+def test_tcull_margins_only_skip_worse_hits(tmp_path, scene):
+    """The walk's exact t-cull (pt_kernels.hip k_traverse4; margins from build_qcull, DESIGN.md
+    §4.3) enters no slot whose margin says A * tau_lo > B + best.  For leaf slots of the tessellated
+    scene (the cull's case) and of config 5 (whose large triangles mostly get no margin), rays aimed
+    at the leaf's triangles — a third of them grazing the triangle's plane at the FLT_EPSILON
+    threshold — must give every computed glm t at or above the largest `best` the slot would be
+    culled at: (A tau_lo)(1 - 2^-20) / (1 + 2^-20) - B, with tau_lo computed as the kernel does."""
+    path = (scenes.tessellated_meshes(tmp_path, res=(64, 36)) if scene == "tessellated"
+            else scenes.random_triangles(tmp_path, n=100_000, res=(64, 36), depth=32))
+    _, frac, w, q, tv = _tcull_tables(path)
+    assert (frac >= 0.25) == (scene == "tessellated")
+    rng = np.random.default_rng(7)
+    leaf_slots = [(qi, k) for qi in range(len(q)) for k in range(4)
+                  if (q["meta"][qi, 0] >> k) & 1 and q["code"][qi, k] < 0 and (w[qi, k] & 0xffff) != 0]
+    assert len(leaf_slots) > 100
+    checked = hits = 0
+    for idx in rng.choice(len(leaf_slots), size=min(400, len(leaf_slots)), replace=False):
+        qi, k = leaf_slots[idx]
+        A = float(np.array([w[qi, k] & 0xffff], np.uint16).view(np.float16)[0])
+        B = float(np.array([w[qi, k] >> 16], np.uint16).view(np.float16)[0])
+        lo_b = np.array([q["b"][qi, 0, k], q["b"][qi, 2, k], q["b"][qi, 4, k]], f32)
+        hi_b = np.array([q["b"][qi, 1, k], q["b"][qi, 3, k], q["b"][qi, 5, k]], f32)
+        t0, t1 = _leaf_range(q["code"][qi, k])
+        for _ in range(12):
+            ti = rng.integers(t0, t1)
+            v = tv[ti].astype(np.float64)
+            a_, b_ = rng.uniform(0, 1, 2)
+            if a_ + b_ > 1:
+                a_, b_ = 1 - a_, 1 - b_
+            P_ = v[0] + a_ * (v[1] - v[0]) + b_ * (v[2] - v[0])
+            n = np.cross(v[1] - v[0], v[2] - v[0])
+            nn = np.linalg.norm(n)
+            if nn == 0:
+                continue
+            nh = n / nn
+            wv = rng.normal(size=3)
+            wv -= wv.dot(nh) * nh
+            wv /= np.linalg.norm(wv)
+            sn = rng.uniform(0.05, 3.0) * 1.19e-7 / nn if rng.random() < 1 / 3 else rng.uniform(0.0, 1.0)
+            sn = min(sn, 1.0)
+            dd = wv * np.sqrt(1 - sn * sn) + nh * sn * (1 if rng.random() < 0.5 else -1)
+            o = (P_ - rng.uniform(0.05, 10.0) * dd).astype(f32)
+            d = dd.astype(f32)
+            dsq = float(_dot(d, d))
+            if not (1 - 2.0**-18 + 2.0**-22 <= dsq <= 1 + 2.0**-18 - 2.0**-22):
+                continue
+            # tau_lo as the kernel computes it (float32)
+            s_ = np.where(d < 0, hi_b, lo_b).astype(f32)
+            t = ((s_ - o).astype(f32) * d).astype(f32)
+            tm = f32(f32(t[0] + t[1]) + t[2])
+            sl = f32(f32(abs(t[0]) + abs(t[1])) + abs(t[2]))
+            lo = f32(tm - f32(sl * f32(2.0**-20)))
+            if lo <= 0:
+                continue
+            thr = (A * float(lo)) * (1 - 2.0**-20) / (1 + 2.0**-20) - B
+            checked += 1
+            for tj in range(t0, t1):
+                h = _ray_tri(tv[tj][0], tv[tj][1], tv[tj][2], o, d)
+                if h is not None:
+                    hits += 1
+                    assert float(h[2]) >= thr, (qi, k, tj, float(h[2]), thr)
+    assert checked > 1000 and hits > 300
