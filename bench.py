@@ -223,7 +223,7 @@ def dropin_bench(scene_path: str, iters: int = 50, warmup: int = 3) -> dict:
             "ms_per_call": ms.value / iters, "segments": seg.value, "flag_syncs": syncs.value,
             "definition": f"{iters} calls of the C++ mirror's pathtrace(nullptr, 0, it) on the same scene (one "
                           "iteration each: per-call pt_set_flags, pt_render_pass, synchronous 7.7 MB image copy "
-                          "to the host, as pathtrace.cu:438-524), after {warmup} warm-up calls; segments / wall time"}
+                          f"to the host, as pathtrace.cu:438-524), after {warmup} warm-up calls; segments / wall time"}
 
 
 def _pmc_leg(args, scene_path, spp_pass, sorted_, avg_ms, kernel_prefix, seg_per_launch, busy_ms, launches,
