@@ -2625,6 +2625,9 @@ void k_sort_produce(const KArgs A, const SortArgs SA) {
 // the tile sums (one workgroup), rescan.  No workgroup waits on another, so unlike the library's
 // single-pass scan (whose static schedule needs its whole grid co-resident) two of these can run
 // side by side.  The histogram is small (nmats x paths / 64 ints) and cache-resident.
+#ifndef PT_HIST_APPLY
+#define PT_HIST_APPLY 2   // the work list: 1 runs written one at a time per wave; 2 lane-parallel (k_hist_apply2)
+#endif
 constexpr int kHistPer = 4;                        // ints per thread (one 16-byte load)
 constexpr int kHistTile = kBlock * kHistPer;       // 1024: 4x the workgroups of 4096 (latency-bound scan)
 
@@ -2784,6 +2787,106 @@ __global__ __launch_bounds__(kBlock) void k_hist_apply(const int32_t* __restrict
         hist_store(out, n, base, run, x);
         hist_store(out2, n, base, run2, y);
         wave_sync();   // (this wave's s_dm rows are rewritten by the next block)
+    }
+}
+
+// k_hist_apply, lane-parallel form (PT_HIST_APPLY=2): the same outputs.  A block's entries write one
+// contiguous range of work positions (their exclusive scan), so instead of walking the runs one at a
+// time per wave, every thread takes work positions w = tid, tid + 256, ... of the block's range,
+// finds its entry by a binary search over the entries' starts (LDS) and its slot in the run (the
+// w-th path that goes on: the run's dead bits skipped by a popcount select), and the block writes
+// perm / fpos in coalesced 256-position strides.
+__device__ __forceinline__ int select_bit(uint32_t m, int i) {   // position of the i-th set bit of m
+    int pos = 0;
+#pragma unroll
+    for (int w = 16; w >= 1; w >>= 1) {
+        const uint32_t lo = m & ((1u << w) - 1u);
+        const int c = __popc(lo);
+        if (i >= c) { i -= c; m >>= w; pos += w; } else { m = lo; }
+    }
+    return pos;
+}
+__global__ __launch_bounds__(kBlock) void k_hist_apply2(const int32_t* __restrict__ in, int32_t* __restrict__ out,
+                                                        const int32_t* __restrict__ in2, int32_t* __restrict__ out2,
+                                                        int64_t n, const uint32_t* nlive, const uint32_t* __restrict__ sums,
+                                                        const int32_t* __restrict__ hslot, int32_t* __restrict__ perm,
+                                                        int32_t* __restrict__ fpos, const uint32_t* __restrict__ dead) {
+    __shared__ uint32_t s_w[4], s_w2[4];
+    __shared__ uint32_t s_start[kHistTile + 1];   // entry j's first work position, block-local (+ end)
+    __shared__ uint32_t s_o[kHistTile];           // entry j's sorted position (out)
+    __shared__ int32_t s_slot[kHistTile];         // entry j's first slot (hslot); -1: no path went on
+    __shared__ uint32_t s_x[kHistTile];           // entry j's survivors (x): == its count that went on when no path ended
+    n = hist_n(n, nlive);
+    const int tid = (int)threadIdx.x;
+    for (int64_t blk = blockIdx.x; blk * kHistTile < n; blk += gridDim.x) {   // (as k_hist_sums)
+        const int64_t base = blk * kHistTile + (int64_t)tid * kHistPer;
+        uint32_t x[kHistPer], y[kHistPer], v = 0, v2 = 0;
+        hist_load(in, n, base, x);
+        hist_load(in2, n, base, y);
+#pragma unroll
+        for (int k = 0; k < kHistPer; ++k) {
+            if (!(base + k < n - 1)) y[k] = 0u;   // (the end offset's entry: no run)
+            v += x[k];
+            v2 += y[k];
+        }
+        uint32_t total, total2;
+        const uint32_t run = block_excl_scan(v, s_w, &total) + sums[2 * blk];
+        const uint32_t lrun2 = block_excl_scan(v2, s_w2, &total2);   // block-local work positions
+        const uint32_t B2 = sums[2 * blk + 1];
+        {
+            uint32_t o = run, o2 = lrun2;
+#pragma unroll
+            for (int k = 0; k < kHistPer; ++k) {
+                const int j = tid * kHistPer + k;
+                s_start[j] = o2;
+                s_o[j] = o;
+                s_x[j] = x[k];
+                s_slot[j] = y[k] != 0u ? hslot[base + k] : -1;
+                o += x[k];
+                o2 += y[k];
+            }
+            if (tid == kBlock - 1) s_start[kHistTile] = o2;
+        }
+        // the scans themselves (out: every survivor's sorted position base; out2: work positions),
+        // from the ORIGINAL counts (the end offset entry included, as k_hist_apply writes them)
+        {
+            uint32_t xs[kHistPer], ys[kHistPer];
+            hist_load(in2, n, base, ys);
+#pragma unroll
+            for (int k = 0; k < kHistPer; ++k) xs[k] = x[k];
+            hist_store(out, n, base, run, xs);
+            hist_store(out2, n, base, lrun2 + B2, ys);
+        }
+        __syncthreads();
+        int e = 0;
+        for (uint32_t w = (uint32_t)tid; w < total2; w += kBlock) {
+            int lo = e, hi = kHistTile - 1;   // the last entry whose start <= w (starts never decrease)
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (s_start[mid] <= w) lo = mid; else hi = mid - 1;
+            }
+            e = lo;
+            const uint32_t i = w - s_start[e];
+            const int32_t rs = s_slot[e];
+            const uint32_t xe = s_x[e], ye = s_start[e + 1] - s_start[e];
+            uint32_t r = i;
+            if (ye != xe) {   // some paths of the run ended in the producer: the i-th that did not
+                const uint32_t* dm = dead + (size_t)((uint32_t)rs >> 8) * (kBlock / 32);
+                const uint32_t b0 = (uint32_t)rs & (kBlock - 1u), b1 = b0 + xe;   // the run's bits [b0, b1)
+                uint32_t left = i;
+                for (uint32_t wd = b0 >> 5; wd <= ((b1 - 1u) >> 5); ++wd) {
+                    uint32_t m = ~dm[wd];
+                    if (wd == (b0 >> 5)) m &= ~0u << (b0 & 31u);
+                    if (wd == ((b1 - 1u) >> 5) && (b1 & 31u)) m &= (1u << (b1 & 31u)) - 1u;
+                    const uint32_t c = (uint32_t)__popc(m);
+                    if (left < c) { r = wd * 32u + (uint32_t)select_bit(m, (int)left) - b0; break; }
+                    left -= c;
+                }
+            }
+            perm[B2 + w] = rs + (int32_t)r;
+            fpos[B2 + w] = (int32_t)(s_o[e] + r);
+        }
+        __syncthreads();   // (the LDS rows are rewritten by the next block)
     }
 }
 
@@ -4165,9 +4268,9 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
         hipLaunchKernelGGL(k_hist_sums, dim3(hgrid), dim3(kBlock), 0, s, (const int32_t*)ss.hist, (const int32_t*)ss.hist2,
                            ss.hist_cap, nlive, ss.sums);
         hipLaunchKernelGGL(k_hist_scan_sums, dim3(1), dim3(kBlock), 0, s, ss.sums, ss.hist_cap, nlive);
-        hipLaunchKernelGGL(k_hist_apply, dim3(hgrid), dim3(kBlock), 0, s, (const int32_t*)ss.hist, ss.offs,
-                           (const int32_t*)ss.hist2, ss.offs2, ss.hist_cap, nlive, (const uint32_t*)ss.sums,
-                           (const int32_t*)ss.hslot, ss.perm, ss.fpos, (const uint32_t*)ss.dead);
+        hipLaunchKernelGGL(PT_HIST_APPLY == 2 ? k_hist_apply2 : k_hist_apply, dim3(hgrid), dim3(kBlock), 0, s,
+                           (const int32_t*)ss.hist, ss.offs, (const int32_t*)ss.hist2, ss.offs2, ss.hist_cap, nlive,
+                           (const uint32_t*)ss.sums, (const int32_t*)ss.hslot, ss.perm, ss.fpos, (const uint32_t*)ss.dead);
         HIP_TRY(hipGetLastError());
         if (int rc = produce(false)) return rc;
         return prof_end(ev, s);
