@@ -2626,7 +2626,7 @@ void k_sort_produce(const KArgs A, const SortArgs SA) {
 // single-pass scan (whose static schedule needs its whole grid co-resident) two of these can run
 // side by side.  The histogram is small (nmats x paths / 64 ints) and cache-resident.
 #ifndef PT_HIST_APPLY
-#define PT_HIST_APPLY 2   // the work list: 1 runs written one at a time per wave; 2 lane-parallel (k_hist_apply2)
+#define PT_HIST_APPLY 1   // the work list: 1 runs written one at a time per wave; 2 lane-parallel (k_hist_apply2)
 #endif
 constexpr int kHistPer = 4;                        // ints per thread (one 16-byte load)
 constexpr int kHistTile = kBlock * kHistPer;       // 1024: 4x the workgroups of 4096 (latency-bound scan)
