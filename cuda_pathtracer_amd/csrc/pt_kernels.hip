@@ -2471,8 +2471,8 @@ void k_sort_produce(const KArgs A, const SortArgs SA) {
         Hit h;
         bool ends = false;
         if (idx < s_sb[it + 1]) {
-            if (FIRST) {
-                raygen(A.cam, A.fl, A.tile, idx, p);
+            if (FIRST) {   // (work position idx = iteration it's pixel idx - it * npix: a tile holds one iteration)
+                raygen_at(A.cam, A.fl, A.tile, idx, it, idx - it_base, p);
                 alive = true;
             } else {
                 const int j = SA.perm[idx];
