@@ -175,3 +175,34 @@ def test_tcull_margins_only_skip_worse_hits(tmp_path, scene):
                     hits += 1
                     assert float(h[2]) >= thr, (qi, k, tj, float(h[2]), thr)
     assert checked > 1000 and hits > 300
+
+
+def test_tcull_words_follow_the_triangle_sizes(tmp_path):
+    """build_qcull's words: binary16 A in [0, 1) and B >= 0 per valid slot; A is positive exactly
+    where c = 9 max|e1||e2| (the subtree's largest triangle) stays below 1, and slots holding config
+    5's largest triangles (|e1||e2| up to 0.62) get A = 0, B = inf — never culled."""
+    path = scenes.tessellated_meshes(tmp_path / "t", res=(64, 36))
+    _, frac, w, q, tv = _tcull_tables(path)
+    A = (w & 0xffff).astype(np.uint16).view(np.float16).astype(np.float64)
+    B = (w >> 16).astype(np.uint16).view(np.float16).astype(np.float64)
+    valid = np.array([[(int(q["meta"][i, 0]) >> k) & 1 for k in range(4)] for i in range(len(q))], bool)
+    assert frac == 1.0 and (A[valid] > 0.9).all() and (A[valid] < 1).all() and (B[valid] >= 0).all()
+    path5 = scenes.random_triangles(tmp_path / "c", n=100_000, res=(64, 36), depth=32)
+    _, frac5, w5, q5, tv5 = _tcull_tables(path5)
+    A5 = (w5 & 0xffff).astype(np.uint16).view(np.float16).astype(np.float64)
+    B5 = (w5 >> 16).astype(np.uint16).view(np.float16).astype(np.float64)
+    e1 = np.linalg.norm((tv5[:, 1] - tv5[:, 0]).astype(np.float64), axis=1)
+    e2 = np.linalg.norm((tv5[:, 2] - tv5[:, 0]).astype(np.float64), axis=1)
+    big = int(np.argmax(e1 * e2))
+    assert e1[big] * e2[big] > 0.6 and frac5 < 0.25
+    # the leaf slot holding the largest triangle: no margin
+    found = 0
+    for i in range(len(q5)):
+        for k in range(4):
+            c = int(q5["code"][i, k])
+            if (int(q5["meta"][i, 0]) >> k) & 1 and c < 0:
+                t0, t1 = _leaf_range(c)
+                if t0 <= big < t1:
+                    assert A5[i, k] == 0 and np.isinf(B5[i, k])
+                    found += 1
+    assert found == 1
