@@ -133,3 +133,29 @@ def test_naive_argument_checks(gpu_device):
         P.naive_scan_device(d, t, t)          # tmp aliases out
     assert lib().sc_naive_scan_i32(None, None, 0, None, None) == 0
     assert lib().sc_thrust_scan_i32(None, None, 0, None) == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("off_in,off_out,off_tmp", [(1, 0, 0), (0, 3, 0), (0, 0, 2), (1, 1, 1)])
+def test_naive_unaligned_views(gpu_device, off_in, off_out, off_tmp):
+    """sc_naive_scan_i32 on torch views with a storage offset (4-byte aligned only): the 16-byte
+    vector path is taken only when every base is 16-byte aligned, the scalar path otherwise (ADVICE
+    r03); results equal the oracle.  Too-short output or scratch tensors are refused."""
+    import torch
+    n = 4099
+    rng = np.random.default_rng(off_in * 7 + off_out * 3 + off_tmp)
+    a = rng.integers(-1000, 1000, size=n, dtype=np.int64).astype(np.int32)
+    big_in = torch.zeros(n + 8, dtype=torch.int32, device=gpu_device)
+    big_in[off_in:off_in + n] = torch.from_numpy(a).to(gpu_device)
+    d_in = big_in[off_in:off_in + n]
+    d_out = torch.zeros(n + 8, dtype=torch.int32, device=gpu_device)[off_out:off_out + n]
+    d_tmp = torch.zeros(n + 8, dtype=torch.int32, device=gpu_device)[off_tmp:off_tmp + n]
+    P.naive_scan_device(d_in, d_out, d_tmp)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(d_out.cpu().numpy(), O.scan(a))
+    with pytest.raises(ValueError):
+        P.naive_scan_device(d_in, d_out[:-1], d_tmp)
+    with pytest.raises(ValueError):
+        P.naive_scan_device(d_in, d_out, d_tmp[:-1])
+    with pytest.raises(ValueError):
+        P.thrust_scan_device(d_in, d_out[:-1])
