@@ -2397,7 +2397,10 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_w, u
 #ifndef PT_PRODUCE_WAVES_FIRST
 #define PT_PRODUCE_WAVES_FIRST PT_PRODUCE_WAVES
 #endif
-template <bool FIRST, bool SPP1, bool MESH>
+// VERIFY: the PT_AMD_VERIFY_BOUNDS=1 build of the producer (the plain-loop re-run of every closest
+// hit compiled in); the default one carries no diagnostic code (round 4: the later producer's 8-byte
+// register spill went away with it).
+template <bool FIRST, bool SPP1, bool MESH, bool VERIFY>
 __global__ __launch_bounds__(kBlock, MESH ? 1 : (FIRST ? PT_PRODUCE_WAVES_FIRST : PT_PRODUCE_WAVES))
 void k_sort_produce(const KArgs A, const SortArgs SA) {
     __shared__ DMaterial s_mats[kLdsMats];
@@ -2529,7 +2532,7 @@ void k_sort_produce(const KArgs A, const SortArgs SA) {
                 gm = A.cmask[lp0 >> 6];
             }
             if (alive) {
-                h = closest_hit<MESH, true, !FIRST>(A.S, A.fl, s_geoms, p.o, p.d, &A.stats->bound_mismatch, gm);
+                h = closest_hit<MESH, VERIFY, !FIRST>(A.S, A.fl, s_geoms, p.o, p.d, &A.stats->bound_mismatch, gm);
                 PathReg e = p;   // (only the verdict here; the colour below)
                 ends = lds_mats ? shade_ends(h, s_mats, e) : shade_ends(h, A.S.mats, e);
             }
@@ -3467,12 +3470,17 @@ KernelFn trace_kernel(bool first, bool spp1, bool mesh) {
 }
 
 using SortKernelFn = void (*)(const KArgs, const SortArgs);
-SortKernelFn produce_kernel(bool first, bool spp1, bool mesh) {
-    static const SortKernelFn table[8] = {
-        k_sort_produce<false, false, false>, k_sort_produce<false, false, true>, k_sort_produce<false, true, false>,
-        k_sort_produce<false, true, true>,   k_sort_produce<true, false, false>, k_sort_produce<true, false, true>,
-        k_sort_produce<true, true, false>,   k_sort_produce<true, true, true>};
-    return table[(first ? 4 : 0) + (spp1 ? 2 : 0) + (mesh ? 1 : 0)];
+SortKernelFn produce_kernel(bool first, bool spp1, bool mesh, bool verify) {
+    static const SortKernelFn table[16] = {
+        k_sort_produce<false, false, false, false>, k_sort_produce<false, false, true, false>,
+        k_sort_produce<false, true, false, false>,  k_sort_produce<false, true, true, false>,
+        k_sort_produce<true, false, false, false>,  k_sort_produce<true, false, true, false>,
+        k_sort_produce<true, true, false, false>,   k_sort_produce<true, true, true, false>,
+        k_sort_produce<false, false, false, true>,  k_sort_produce<false, false, true, true>,
+        k_sort_produce<false, true, false, true>,   k_sort_produce<false, true, true, true>,
+        k_sort_produce<true, false, false, true>,   k_sort_produce<true, false, true, true>,
+        k_sort_produce<true, true, false, true>,    k_sort_produce<true, true, true, true>};
+    return table[(verify ? 8 : 0) + (first ? 4 : 0) + (spp1 ? 2 : 0) + (mesh ? 1 : 0)];
 }
 
 template <typename K>
@@ -4248,7 +4256,11 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
             a.out = bufs[lcur ^ 1];
             a.hit.uv = ss.uv[lcur];
             const SortArgs sa{ss.hslot, ss.hist, ss.offs, ss.hist2, ss.offs2, ss.perm, ss.fpos, ss.itb, ss.uv[lcur ^ 1], ss.dead};
-            hipLaunchKernelGGL(produce_kernel(first, spp1, mesh), dim3(c->grid_bounce[0]), dim3(kBlock),
+#ifndef PT_PRODUCER_ALWAYS_VERIFY
+#define PT_PRODUCER_ALWAYS_VERIFY 0   // (A/B knob: the diagnostic producer build for every run, round 3's form)
+#endif
+            hipLaunchKernelGGL(produce_kernel(first, spp1, mesh, a.fl.verify != 0 || PT_PRODUCER_ALWAYS_VERIFY),
+                               dim3(c->grid_bounce[0]), dim3(kBlock),
                                (size_t)16 * c->nmats * sizeof(uint32_t), s, a, sa);
             HIP_TRY(hipGetLastError());
             ++lc;
