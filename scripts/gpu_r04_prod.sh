@@ -1,0 +1,11 @@
+# Round 4: the sorted producer without its diagnostic code — sorted-pipeline parity (incl. the
+# VERIFY instantiation's camera-mask check), then config 3 A/B vs the always-diagnostic variant av.
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$R"; O=gpurun_out/prod; mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests/test_render_gpu.py -m gpu -x -q -p no:cacheprovider --timeout 600 \
+    --timeout-method thread -k "sort or Sort or config3 or ends or verified or many_materials or histogram" \
+    > $O/pytest.log 2>&1; rc=$?
+echo "pytest rc=$rc"; tail -3 $O/pytest.log
+[ $rc -eq 0 ] || exit 1
+VARIANTS="av" RUNS=3 STEPS=10 BENCH_ARGS="--config cornell_hd_sorted" bash scripts/gpu_ab_variants.sh || exit 1
