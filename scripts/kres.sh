@@ -1,6 +1,6 @@
 # Per-kernel VGPR / SGPR / occupancy of a HIP source (compile-time resource report).
 f=${1:?source}; shift
-hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -I "$(dirname "$0")/../include" "$@" -c "$f" -o /tmp/kres.o \
+hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-slp-vectorize -I "$(dirname "$0")/../include" "$@" -c "$f" -o /tmp/kres.o \
   -Rpass-analysis=kernel-resource-usage 2>&1 | python3 -c '
 import re,sys
 cur=None
