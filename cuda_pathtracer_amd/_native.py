@@ -125,6 +125,8 @@ SIGNATURES = {
     "pt_scene_counts": (_I, [_P, _IP, _IP, _IP, _IP, _IP]),
     "pt_scene_get_camera": (_I, [_P, C.POINTER(Camera)]),
     "pt_scene_get_render": (_I, [_P, _IP, _IP, C.c_char_p, _I]),
+    "pt_scene_get_orbit": (_I, [_P, _FP, _FP, _FP]),
+    "pt_scene_set_orbit": (_I, [_P, _F, _F, _F, _FP]),
     "pt_scene_get_geoms": (_I, [_P, C.POINTER(Geom), _I]),
     "pt_scene_get_materials": (_I, [_P, C.POINTER(Material), _I]),
     "pt_scene_get_triangles": (_I, [_P, C.POINTER(Triangle), _I]),

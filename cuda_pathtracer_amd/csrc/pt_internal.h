@@ -27,6 +27,7 @@ struct Scene {
     pt_camera camera{};
     float fovy = 45.0f;
     float eye[3] = {0, 0, 0}, look_at[3] = {0, 0, 0}, up[3] = {0, 1, 0};
+    float orbit[3] = {0, 0, 0};   // phi, theta, zoom of the loaded camera (main.cpp:59-73), set by finalize
     int32_t iterations = 1, depth = 8;
     std::string file = "render";
     bool camera_set = false;

@@ -192,6 +192,26 @@ void read3(const jl::Value& a, float* out) {
 }  // namespace
 
 // ---- camera (scene.cpp:185-211 + main.cpp:59-73 + main.cpp:117-136) ----------------------
+// runCuda's camchanged block (main.cpp:117-136): the position on the orbit (zoom, phi, theta) about
+// look_at, view towards it, right = view x (0,1,0) (not normalised), up = right x view.
+static void apply_orbit(Scene& S, float phi, float theta, float zoom, const float* la_in) {
+    pt_camera& cam = S.camera;
+    const V la{la_in[0], la_in[1], la_in[2]};
+    const V cp{(zoom * sinf(phi)) * sinf(theta), zoom * cosf(theta), (zoom * cosf(phi)) * sinf(theta)};
+    const V nv = normv(cp);
+    const V v{-nv.x, -nv.y, -nv.z};
+    const V r = crossv(v, V{0, 1, 0});
+    const V u = crossv(r, v);
+    const float p[3] = {cp.x + la.x, cp.y + la.y, cp.z + la.z};
+    for (int i = 0; i < 3; ++i) {
+        cam.position[i] = p[i];
+        cam.look_at[i] = la_in[i];
+    }
+    cam.view[0] = v.x; cam.view[1] = v.y; cam.view[2] = v.z;
+    cam.up[0] = u.x; cam.up[1] = u.y; cam.up[2] = u.z;
+    cam.right[0] = r.x; cam.right[1] = r.y; cam.right[2] = r.z;
+}
+
 static void finalize_camera(Scene& S) {
     pt_camera& cam = S.camera;
     const V pos{S.eye[0], S.eye[1], S.eye[2]}, la{S.look_at[0], S.look_at[1], S.look_at[2]};
@@ -203,24 +223,16 @@ static void finalize_camera(Scene& S) {
     cam.fov[1] = fovy;
     cam.pixel_length[0] = 2 * xscaled / (float)cam.res[0];
     cam.pixel_length[1] = 2 * yscaled / (float)cam.res[1];
+    // main.cpp:59-73: the orbit angles of the loaded view and its distance to the look-at point
     const V view = normv(sub(la, pos));
     const V vxz{view.x, 0.0f, view.z}, vzy{0.0f, view.y, view.z};
     const float phi = acosf(dotv(normv(vxz), V{0, 0, -1}));
     const float theta = acosf(dotv(normv(vzy), V{0, 1, 0}));
     const float zoom = sqrtf(dotv(sub(pos, la), sub(pos, la)));
-    const V cp{(zoom * sinf(phi)) * sinf(theta), zoom * cosf(theta), (zoom * cosf(phi)) * sinf(theta)};
-    const V nv = normv(cp);
-    const V v{-nv.x, -nv.y, -nv.z};
-    const V r = crossv(v, V{0, 1, 0});
-    const V u = crossv(r, v);
-    const float p[3] = {cp.x + la.x, cp.y + la.y, cp.z + la.z};
-    for (int i = 0; i < 3; ++i) {
-        cam.position[i] = p[i];
-        cam.look_at[i] = S.look_at[i];
-    }
-    cam.view[0] = v.x; cam.view[1] = v.y; cam.view[2] = v.z;
-    cam.up[0] = u.x; cam.up[1] = u.y; cam.up[2] = u.z;
-    cam.right[0] = r.x; cam.right[1] = r.y; cam.right[2] = r.z;
+    S.orbit[0] = phi;
+    S.orbit[1] = theta;
+    S.orbit[2] = zoom;
+    apply_orbit(S, phi, theta, zoom, S.look_at);   // the first frame (camchanged starts true)
 }
 
 int scene_add_geom(Scene& S, int32_t type, int32_t mat, const float* t, const float* r, const float* s) {
@@ -518,6 +530,24 @@ int pt_scene_counts(const pt_scene* s, int32_t* ng, int32_t* nm, int32_t* nt, in
 int pt_scene_get_camera(const pt_scene* s, pt_camera* out) {
     if (!s || !out) return fail(PT_ERR_ARG, "null argument");
     *out = reinterpret_cast<const pt::Scene*>(s)->camera;
+    return PT_OK;
+}
+
+int pt_scene_get_orbit(const pt_scene* s, float* phi, float* theta, float* zoom) {
+    if (!s) return fail(PT_ERR_ARG, "null scene");
+    const auto& S = *reinterpret_cast<const pt::Scene*>(s);
+    if (!S.finalized) return fail(PT_ERR_ARG, "scene not finalized (pt_scene_finalize)");
+    if (phi) *phi = S.orbit[0];
+    if (theta) *theta = S.orbit[1];
+    if (zoom) *zoom = S.orbit[2];
+    return PT_OK;
+}
+
+int pt_scene_set_orbit(pt_scene* s, float phi, float theta, float zoom, const float* look_at) {
+    if (!s || !look_at) return fail(PT_ERR_ARG, "null argument");
+    auto& S = *reinterpret_cast<pt::Scene*>(s);
+    if (!S.finalized) return fail(PT_ERR_ARG, "scene not finalized (pt_scene_finalize)");
+    pt::apply_orbit(S, phi, theta, zoom, look_at);   // geometry unchanged: the scene stays finalized
     return PT_OK;
 }
 

@@ -200,6 +200,17 @@ class Scene:
         check_pt(lib().pt_scene_get_camera(self._h, C.byref(cam)))
         return cam
 
+    def orbit(self) -> tuple[float, float, float]:
+        """(phi, theta, zoom) of the loaded camera, as main.cpp:59-73 derives them."""
+        p, t, z = C.c_float(), C.c_float(), C.c_float()
+        check_pt(lib().pt_scene_get_orbit(self._h, C.byref(p), C.byref(t), C.byref(z)))
+        return p.value, t.value, z.value
+
+    def set_orbit(self, phi: float, theta: float, zoom: float, look_at) -> None:
+        """runCuda's camera recompute (main.cpp:117-136) for an orbit about look_at; contexts created
+        afterwards render it."""
+        check_pt(lib().pt_scene_set_orbit(self._h, float(phi), float(theta), float(zoom), N.f3(look_at)))
+
     def state(self) -> RenderState:
         it, d = C.c_int32(), C.c_int32()
         buf = C.create_string_buffer(1024)

@@ -206,6 +206,14 @@ int pt_scene_counts(const pt_scene* s, int32_t* ngeoms, int32_t* nmats, int32_t*
                     int32_t* nnodes, int32_t* ntex);
 int pt_scene_get_camera(const pt_scene* s, pt_camera* out);
 int pt_scene_get_render(const pt_scene* s, int32_t* iterations, int32_t* depth, char* file, int32_t cap);
+/* The interactive camera of the preview (main.cpp).  pt_scene_get_orbit: the orbit of the loaded
+ * camera, phi / theta / zoom as main.cpp:59-73 derives them (pt_scene_finalize computes them).
+ * pt_scene_set_orbit: runCuda's camchanged recompute (main.cpp:117-136) for the orbit (phi, theta,
+ * zoom) about look_at — position, view, right (= view x (0,1,0), unnormalised) and up; the scene stays
+ * finalized, and contexts created after the call render the new camera (the reference re-runs
+ * pathtraceInit at iteration 0).  Both need a finalized scene (PT_ERR_ARG otherwise). */
+int pt_scene_get_orbit(const pt_scene* s, float* phi, float* theta, float* zoom);
+int pt_scene_set_orbit(pt_scene* s, float phi, float theta, float zoom, const float look_at[3]);
 /* Getters copy min(count, cap) records and return that number (>= 0), or -PT_ERR_ARG. */
 int pt_scene_get_geoms(const pt_scene* s, pt_geom* out, int32_t cap);
 int pt_scene_get_materials(const pt_scene* s, pt_material* out, int32_t cap);
