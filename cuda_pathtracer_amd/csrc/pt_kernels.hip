@@ -812,6 +812,7 @@ __device__ __forceinline__ Hit intersect_bounded(const SceneDev& S, const FlagsD
                 atomicAdd(&g_stamps[12], m3 ? 1ull : 0ull);
                 atomicAdd(&g_stamps[13], (ms && ms != mg) ? 1ull : 0ull);
                 atomicAdd(&g_stamps[14], (unsigned long long)__popcll(mg));
+                atomicAdd(&g_stamps[15], (unsigned long long)__popc(gmask & ng_all_mask(S.ngeoms)));   // bounded geoms
             }
         }
 #endif
@@ -2377,6 +2378,19 @@ __device__ __forceinline__ int tile_iteration(const int32_t* s_tb, int spp, int 
     }
     return lo;
 }
+// The same for a workgroup's increasing tiles t (uniform): from the previous tile's iteration `it`,
+// one LDS read when t is still in it (the common case), else a scalar binary search above it.  The
+// result and every read are wave-uniform (readfirstlane), so the tile's iteration, its bases and the
+// RNG's iteration hash stay on the SALU.
+__device__ __forceinline__ int tile_iteration_next(const int32_t* s_tb, int spp, int t, int it) {
+    if (it + 1 >= spp || __builtin_amdgcn_readfirstlane(s_tb[it + 1]) > t) return it;
+    int lo = it + 1, hi = spp - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (__builtin_amdgcn_readfirstlane(s_tb[mid]) <= t) lo = mid; else hi = mid - 1;
+    }
+    return __builtin_amdgcn_readfirstlane(lo);
+}
 
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_w, uint32_t* total) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -2462,18 +2476,19 @@ void k_sort_produce(const KArgs A, const SortArgs SA) {
     const bool lds_geoms = !MESH && A.S.ngeoms <= kLdsGeoms;   // (stage_geoms / stage_frames ran)
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     uint32_t emit_cnt = 0, emit_next = 0;
-    int k = 0;
+    int k = 0, it = 0;
     for (int t = (int)blockIdx.x; t < T; t += (int)gridDim.x, ++k) {
-        const int it = tile_iteration(s_tb, spp, t);
-        const int t0 = s_tb[it], t1 = s_tb[it + 1];
-        const int it_base = s_sb[it];
+        it = tile_iteration_next(s_tb, spp, t, it);
+        const int t0 = __builtin_amdgcn_readfirstlane(s_tb[it]), t1 = __builtin_amdgcn_readfirstlane(s_tb[it + 1]);
+        const int it_base = __builtin_amdgcn_readfirstlane(s_sb[it]);
+        const int it_end = __builtin_amdgcn_readfirstlane(s_sb[it + 1]);
         const int idx = it_base + (t - t0) * kBlock + tid;   // work position
         const int iter = A.tile.iter_first + it;
         bool alive = false, emitted = false;
         PathReg p;
         Hit h;
         bool ends = false;
-        if (idx < s_sb[it + 1]) {
+        if (idx < it_end) {
             if (FIRST) {   // (work position idx = iteration it's pixel idx - it * npix: a tile holds one iteration)
                 raygen_at(A.cam, A.fl, A.tile, idx, it, idx - it_base, p);
                 alive = true;
@@ -2517,7 +2532,7 @@ void k_sort_produce(const KArgs A, const SortArgs SA) {
                 }
                 // key: sorted index within the path's own iteration (paths that ended in the
                 // previous launch hold positions too: fpos)
-                const int key = A.fl.rng_pixel ? slot_pixel(A.cam, A.tile, p.slot) : SA.fpos[idx] - s_fb[it];
+                const int key = A.fl.rng_pixel ? slot_pixel(A.cam, A.tile, p.slot) : SA.fpos[idx] - __builtin_amdgcn_readfirstlane(s_fb[it]);
                 const float* frames = lds_geoms ? s_frm : nullptr;
                 alive = lds_mats ? shade_from(A.S, A.fl, A.tile.depth, iter, key, p, h, hitp, s_mats, frames)
                                  : shade_from(A.S, A.fl, A.tile.depth, iter, key, p, h, hitp, A.S.mats, frames);
