@@ -2363,6 +2363,23 @@ struct SortArgs {
     float* uv_out;      // textured scenes: (u, v) of the output records ([2 * cap])
     uint32_t* dead;     // one bit per output slot: the path ended in this launch (no record; 8 words per tile)
 };
+// The next producer's work list: per work position, the slot it gathers and its sorted position.
+// PT_PF_PACKED (default): one (slot, position) pair per work position in `perm` (8 bytes: one store
+// and one load per path instead of two each); 0: the separate arrays perm / fpos.
+#ifndef PT_PF_PACKED
+#define PT_PF_PACKED 1
+#endif
+typedef int v2i_pf __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void pf_store(int32_t* perm, int32_t* fpos, uint32_t w, int32_t slot, int32_t pos) {
+#if PT_PF_PACKED
+    (void)fpos;
+    reinterpret_cast<v2i_pf*>(perm)[w] = v2i_pf{slot, pos};
+#else
+    perm[w] = slot;
+    fpos[w] = pos;
+#endif
+}
+
 constexpr int kSortMaxMats = 256;  // per-tile material counts in LDS (one thread per material)
 
 // Histogram entry of tile t (iteration tiles [t0, t1)) for material m: [iteration block][material][tile].
@@ -2493,7 +2510,12 @@ void k_sort_produce(const KArgs A, const SortArgs SA) {
                 raygen_at(A.cam, A.fl, A.tile, idx, it, idx - it_base, p);
                 alive = true;
             } else {
-                const int j = SA.perm[idx];
+#if PT_PF_PACKED
+                const v2i_pf pf = reinterpret_cast<const v2i_pf*>(SA.perm)[idx];
+                const int j = pf[0], fp = pf[1];
+#else
+                const int j = SA.perm[idx], fp = 0;
+#endif
                 const v4f* r = srec(A.in, j);
                 // (plain loads: a gather of 32-byte records)
                 const v4f r0 = r[0], r1 = r[1];
@@ -2532,7 +2554,7 @@ void k_sort_produce(const KArgs A, const SortArgs SA) {
                 }
                 // key: sorted index within the path's own iteration (paths that ended in the
                 // previous launch hold positions too: fpos)
-                const int key = A.fl.rng_pixel ? slot_pixel(A.cam, A.tile, p.slot) : SA.fpos[idx] - __builtin_amdgcn_readfirstlane(s_fb[it]);
+                const int key = A.fl.rng_pixel ? slot_pixel(A.cam, A.tile, p.slot) : (PT_PF_PACKED ? fp : SA.fpos[idx]) - __builtin_amdgcn_readfirstlane(s_fb[it]);
                 const float* frames = lds_geoms ? s_frm : nullptr;
                 alive = lds_mats ? shade_from(A.S, A.fl, A.tile.depth, iter, key, p, h, hitp, s_mats, frames)
                                  : shade_from(A.S, A.fl, A.tile.depth, iter, key, p, h, hitp, A.S.mats, frames);
@@ -2779,8 +2801,7 @@ __global__ __launch_bounds__(kBlock) void k_hist_apply(const int32_t* __restrict
                 const uint32_t rs = (uint32_t)__builtin_amdgcn_readlane(s0[k], src);
                 if (rl == rc) {   // no path of the run ended: 64 consecutive positions per store
                     for (uint32_t r = (uint32_t)lane; r < rc; r += 64) {
-                        perm[ro2 + r] = (int32_t)(rs + r);
-                        fpos[ro2 + r] = (int32_t)(ro + r);
+                        pf_store(perm, fpos, ro2 + r, (int32_t)(rs + r), (int32_t)(ro + r));
                     }
                 } else {
                     const uint32_t* dm = s_dm + (((int)threadIdx.x & ~63) + src) * kHistPer * (kBlock / 32) + k * (kBlock / 32);
@@ -2791,8 +2812,7 @@ __global__ __launch_bounds__(kBlock) void k_hist_apply(const int32_t* __restrict
                         const uint64_t km = __ballot(keep);
                         if (keep) {
                             const uint32_t i = i0 + (uint32_t)__popcll(km & lt);
-                            perm[ro2 + i] = (int32_t)(rs + r);
-                            fpos[ro2 + i] = (int32_t)(ro + r);
+                            pf_store(perm, fpos, ro2 + i, (int32_t)(rs + r), (int32_t)(ro + r));
                         }
                         i0 += (uint32_t)__popcll(km);
                     }
@@ -2901,8 +2921,7 @@ __global__ __launch_bounds__(kBlock) void k_hist_apply2(const int32_t* __restric
                     left -= c;
                 }
             }
-            perm[B2 + w] = rs + (int32_t)r;
-            fpos[B2 + w] = (int32_t)(s_o[e] + r);
+            pf_store(perm, fpos, B2 + w, rs + (int32_t)r, (int32_t)(s_o[e] + r));
         }
         __syncthreads();   // (the LDS rows are rewritten by the next block)
     }
@@ -4175,9 +4194,9 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
         ss.hist_cap = (int64_t)((size_t)c->nmats * (cap / kBlock + 1) + 2);
         const size_t tiles = ((size_t)ss.hist_cap + kHistTile - 1) / kHistTile;
         if (int rc = c->alloc(&ss.hslot, (size_t)ss.hist_cap)) return bail(rc);
-        if (int rc = c->alloc(&ss.perm, paths)) return bail(rc);
+        if (int rc = c->alloc(&ss.perm, PT_PF_PACKED ? 2 * paths : paths)) return bail(rc);   // (pf_store)
         if (int rc = c->alloc(&ss.dead, (cap / kBlock + 2) * (kBlock / 32))) return bail(rc);
-        if (int rc = c->alloc(&ss.fpos, paths)) return bail(rc);
+        if (int rc = c->alloc(&ss.fpos, PT_PF_PACKED ? 1 : paths)) return bail(rc);
         if (int rc = c->alloc(&ss.hist2, (size_t)ss.hist_cap)) return bail(rc);
         if (int rc = c->alloc(&ss.offs2, (size_t)ss.hist_cap)) return bail(rc);
         if (int rc = c->alloc(&ss.hist, (size_t)ss.hist_cap)) return bail(rc);

@@ -9,8 +9,9 @@ for v in $VARIANTS; do
   name=${v%%:*}; flags=$(echo ${v#*:} | tr ',' ' ')
   /opt/rocm/bin/hipcc -x hip --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-slp-vectorize $flags -I $R/include \
       -c $R/cuda_pathtracer_amd/csrc/pt_kernels.hip -o $B/pt_kernels_$name.o &
+  pids="$pids $!"
 done
-wait
+for p in $pids; do wait $p || { echo "variant compile failed" >&2; exit 1; }; done
 for v in $VARIANTS; do
   name=${v%%:*}
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $B/libpt_amd_$name.so $B/pt_kernels_$name.o \
