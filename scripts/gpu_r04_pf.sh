@@ -1,5 +1,5 @@
 # Packed work list (slot, sorted position) per work position: sorted-pipeline parity, config 3 A/B
-# against the separate arrays (library "sep"), then a PC-sampling attempt of the Cornell bench.
+# against the separate arrays (library "sep").
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"; O=gpurun_out/pf; mkdir -p $O
@@ -9,4 +9,3 @@ timeout -k 10 900 python -u -m pytest tests/test_render_gpu.py -m gpu -x -q -p n
 echo "pytest rc=$rc"; tail -3 $O/pytest.log
 [ $rc -eq 0 ] || exit 1
 VARIANTS="sep" RUNS=3 STEPS=10 BENCH_ARGS="--config cornell_hd_sorted" bash scripts/gpu_ab_variants.sh || exit 1
-cd "$R" && bash scripts/gpu_pcsample.sh
