@@ -143,6 +143,23 @@ struct Hit {
     float u, v;
     int32_t frame = -1;   // cube hits: geom * 6 + slab code (the precomputed tangent frame, DGeom::frm)
 };
+#ifndef PT_SKIP_MISS_WAVES
+#define PT_SKIP_MISS_WAVES 1   // (A/B knob: the sorted camera-ray producer's waves whose camera mask is empty skip
+                               // raygen + closest hit: config 3 35.6k -> 36.9k, same box)
+#endif
+#ifndef PT_SKIP_MISS_WAVES_FUSED
+#define PT_SKIP_MISS_WAVES_FUSED 0   // (the same in the fused first bounce: 5 more VGPRs there, Cornell -1.1%)
+#endif
+// What the closest hit returns for a ray that meets nothing (intersect_bounded, computeIntersections'
+// t = -1 with materialId 0: pathtrace.cu:466).
+__device__ __forceinline__ Hit miss_hit() {
+    Hit h;
+    h.t = -1.0f;
+    h.mat = 0;
+    h.n = F3(0, 0, 0);
+    h.u = h.v = 0.0f;
+    return h;
+}
 
 // boxIntersectionTest (intersections.cu:3-58).  The world normal is deferred to the closest
 // hit: we keep the slab code (axis*2 + sign, -1 = zero vector) and rebuild n from it.
@@ -2135,7 +2152,20 @@ __global__ __launch_bounds__(kBlock, FIRST || MESH ? 1 : PT_LATER_WAVES) void k_
 #ifdef PT_STAMPS
         t1 = t2 = t0;   // lanes past the end of a partial tile skip the inner stamps
 #endif
-        if (i < last) {
+        // a wave whose camera rays can hit no geom (camera mask 0): no raygen, no closest hit
+        // (misses draw no random number)
+        bool skip = false;
+        if (FIRST && PT_SKIP_MISS_WAVES_FUSED && MESH != kMeshPre && A.cmask) {
+            const int lp0 = __builtin_amdgcn_readfirstlane(i - it_base);
+            skip = lp0 < last - it_base && A.cmask[lp0 >> 6] == 0u;
+        }
+        if (FIRST && skip) {
+            if (i < last) {   // shade's miss exit: colour 0, retired (no record, no random number)
+                p.c = F3(0.0f, 0.0f, 0.0f);
+                p.slot = i;
+                retire<SPP1>(A, p);
+            }
+        } else if (i < last) {
             int q = i;   // physical index of the path (and of its k_traverse record)
             if (FIRST) {
                 raygen_at(A.cam, A.fl, A.tile, i, my_it, i - it_base, p);   // (a workgroup holds one iteration)
@@ -2505,7 +2535,21 @@ void k_sort_produce(const KArgs A, const SortArgs SA) {
         PathReg p;
         Hit h;
         bool ends = false;
-        if (idx < it_end) {
+        bool skip = false;
+        if (FIRST && PT_SKIP_MISS_WAVES && !VERIFY && A.cmask) {
+            const int lp0 = __builtin_amdgcn_readfirstlane(idx - it_base);
+            skip = lp0 < it_end - it_base && A.cmask[lp0 >> 6] == 0u;
+        }
+        if (skip) {
+            // A wave whose camera rays can hit no geom (mask 0) skips raygen and the closest hit: a
+            // miss draws no random number and keeps only its slot and sort key 0 (shade_ends below).
+            if (idx < it_end) {
+                p.slot = idx;
+                h = miss_hit();
+                alive = true;
+                ends = true;
+            }
+        } else if (idx < it_end) {
             if (FIRST) {   // (work position idx = iteration it's pixel idx - it * npix: a tile holds one iteration)
                 raygen_at(A.cam, A.fl, A.tile, idx, it, idx - it_base, p);
                 alive = true;

@@ -760,6 +760,10 @@ def test_two_lanes_equal_one_lane(cornell_path, monkeypatch, spp, lanes, sort):
     (((70, 30), 80.0, (3.5, 8.0, 4.0), (-2, 1, -3)), dict(aperture=1.5, focal_len=4.0, sortbyMaterial=True), (0, 1)),   # wide lens, near focus, sorted
     (((64, 48), 30.0, (0.5, 2.0, 3.0), (-1, 4, -1)), dict(SSAA=False, DoF=False), (1, 3)),   # inside the box, shard 1 of 3
     (((40, 40), 100.0, (-4.5, 9.5, 4.5), (4, 0, -4)), dict(DoF=False), (2, 4)),          # grazing views of the walls
+    # half the view past the box's open side: waves whose mask is empty skip raygen and the closest
+    # hit (PT_SKIP_MISS_WAVES), beside mixed waves; fused and material-sorted
+    (((192, 64), 45.0, (0, 5, 10.5), (14, 5, 0)), dict(), (0, 1)),
+    (((192, 64), 45.0, (0, 5, 10.5), (14, 5, 0)), dict(sortbyMaterial=True), (0, 1)),
 ])
 def test_first_bounce_camera_masks(cornell_path, monkeypatch, cam, kw, shard):
     """First-bounce geom masks (pt_kernels.hip build_cmask): each wave of camera rays bounds only
