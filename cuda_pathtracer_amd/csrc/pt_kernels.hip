@@ -2354,24 +2354,31 @@ __global__ __launch_bounds__(kBlock) void k_compact_paths(const KArgs A) {
 //                   every iteration of the pass at once.
 //                   Sort keys are counted per tile: hist[iteration][material][tile of that
 //                   iteration], and every survivor gets its rank among the same-material survivors
-//                   of its tile (one ballot per material present in the wave); hslot holds the
-//                   first slot of each (iteration, material, tile) run, 256 t + base(t, m);
+//                   of its tile (one ballot per material present in the wave).  Only the survivors
+//                   that go on to be shaded (not ending at the next shade) get a record, and those
+//                   are written compacted: material m's at 256 t + kbase(t, m) + their rank among
+//                   the tile's m-survivors that go on (kbase: the exclusive prefix of those counts
+//                   over the materials), each record carrying its rank among ALL the tile's
+//                   m-survivors (the sorted position's offset in its run); hslot holds the first
+//                   record slot of each (iteration, material, tile) run, 256 t + kbase(t, m);
 //   scan            of the histogram (k_hist_sums / k_hist_scan_sums / k_hist_apply, no co-residency
 //                   needed): tiles are in logical order, so hist's flat exclusive scan + the in-tile
 //                   rank IS the survivor's position in the stable sort by (iteration, material).
-//                   Run e's survivors are consecutive in both orders, so k_hist_apply, once it has
-//                   offs[e], writes perm[offs[e] + r] = hslot[e] + r (r < hist[e]) itself: whole
-//                   runs of coalesced stores, no scatter kernel and no per-survivor sort key.
+//                   Run e's records are consecutive in both orders, so k_hist_apply, once it has
+//                   offs[e] and offs2[e], writes the work list itself: work position offs2[e] + i
+//                   gathers record hslot[e] + i (i < hist2[e]) and keys it offs[e] + the record's
+//                   rank — whole runs of coalesced stores, no scatter kernel, no per-survivor key.
 // Batched passes sort every iteration on its own (stable sort by (iteration, material), as `spp`
 // sequential pathtrace() calls would): tiles never span two iterations, and an iteration's tiles
 // form one block of the histogram.
 // Path j of the sorted pipeline is ONE 32-byte record (only paths that go on to be shaded have one:
 // a miss or an emitter ends in the producer), so the gather reads one 32-byte span:
-//   r0 = (hit point.xyz, c.r)   r1 = (c.gb, slot, code)
+//   r0 = (hit point.xyz, c.r)   r1 = (c.gb, slot, code | rank << 24)
 // The hit point (getPointOnRay, as shade computes it) replaces the ray's origin and length.  code
 // >= 0: a cube hit, geom * 6 + slab code (Hit::frame): the material is the geom's, the normal its
 // precomputed slab normal (box_normal, which is how the hit's normal was made) and the tangent
-// frame its precomputed one.  code < 0: -(material + 1), the normal in a side plane.  The ray's
+// frame its precomputed one.  code < 0: -(material + 1), the normal in a side plane (code: 24 bits,
+// signed; rank: the record's offset in its run of the sorted order, < 256, rec_code / rec_rank).  The ray's
 // direction, which only a refractive or possibly reflective material reads (mat_needs_dir), goes
 // to a second side plane for those paths alone.  Block of 4P planes: records in the first two,
 // directions in the third, normals in the fourth.  `bounces` is not stored: every path entering
@@ -2380,20 +2387,23 @@ __global__ __launch_bounds__(kBlock) void k_compact_paths(const KArgs A) {
 __device__ __forceinline__ v4f* srec(const PathSoA& B, int j) { return B.a + 2 * (size_t)(uint32_t)j; }
 __device__ __forceinline__ v4f* sdir(const PathSoA& B, int j) { return B.a + 2 * (B.b - B.a) + (size_t)(uint32_t)j; }
 __device__ __forceinline__ v4f* snrm(const PathSoA& B, int j) { return B.a + 3 * (B.b - B.a) + (size_t)(uint32_t)j; }
+__device__ __forceinline__ int32_t rec_pack(int code, uint32_t rank) { return (int32_t)((rank << 24) | ((uint32_t)code & 0xffffffu)); }
+__device__ __forceinline__ int rec_code(int32_t w) { return (int32_t)((uint32_t)w << 8) >> 8; }
+__device__ __forceinline__ uint32_t rec_rank(int32_t w) { return (uint32_t)w >> 24; }
 
 struct SortArgs {
-    int32_t* hslot;     // per (iteration, material, tile): first slot of its run (sort_hidx)
+    int32_t* hslot;     // per (iteration, material, tile): first record slot of its run (sort_hidx)
     int32_t* hist;      // per (iteration, material, tile) survivor counts (sort_hidx)
     int32_t* offs;      // its exclusive scan: sorted positions (RNG keys)
     int32_t* hist2;     // per entry: survivors that did not end in the producer (records to shade)
     int32_t* offs2;     // its exclusive scan: the next producer's work positions
-    int32_t* perm;      // [P] work position -> physical slot
-    int32_t* fpos;      // [P] work position -> sorted position
+    int32_t* perm;      // [P] work position -> record slot
+    int32_t* fpos;      // [P] work position -> sorted position of its run's first survivor
     int32_t* itb;       // [2][kMaxSpp + 1] per parity: first tile of each iteration ([spp] = tiles)
     float* uv_out;      // textured scenes: (u, v) of the output records ([2 * cap])
-    uint32_t* dead;     // one bit per output slot: the path ended in this launch (no record; 8 words per tile)
 };
-// The next producer's work list: per work position, the slot it gathers and its sorted position.
+// The next producer's work list: per work position, the record it gathers and the sorted position
+// of the record's run (+ the record's rank = its sorted position).
 // PT_PF_PACKED (default): one (slot, position) pair per work position in `perm` (8 bytes: one store
 // and one load per path instead of two each); 0: the separate arrays perm / fpos.
 #ifndef PT_PF_PACKED
@@ -2472,8 +2482,8 @@ void k_sort_produce(const KArgs A, const SortArgs SA) {
     __shared__ int32_t s_tb[kMaxSpp + 1];      // first tile of every iteration ([spp] = all tiles)
     __shared__ uint32_t s_tmp[8];
     __shared__ uint32_t s_mw[4];
-    __shared__ uint32_t s_base[kSortMaxMats];  // the tile's exclusive prefix over materials
-    __shared__ uint32_t s_dead[2][kBlock / 32];   // per tile (two in flight): SA.dead's words
+    __shared__ uint32_t s_base[kSortMaxMats];  // the tile's exclusive prefix over materials: survivors
+    __shared__ uint32_t s_kbase[kSortMaxMats]; // ... and records (survivors that go on)
     extern __shared__ uint32_t s_kc[];   // [2][2][4][nmats] (dynamic): per wave, survivors of each material in the tile
 #define KC(buf, w, m) s_kc[((buf) * 4 + (w)) * nmats + (m)]
 #define KL(buf, w, m) s_kc[(8 + (buf) * 4 + (w)) * nmats + (m)]   // (those that did not end here)
@@ -2517,8 +2527,7 @@ void k_sort_produce(const KArgs A, const SortArgs SA) {
     if ((int)blockIdx.x >= T) return;
     if (!MESH) stage_geoms(A.S, s_geoms);
     if (!MESH && !FIRST) stage_frames(A.S, s_frm);
-    if (tid < 2 * (kBlock / 32)) s_dead[tid / (kBlock / 32)][tid % (kBlock / 32)] = 0u;
-    stage_materials(A, s_mats);   // (its barrier also orders s_dead's clearing)
+    stage_materials(A, s_mats);   // (its barrier publishes the staged tables)
     const bool lds_mats = nmats <= kLdsMats;
     const bool lds_geoms = !MESH && A.S.ngeoms <= kLdsGeoms;   // (stage_geoms / stage_frames ran)
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
@@ -2567,7 +2576,8 @@ void k_sort_produce(const KArgs A, const SortArgs SA) {
                 p.c = F3(r0[3], r1[0], r1[1]);
                 p.slot = __float_as_int(r1[2]);
                 p.bounces = A.bounce;
-                const int code = __float_as_int(r1[3]);
+                const int code = rec_code(__float_as_int(r1[3]));
+                const uint32_t rank = rec_rank(__float_as_int(r1[3]));
                 if (code >= 0) {   // a cube's slab: the geom's material, normal and frame
                     const int g = code / 6, f = code - 6 * g;
                     if (lds_geoms) {
@@ -2598,7 +2608,7 @@ void k_sort_produce(const KArgs A, const SortArgs SA) {
                 }
                 // key: sorted index within the path's own iteration (paths that ended in the
                 // previous launch hold positions too: fpos)
-                const int key = A.fl.rng_pixel ? slot_pixel(A.cam, A.tile, p.slot) : (PT_PF_PACKED ? fp : SA.fpos[idx]) - __builtin_amdgcn_readfirstlane(s_fb[it]);
+                const int key = A.fl.rng_pixel ? slot_pixel(A.cam, A.tile, p.slot) : ((PT_PF_PACKED ? fp : SA.fpos[idx]) + (int)rank) - __builtin_amdgcn_readfirstlane(s_fb[it]);
                 const float* frames = lds_geoms ? s_frm : nullptr;
                 alive = lds_mats ? shade_from(A.S, A.fl, A.tile.depth, iter, key, p, h, hitp, s_mats, frames)
                                  : shade_from(A.S, A.fl, A.tile.depth, iter, key, p, h, hitp, A.S.mats, frames);
@@ -2628,13 +2638,16 @@ void k_sort_produce(const KArgs A, const SortArgs SA) {
 #pragma unroll
         for (int q = 0; q < kSortMaxMats / 64; ++q)   // (fixed trip count: a dynamic loop here cost 34 VGPRs)
             if (lane + 64 * q < nmats) KC(k & 1, wave, lane + 64 * q) = KL(k & 1, wave, lane + 64 * q) = 0u;
-        uint32_t krank = 0;
+        uint32_t krank = 0, krank2 = 0;
         uint64_t rem = m;
         while (rem) {
             const int src = __builtin_ctzll(rem);
             const int kk = __builtin_amdgcn_readlane(key, src);
             const uint64_t mk = __ballot(key == kk);
-            if (key == kk) krank = (uint32_t)__popcll(mk & lt);
+            if (key == kk) {
+                krank = (uint32_t)__popcll(mk & lt);
+                krank2 = (uint32_t)__popcll(mk & ~me & lt);
+            }
             if (lane == src) {
                 KC(k & 1, wave, kk) = (uint32_t)__popcll(mk);
                 KL(k & 1, wave, kk) = (uint32_t)__popcll(mk & ~me);
@@ -2642,49 +2655,50 @@ void k_sort_produce(const KArgs A, const SortArgs SA) {
             rem &= ~mk;
         }
         __syncthreads();
-        if (k > 0 && tid < kBlock / 32) {   // the previous tile's SA.dead words (its ORs are behind the barrier)
-            SA.dead[(size_t)(t - (int)gridDim.x) * (kBlock / 32) + tid] = s_dead[(k - 1) & 1][tid];
-            s_dead[(k - 1) & 1][tid] = 0u;   // (next written two tiles on, after this tile's second barrier)
-        }
-        {   // material mm = tid: the tile's count and its run's first slot (exclusive prefix over the
-            // materials); the histogram entries of the tile
+        {   // material mm = tid: the tile's survivor and record counts and their exclusive prefixes over
+            // the materials (one scan of both, 16 bits each: counts <= 256); the histogram entries
             const int mm = tid;
             const uint32_t cm = mm < nmats ? (KC(k & 1, 0, mm) + KC(k & 1, 1, mm)) + (KC(k & 1, 2, mm) + KC(k & 1, 3, mm)) : 0u;
+            const uint32_t cl = mm < nmats ? (KL(k & 1, 0, mm) + KL(k & 1, 1, mm)) + (KL(k & 1, 2, mm) + KL(k & 1, 3, mm)) : 0u;
             uint32_t tot;
-            const uint32_t bm = block_excl_scan(cm, s_mw, &tot);   // (its barriers: s_base's readers are done)
+            const uint32_t bb = block_excl_scan(cm | (cl << 16), s_mw, &tot);   // (its barriers: s_base's readers are done)
             if (mm < nmats) {
-                s_base[mm] = bm;
+                s_base[mm] = bb & 0xffffu;
+                s_kbase[mm] = bb >> 16;
                 const size_t e = sort_hidx(t0, t1, nmats, t, mm);
                 SA.hist[e] = (int32_t)cm;
-                SA.hist2[e] = (int32_t)((KL(k & 1, 0, mm) + KL(k & 1, 1, mm)) + (KL(k & 1, 2, mm) + KL(k & 1, 3, mm)));
-                SA.hslot[e] = t * kBlock + (int32_t)bm;
+                SA.hist2[e] = (int32_t)cl;
+                SA.hslot[e] = t * kBlock + (int32_t)(bb >> 16);
             }
         }
         __syncthreads();
         bool em_next = false;
         if (alive) {
-            uint32_t kb = krank;
-            for (int w = 0; w < wave; ++w) kb += KC(k & 1, w, key);
-            const int q = t * kBlock + (int)(s_base[key] + kb);
+            // kb: the survivor's rank among the tile's same-material survivors (its sorted position
+            // is its run's + kb); kb2: among those that go on (its record's place in the run)
+            uint32_t kb = krank, kb2 = krank2;
+            for (int w = 0; w < wave; ++w) {
+                kb += KC(k & 1, w, key);
+                kb2 += KL(k & 1, w, key);
+            }
             // A path whose new ray misses or meets an emitter ends at the next shade without drawing
             // a random number (shade_ends): it keeps its sorted position (hist counts it, so the
             // next launch's RNG keys do), but ends here — retired with the colour that shade would
-            // give it, its slot flagged in SA.dead, no record written, and no work position in the
-            // next launch (hist2 leaves it out; k_hist_apply skips its slot).
+            // give it, no record written, and no work position in the next launch (hist2 leaves it out).
             if (ends) {
                 PathReg e = p;
                 (void)(lds_mats ? shade_ends(h, s_mats, e) : shade_ends(h, A.S.mats, e));
-                atomicOr(&s_dead[k & 1][(q - t * kBlock) >> 5], 1u << (q & 31));
                 em_next = e.c.x != 0.0f || e.c.y != 0.0f || e.c.z != 0.0f;
                 retire<SPP1>(A, e);
             } else {
+                const int q = t * kBlock + (int)(s_kbase[key] + kb2);
                 v4f* r = srec(A.out, q);
                 // (plain stores: each store instruction covers 16 of every 32 bytes, and L2 merges the
                 // two into whole lines; non-temporal ones halved config 3's rate)
                 const f3 hitp = point_on_ray(p.o, p.d, h.t);
                 const int code = h.frame >= 0 ? h.frame : -(h.mat + 1);
                 r[0] = v4f{hitp.x, hitp.y, hitp.z, p.c.x};
-                r[1] = v4f{p.c.y, p.c.z, __int_as_float(p.slot), __int_as_float(code)};
+                r[1] = v4f{p.c.y, p.c.z, __int_as_float(p.slot), __int_as_float(rec_pack(code, kb))};
                 if (code < 0) snrm(A.out, q)[0] = v4f{h.n.x, h.n.y, h.n.z, 0.0f};
                 if (lds_mats ? mat_needs_dir(s_mats[h.mat]) : mat_needs_dir(A.S.mats[h.mat]))
                     sdir(A.out, q)[0] = v4f{p.d.x, p.d.y, p.d.z, 0.0f};
@@ -2696,9 +2710,6 @@ void k_sort_produce(const KArgs A, const SortArgs SA) {
         }
         emit_next += (uint32_t)__popcll(__ballot(em_next));
     }
-    __syncthreads();   // the last tile's SA.dead words
-    if (k > 0 && tid < kBlock / 32)
-        SA.dead[(size_t)((int)blockIdx.x + (k - 1) * (int)gridDim.x) * (kBlock / 32) + tid] = s_dead[(k - 1) & 1][tid];
     // (the camera rays' ends are bounce 0's; a later producer's are the next bounce's)
     flush_emissive2(A, emit_cnt, FIRST ? A.bounce : A.bounce + 1, emit_next, s_cnt);
 #undef KC
@@ -2709,9 +2720,6 @@ void k_sort_produce(const KArgs A, const SortArgs SA) {
 // the tile sums (one workgroup), rescan.  No workgroup waits on another, so unlike the library's
 // single-pass scan (whose static schedule needs its whole grid co-resident) two of these can run
 // side by side.  The histogram is small (nmats x paths / 64 ints) and cache-resident.
-#ifndef PT_HIST_APPLY
-#define PT_HIST_APPLY 1   // the work list: 1 runs written one at a time per wave; 2 lane-parallel (k_hist_apply2)
-#endif
 constexpr int kHistPer = 4;                        // ints per thread (one 16-byte load)
 constexpr int kHistTile = kBlock * kHistPer;       // 1024: 4x the workgroups of 4096 (latency-bound scan)
 
@@ -2796,21 +2804,17 @@ __device__ __forceinline__ void hist_store(int32_t* __restrict__ out, int64_t n,
 }
 
 // The scans (out: sorted positions, out2: work positions) and the next producer's work list: for
-// the live entries but the last (the end offset, whose count is not written), the run's slots
-// hslot[e] + r whose path did not end (SA.dead bit clear), in order, at work positions out2[e] + i:
-// perm = the slot, fpos = its sorted position out[e] + r.
+// the live entries but the last (the end offset, whose count is not written), run e's records
+// hslot[e] + i (i < in2[e]: the survivors that go on, stored consecutively by the producer) at work
+// positions out2[e] + i, each with its run's sorted position out[e] (the record adds its rank).
 __global__ __launch_bounds__(kBlock) void k_hist_apply(const int32_t* __restrict__ in, int32_t* __restrict__ out,
                                                        const int32_t* __restrict__ in2, int32_t* __restrict__ out2,
                                                        int64_t n, const uint32_t* nlive, const uint32_t* __restrict__ sums,
                                                        const int32_t* __restrict__ hslot, int32_t* __restrict__ perm,
-                                                       int32_t* __restrict__ fpos, const uint32_t* __restrict__ dead) {
+                                                       int32_t* __restrict__ fpos) {
     __shared__ uint32_t s_w[4], s_w2[4];
-    // each entry's tile's 8 SA.dead words (entries with ended paths only), all loads in flight at
-    // once, so the stores below wait on no load per run (rows are per wave: no block barrier)
-    __shared__ uint32_t s_dm[kHistTile * (kBlock / 32)];
     n = hist_n(n, nlive);
     const int lane = (int)threadIdx.x & 63;
-    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     for (int64_t blk = blockIdx.x; blk * kHistTile < n; blk += gridDim.x) {   // (as k_hist_sums)
         const int64_t base = blk * kHistTile + (int64_t)threadIdx.x * kHistPer;
         uint32_t x[kHistPer], y[kHistPer], v = 0, v2 = 0;
@@ -2824,16 +2828,6 @@ __global__ __launch_bounds__(kBlock) void k_hist_apply(const int32_t* __restrict
         int32_t s0[kHistPer];
 #pragma unroll
         for (int k = 0; k < kHistPer; ++k) s0[k] = (base + k < n - 1 && y[k] != 0u) ? hslot[base + k] : 0;
-#pragma unroll
-        for (int k = 0; k < kHistPer; ++k) {
-            if (base + k < n - 1 && y[k] != 0u && y[k] != x[k]) {
-                const v4i_h* d = reinterpret_cast<const v4i_h*>(dead + (size_t)((uint32_t)s0[k] >> 8) * (kBlock / 32));
-                v4i_h* l = reinterpret_cast<v4i_h*>(s_dm + ((int)threadIdx.x * kHistPer + k) * (kBlock / 32));
-                l[0] = d[0];
-                l[1] = d[1];
-            }
-        }
-        wave_sync();   // (each wave reads only its own entries' rows)
         uint32_t o = run, o2 = run2;
 #pragma unroll
         for (int k = 0; k < kHistPer; ++k) {   // the wave writes its entries' runs one after the other
@@ -2841,26 +2835,10 @@ __global__ __launch_bounds__(kBlock) void k_hist_apply(const int32_t* __restrict
             while (rem) {
                 const int src = __builtin_ctzll(rem);
                 const uint32_t ro = __builtin_amdgcn_readlane(o, src), ro2 = __builtin_amdgcn_readlane(o2, src);
-                const uint32_t rc = __builtin_amdgcn_readlane(x[k], src), rl = __builtin_amdgcn_readlane(y[k], src);
-                const uint32_t rs = (uint32_t)__builtin_amdgcn_readlane(s0[k], src);
-                if (rl == rc) {   // no path of the run ended: 64 consecutive positions per store
-                    for (uint32_t r = (uint32_t)lane; r < rc; r += 64) {
-                        pf_store(perm, fpos, ro2 + r, (int32_t)(rs + r), (int32_t)(ro + r));
-                    }
-                } else {
-                    const uint32_t* dm = s_dm + (((int)threadIdx.x & ~63) + src) * kHistPer * (kBlock / 32) + k * (kBlock / 32);
-                    uint32_t i0 = 0;
-                    for (uint32_t r0 = 0; r0 < rc; r0 += 64) {
-                        const uint32_t r = r0 + (uint32_t)lane, b = (rs & (kBlock - 1)) + r;   // (a run lies inside its tile)
-                        const bool keep = r < rc && ((dm[(b >> 5) & 7] >> (b & 31)) & 1u) == 0u;
-                        const uint64_t km = __ballot(keep);
-                        if (keep) {
-                            const uint32_t i = i0 + (uint32_t)__popcll(km & lt);
-                            pf_store(perm, fpos, ro2 + i, (int32_t)(rs + r), (int32_t)(ro + r));
-                        }
-                        i0 += (uint32_t)__popcll(km);
-                    }
-                }
+                const uint32_t rl = __builtin_amdgcn_readlane(y[k], src);
+                const int32_t rs = __builtin_amdgcn_readlane(s0[k], src);
+                for (uint32_t r = (uint32_t)lane; r < rl; r += 64)   // 64 consecutive positions per store
+                    pf_store(perm, fpos, ro2 + r, rs + (int32_t)r, (int32_t)ro);
                 rem &= rem - 1;
             }
             o += x[k];
@@ -2868,106 +2846,6 @@ __global__ __launch_bounds__(kBlock) void k_hist_apply(const int32_t* __restrict
         }
         hist_store(out, n, base, run, x);
         hist_store(out2, n, base, run2, y);
-        wave_sync();   // (this wave's s_dm rows are rewritten by the next block)
-    }
-}
-
-// k_hist_apply, lane-parallel form (PT_HIST_APPLY=2): the same outputs.  A block's entries write one
-// contiguous range of work positions (their exclusive scan), so instead of walking the runs one at a
-// time per wave, every thread takes work positions w = tid, tid + 256, ... of the block's range,
-// finds its entry by a binary search over the entries' starts (LDS) and its slot in the run (the
-// w-th path that goes on: the run's dead bits skipped by a popcount select), and the block writes
-// perm / fpos in coalesced 256-position strides.
-__device__ __forceinline__ int select_bit(uint32_t m, int i) {   // position of the i-th set bit of m
-    int pos = 0;
-#pragma unroll
-    for (int w = 16; w >= 1; w >>= 1) {
-        const uint32_t lo = m & ((1u << w) - 1u);
-        const int c = __popc(lo);
-        if (i >= c) { i -= c; m >>= w; pos += w; } else { m = lo; }
-    }
-    return pos;
-}
-__global__ __launch_bounds__(kBlock) void k_hist_apply2(const int32_t* __restrict__ in, int32_t* __restrict__ out,
-                                                        const int32_t* __restrict__ in2, int32_t* __restrict__ out2,
-                                                        int64_t n, const uint32_t* nlive, const uint32_t* __restrict__ sums,
-                                                        const int32_t* __restrict__ hslot, int32_t* __restrict__ perm,
-                                                        int32_t* __restrict__ fpos, const uint32_t* __restrict__ dead) {
-    __shared__ uint32_t s_w[4], s_w2[4];
-    __shared__ uint32_t s_start[kHistTile + 1];   // entry j's first work position, block-local (+ end)
-    __shared__ uint32_t s_o[kHistTile];           // entry j's sorted position (out)
-    __shared__ int32_t s_slot[kHistTile];         // entry j's first slot (hslot); -1: no path went on
-    __shared__ uint32_t s_x[kHistTile];           // entry j's survivors (x): == its count that went on when no path ended
-    n = hist_n(n, nlive);
-    const int tid = (int)threadIdx.x;
-    for (int64_t blk = blockIdx.x; blk * kHistTile < n; blk += gridDim.x) {   // (as k_hist_sums)
-        const int64_t base = blk * kHistTile + (int64_t)tid * kHistPer;
-        uint32_t x[kHistPer], y[kHistPer], v = 0, v2 = 0;
-        hist_load(in, n, base, x);
-        hist_load(in2, n, base, y);
-#pragma unroll
-        for (int k = 0; k < kHistPer; ++k) {
-            if (!(base + k < n - 1)) y[k] = 0u;   // (the end offset's entry: no run)
-            v += x[k];
-            v2 += y[k];
-        }
-        uint32_t total, total2;
-        const uint32_t run = block_excl_scan(v, s_w, &total) + sums[2 * blk];
-        const uint32_t lrun2 = block_excl_scan(v2, s_w2, &total2);   // block-local work positions
-        const uint32_t B2 = sums[2 * blk + 1];
-        {
-            uint32_t o = run, o2 = lrun2;
-#pragma unroll
-            for (int k = 0; k < kHistPer; ++k) {
-                const int j = tid * kHistPer + k;
-                s_start[j] = o2;
-                s_o[j] = o;
-                s_x[j] = x[k];
-                s_slot[j] = y[k] != 0u ? hslot[base + k] : -1;
-                o += x[k];
-                o2 += y[k];
-            }
-            if (tid == kBlock - 1) s_start[kHistTile] = o2;
-        }
-        // the scans themselves (out: every survivor's sorted position base; out2: work positions),
-        // from the ORIGINAL counts (the end offset entry included, as k_hist_apply writes them)
-        {
-            uint32_t xs[kHistPer], ys[kHistPer];
-            hist_load(in2, n, base, ys);
-#pragma unroll
-            for (int k = 0; k < kHistPer; ++k) xs[k] = x[k];
-            hist_store(out, n, base, run, xs);
-            hist_store(out2, n, base, lrun2 + B2, ys);
-        }
-        __syncthreads();
-        int e = 0;
-        for (uint32_t w = (uint32_t)tid; w < total2; w += kBlock) {
-            int lo = e, hi = kHistTile - 1;   // the last entry whose start <= w (starts never decrease)
-            while (lo < hi) {
-                const int mid = (lo + hi + 1) >> 1;
-                if (s_start[mid] <= w) lo = mid; else hi = mid - 1;
-            }
-            e = lo;
-            const uint32_t i = w - s_start[e];
-            const int32_t rs = s_slot[e];
-            const uint32_t xe = s_x[e], ye = s_start[e + 1] - s_start[e];
-            uint32_t r = i;
-            if (ye != xe) {   // some paths of the run ended in the producer: the i-th that did not
-                const uint32_t* dm = dead + (size_t)((uint32_t)rs >> 8) * (kBlock / 32);
-                const uint32_t b0 = (uint32_t)rs & (kBlock - 1u), b1 = b0 + xe;   // the run's bits [b0, b1)
-                uint32_t left = i;
-                for (uint32_t wd = b0 >> 5; wd <= ((b1 - 1u) >> 5); ++wd) {
-                    uint32_t m = ~dm[wd];
-                    if (wd == (b0 >> 5)) m &= ~0u << (b0 & 31u);
-                    if (wd == ((b1 - 1u) >> 5) && (b1 & 31u)) m &= (1u << (b1 & 31u)) - 1u;
-                    const uint32_t c = (uint32_t)__popc(m);
-                    if (left < c) { r = wd * 32u + (uint32_t)select_bit(m, (int)left) - b0; break; }
-                    left -= c;
-                }
-            }
-            pf_store(perm, fpos, B2 + w, rs + (int32_t)r, (int32_t)(s_o[e] + r));
-        }
-        __syncthreads();   // (the LDS rows are rewritten by the next block)
     }
 }
 
@@ -3111,7 +2989,6 @@ struct pt_ctx {
     struct SortSet {   // material-sort buffers of one lane (k_sort_produce / k_hist_*)
         int32_t *hslot = nullptr, *hist = nullptr, *offs = nullptr, *perm = nullptr, *itb = nullptr;
         int32_t *hist2 = nullptr, *offs2 = nullptr, *fpos = nullptr;
-        uint32_t* dead = nullptr;   // (k_sort_produce -> k_hist_apply: slots whose path ended)
         float* uv[2] = {nullptr, nullptr};   // (u, v) of the records in buf[0] / buf[1]
         uint32_t* sums = nullptr;            // histogram scan: tile sums
         int64_t hist_cap = 0;                // histogram entries allocated (+ the end offset)
@@ -4239,7 +4116,6 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
         const size_t tiles = ((size_t)ss.hist_cap + kHistTile - 1) / kHistTile;
         if (int rc = c->alloc(&ss.hslot, (size_t)ss.hist_cap)) return bail(rc);
         if (int rc = c->alloc(&ss.perm, PT_PF_PACKED ? 2 * paths : paths)) return bail(rc);   // (pf_store)
-        if (int rc = c->alloc(&ss.dead, (cap / kBlock + 2) * (kBlock / 32))) return bail(rc);
         if (int rc = c->alloc(&ss.fpos, PT_PF_PACKED ? 1 : paths)) return bail(rc);
         if (int rc = c->alloc(&ss.hist2, (size_t)ss.hist_cap)) return bail(rc);
         if (int rc = c->alloc(&ss.offs2, (size_t)ss.hist_cap)) return bail(rc);
@@ -4333,7 +4209,7 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
             a.in = bufs[lcur];
             a.out = bufs[lcur ^ 1];
             a.hit.uv = ss.uv[lcur];
-            const SortArgs sa{ss.hslot, ss.hist, ss.offs, ss.hist2, ss.offs2, ss.perm, ss.fpos, ss.itb, ss.uv[lcur ^ 1], ss.dead};
+            const SortArgs sa{ss.hslot, ss.hist, ss.offs, ss.hist2, ss.offs2, ss.perm, ss.fpos, ss.itb, ss.uv[lcur ^ 1]};
 #ifndef PT_PRODUCER_ALWAYS_VERIFY
 #define PT_PRODUCER_ALWAYS_VERIFY 0   // (A/B knob: the diagnostic producer build for every run, round 3's form)
 #endif
@@ -4358,9 +4234,9 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
         hipLaunchKernelGGL(k_hist_sums, dim3(hgrid), dim3(kBlock), 0, s, (const int32_t*)ss.hist, (const int32_t*)ss.hist2,
                            ss.hist_cap, nlive, ss.sums);
         hipLaunchKernelGGL(k_hist_scan_sums, dim3(1), dim3(kBlock), 0, s, ss.sums, ss.hist_cap, nlive);
-        hipLaunchKernelGGL(PT_HIST_APPLY == 2 ? k_hist_apply2 : k_hist_apply, dim3(hgrid), dim3(kBlock), 0, s,
+        hipLaunchKernelGGL(k_hist_apply, dim3(hgrid), dim3(kBlock), 0, s,
                            (const int32_t*)ss.hist, ss.offs, (const int32_t*)ss.hist2, ss.offs2, ss.hist_cap, nlive,
-                           (const uint32_t*)ss.sums, (const int32_t*)ss.hslot, ss.perm, ss.fpos, (const uint32_t*)ss.dead);
+                           (const uint32_t*)ss.sums, (const int32_t*)ss.hslot, ss.perm, ss.fpos);
         HIP_TRY(hipGetLastError());
         if (int rc = produce(false)) return rc;
         return prof_end(ev, s);
