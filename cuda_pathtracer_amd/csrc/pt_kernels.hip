@@ -147,9 +147,10 @@ struct Hit {
 #define PT_SKIP_MISS_WAVES 1   // (A/B knob: the sorted camera-ray producer's waves whose camera mask is empty skip
                                // raygen + closest hit: config 3 35.6k -> 36.9k, same box)
 #endif
-#ifndef PT_SKIP_MISS_WAVES_FUSED
-#define PT_SKIP_MISS_WAVES_FUSED 0   // (the same in the fused first bounce: 5 more VGPRs there, Cornell -1.1%)
-#endif
+// The fused first bounce does the same in its own instantiation (k_bounce<true, .., kAnalyticSkip>: 5
+// more VGPRs), chosen per context when at least kSkipEmptyMin of the camera-mask blocks are empty
+// (build_cmask; config 4's 16:9 view +4.0%, while Cornell at 800x800 lost 1.1% to the registers).
+constexpr double kSkipEmptyMin = 0.2;
 // What the closest hit returns for a ray that meets nothing (intersect_bounded, computeIntersections'
 // t = -1 with materialId 0: pathtrace.cu:466).
 __device__ __forceinline__ Hit miss_hit() {
@@ -1341,7 +1342,8 @@ __device__ __forceinline__ int seg_walk(const int32_t* s_pre, int nseg, int s, i
 // the k-th survivor of the previous launch's segments (prefix of the segment words in LDS), record =
 // its physical slot.  Record: (t, BVH-order triangle index or -1, bx, by).
 constexpr int kMeshInline = 1;   // k_bounce MESH modes: 0 no mesh, 1 traversal inside k_bounce,
-constexpr int kMeshPre = 2;      // 2 closest mesh hit precomputed by k_traverse
+constexpr int kMeshPre = 2;      // 2 closest mesh hit precomputed by k_traverse,
+constexpr int kAnalyticSkip = 3; // 3 no mesh, first bounce: waves with an empty camera mask skip raygen + hit
 constexpr int kTravChunk = 256;  // rays per ticket grab
 constexpr int kRefillMin = 16;   // idle lanes that trigger a refill
 constexpr int kTravLdsRows = 32; // LDS stack entries per thread (HybStack; the rest in scratch)
@@ -2155,7 +2157,7 @@ __global__ __launch_bounds__(kBlock, FIRST || MESH ? 1 : PT_LATER_WAVES) void k_
         // a wave whose camera rays can hit no geom (camera mask 0): no raygen, no closest hit
         // (misses draw no random number)
         bool skip = false;
-        if (FIRST && PT_SKIP_MISS_WAVES_FUSED && MESH != kMeshPre && A.cmask) {
+        if (FIRST && MESH == kAnalyticSkip && A.cmask) {
             const int lp0 = __builtin_amdgcn_readfirstlane(i - it_base);
             skip = lp0 < last - it_base && A.cmask[lp0 >> 6] == 0u;
         }
@@ -2949,6 +2951,8 @@ struct pt_ctx {
     bool fused = true;   // pipeline: fused bounce kernel (default) or trace + compact
     uint64_t compact_launches = 0;   // parity of the look-back status / live-count words
     uint64_t n_cmask_builds = 0, n_flag_syncs = 0;   // pt_ctx_counters
+    double cmask_empty = 0.0;    // share of the camera-mask blocks whose mask is empty (build_cmask)
+    bool cmask_skip = false;     // the fused first bounce's empty-wave instantiation is in use
     // owned device allocations
     std::vector<void*> allocs;
     PathSoA buf[2]{};
@@ -3217,6 +3221,8 @@ int build_cmask(pt_ctx* c) {
     KArgs& A = c->args;
     A.cmask = nullptr;
     ++c->n_cmask_builds;
+    c->cmask_empty = 0.0;
+    c->cmask_skip = false;
     const int ng = A.S.ngeoms;
     const char* off = std::getenv("PT_AMD_NO_CMASK");
     if ((off && std::strcmp(off, "1") == 0) || ng <= 0 || ng > kLdsGeoms || A.S.ntris > 0) return PT_OK;
@@ -3340,6 +3346,14 @@ int build_cmask(pt_ctx* c) {
     hipError_t e = hipMemcpy(c->d_cmask, mask.data(), nblk * sizeof(uint32_t), hipMemcpyHostToDevice);
     if (e != hipSuccess) return pt::fail(PT_ERR_HIP, std::string("camera masks: ") + hipGetErrorString(e));
     A.cmask = c->d_cmask;
+    size_t empty = 0;
+    for (uint32_t m : mask) empty += m == 0u;
+    c->cmask_empty = nblk ? (double)empty / (double)nblk : 0.0;
+    c->cmask_skip = c->cmask_empty >= kSkipEmptyMin;
+    if (const char* sk = std::getenv("PT_AMD_SKIP_EMPTY")) {   // A/B and tests: 0 never, 1 always
+        if (std::strcmp(sk, "0") == 0) c->cmask_skip = false;
+        if (std::strcmp(sk, "1") == 0) c->cmask_skip = true;
+    }
     return PT_OK;
 }
 
@@ -3408,7 +3422,8 @@ int mesh_mode(const pt_ctx* c) {
 }
 
 using KernelFn = void (*)(const KArgs);
-KernelFn bounce_kernel(bool first, bool spp1, int mesh) {   // mesh: 0, kMeshInline, kMeshPre
+KernelFn bounce_kernel(bool first, bool spp1, int mesh, bool skip = false) {   // mesh: 0, kMeshInline, kMeshPre
+    if (first && skip && mesh == 0) return spp1 ? k_bounce<true, true, kAnalyticSkip> : k_bounce<true, false, kAnalyticSkip>;
     static const KernelFn table[12] = {
         k_bounce<false, false, 0>, k_bounce<false, false, 1>, k_bounce<false, false, 2>,
         k_bounce<false, true, 0>,  k_bounce<false, true, 1>,  k_bounce<false, true, 2>,
@@ -3466,7 +3481,7 @@ int launch_bounce(pt_ctx* c, bool first, bool spp1, int mesh, hipStream_t st, co
         if (int rc = prof_end(ev, st)) return rc;
     }
     if (int rc = prof_begin(c, st, first ? PT_KIND_FIRST_BOUNCE : PT_KIND_BOUNCE, &ev)) return rc;
-    hipLaunchKernelGGL(bounce_kernel(first, spp1, mesh), dim3(c->grid_bounce[first]), dim3(kBlock),
+    hipLaunchKernelGGL(bounce_kernel(first, spp1, mesh, first && c->cmask_skip), dim3(c->grid_bounce[first]), dim3(kBlock),
                        bounce_lds_bytes(a.S, mesh), st, a);
     HIP_TRY(hipGetLastError());
     return prof_end(ev, st);
@@ -4171,6 +4186,14 @@ int pt_ctx_walk_info(const pt_ctx* c, int32_t* quad_walk, int32_t* tcull_on, dou
     if (quad_walk) *quad_walk = c->trav_quads ? 1 : 0;
     if (tcull_on) *tcull_on = c->args.S.qcull != nullptr ? 1 : 0;
     if (tcull_frac) *tcull_frac = c->tcull_frac;
+    return PT_OK;
+}
+
+int pt_ctx_cmask_info(const pt_ctx* c, int32_t* on, double* empty_frac, int32_t* skip_fused) {
+    if (!c) return pt::fail(PT_ERR_ARG, "null context");
+    if (on) *on = c->args.cmask != nullptr ? 1 : 0;
+    if (empty_frac) *empty_frac = c->cmask_empty;
+    if (skip_fused) *skip_fused = c->cmask_skip ? 1 : 0;
     return PT_OK;
 }
 

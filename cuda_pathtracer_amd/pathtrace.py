@@ -301,6 +301,13 @@ class PathTracer:
         check_pt(lib().pt_ctx_counters(self._h, C.byref(b), C.byref(y)))
         return {"mask_builds": int(b.value), "flag_syncs": int(y.value)}
 
+    def cmask_info(self) -> dict:
+        """First-bounce camera masks (pt_ctx_cmask_info): built, share of empty 64-pixel blocks, and
+        whether the fused first bounce skips those waves in its own instantiation."""
+        on, sk, fr = C.c_int32(), C.c_int32(), C.c_double()
+        check_pt(lib().pt_ctx_cmask_info(self._h, C.byref(on), C.byref(fr), C.byref(sk)))
+        return {"on": bool(on.value), "empty_frac": float(fr.value), "skip_fused": bool(sk.value)}
+
     def walk_info(self) -> dict:
         """Mesh scenes: 4-wide walk on/off, its exact t-cull on/off and the share of slots whose
         cull margin can pay (pt_ctx_walk_info)."""

@@ -242,6 +242,11 @@ int pt_set_flags(pt_ctx* c, const pt_flags* flags);
 /* Host-side counters of a context: first-bounce camera-mask builds (pt_create builds one) and the
  * pt_set_flags calls that synchronised the device. */
 int pt_ctx_counters(const pt_ctx* c, uint64_t* mask_builds, uint64_t* flag_syncs);
+/* Inspection: the first-bounce camera masks of a context — built (on), the share of 64-pixel blocks
+ * whose mask is empty (no geom reachable: those waves skip raygen and the closest hit), and whether
+ * the fused first bounce runs its empty-wave instantiation (chosen when that share is >= 0.2;
+ * PT_AMD_SKIP_EMPTY=0/1 forces it).  Results are the same bits either way. */
+int pt_ctx_cmask_info(const pt_ctx* c, int32_t* on, double* empty_frac, int32_t* skip_fused);
 /* Mesh scenes: whether the BVH walk runs on the 4-wide layout, whether its exact t-cull is on, and
  * the share of the layout's slots whose cull margin can pay.  The cull is on when
  * that share is >= 1/4 (PT_AMD_TCULL=0/1 forces it); it never changes a result. */

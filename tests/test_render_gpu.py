@@ -796,6 +796,38 @@ def test_first_bounce_camera_masks(cornell_path, monkeypatch, cam, kw, shard):
     _assert_bitexact(gi, img, f"masks after set_flags {kw2}")
 
 
+@pytest.mark.parametrize("look,want_skip", [((14, 5, 0), True), ((0, 5, 0), None)])
+def test_fused_empty_wave_skip(cornell_path, monkeypatch, look, want_skip):
+    """The fused first bounce's empty-wave instantiation (k_bounce mode kAnalyticSkip: waves whose
+    camera mask is empty skip raygen and the closest hit) is chosen from the share of empty mask
+    blocks (pt_ctx_cmask_info); forced on, forced off and chosen, the image equals the oracle's."""
+    from cuda_pathtracer_amd import PathTracer, Scene
+    res = (192, 64)
+    s = Scene(cornell_path)
+    s.set_camera(res, 45.0, (0, 5, 10.5), look, (0, 1, 0))
+    s.finalize()
+    o = O.OracleScene.from_json(cornell_path)
+    o.set_camera(res, 45.0, (0, 5, 10.5), look, (0, 1, 0))
+    pt = PathTracer(s, _gui(), spp=2)
+    info = pt.cmask_info()
+    pt.free()
+    assert info["on"]
+    assert info["skip_fused"] == (info["empty_frac"] >= 0.2)
+    if want_skip is not None:
+        assert info["skip_fused"] == want_skip and info["empty_frac"] > 0.3
+    ref = None
+    for force in ("1", "0", None):
+        if force is None:
+            monkeypatch.delenv("PT_AMD_SKIP_EMPTY", raising=False)
+        else:
+            monkeypatch.setenv("PT_AMD_SKIP_EMPTY", force)
+        g, r, _, _ = _run(s, o, _gui(), iters=4, spp=2)
+        _assert_bitexact(g, r, f"skip forced {force} look {look}")
+        if ref is not None:
+            _assert_bitexact(g, ref, "skip on vs off")
+        ref = g
+
+
 def test_set_flags_unchanged_is_cheap(cornell_path):
     """The reference re-reads its GUI flags on every pathtrace() call (pathtrace.cu:438-463), so a
     drop-in caller calls pt_set_flags once per iteration.  Unchanged flags — and flags that do not
