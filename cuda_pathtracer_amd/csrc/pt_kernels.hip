@@ -4253,7 +4253,10 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
         a.parity = (int)(lc & 1);
         const uint32_t* nlive = &a.ctl[a.parity].hist_live;
         const int tiles = (int)((ss.hist_cap + kHistTile - 1) / kHistTile);
-        const int hgrid = std::min(tiles, 4 * c->cus);   // (grid-stride over the live blocks)
+#ifndef PT_HIST_GRID
+#define PT_HIST_GRID 4   // (A/B knob: histogram-scan workgroups per CU)
+#endif
+        const int hgrid = std::min(tiles, PT_HIST_GRID * c->cus);   // (grid-stride over the live blocks)
         hipLaunchKernelGGL(k_hist_sums, dim3(hgrid), dim3(kBlock), 0, s, (const int32_t*)ss.hist, (const int32_t*)ss.hist2,
                            ss.hist_cap, nlive, ss.sums);
         hipLaunchKernelGGL(k_hist_scan_sums, dim3(1), dim3(kBlock), 0, s, ss.sums, ss.hist_cap, nlive);
