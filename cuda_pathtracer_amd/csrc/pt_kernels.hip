@@ -151,6 +151,9 @@ struct Hit {
 // more VGPRs), chosen per context when at least kSkipEmptyMin of the camera-mask blocks are empty
 // (build_cmask; config 4's 16:9 view +4.0%, while Cornell at 800x800 lost 1.1% to the registers).
 constexpr double kSkipEmptyMin = 0.2;
+#ifndef PT_SKIP_EMPTY_TILES
+#define PT_SKIP_EMPTY_TILES 1   // (A/B knob: the plain fused first bounce skips tiles whose 4 mask blocks are all empty)
+#endif
 // What the closest hit returns for a ray that meets nothing (intersect_bounded, computeIntersections'
 // t = -1 with materialId 0: pathtrace.cu:466).
 __device__ __forceinline__ Hit miss_hit() {
@@ -2148,6 +2151,28 @@ __global__ __launch_bounds__(kBlock, FIRST || MESH ? 1 : PT_LATER_WAVES) void k_
 #endif
     for (int base = first; base < last; base += kBlock, ++k) {
         const int i = base + tid;
+        if (FIRST && MESH == 0 && PT_SKIP_EMPTY_TILES && A.cmask) {
+            // a tile whose four camera-mask blocks are all empty: every ray misses — shade's miss exit
+            // (colour 0, no random number) without raygen, closest hit or the tile's ballots and
+            // barrier (workgroup-uniform; k stays, so the count buffers keep alternating per barrier)
+            const int lp0 = base - it_base, nb = ((last - it_base) + 63) >> 6;
+            uint32_t any = 0u;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                const int b = (lp0 >> 6) + w;
+                any |= b < nb ? A.cmask[b] : 0u;
+            }
+            if (any == 0u) {
+                if (i < last) {
+                    PathReg z;
+                    z.c = F3(0.0f, 0.0f, 0.0f);
+                    z.slot = i;
+                    retire<SPP1>(A, z);
+                }
+                --k;
+                continue;
+            }
+        }
         bool alive = false, emitted = false;
         PathReg p;
         STAMP(t0);
