@@ -2571,6 +2571,34 @@ void k_sort_produce(const KArgs A, const SortArgs SA) {
         PathReg p;
         Hit h;
         bool ends = false;
+        if (FIRST && PT_SKIP_EMPTY_TILES && !VERIFY && A.cmask) {
+            // the whole tile's camera-mask blocks empty (workgroup-uniform): every ray misses — colour
+            // 0 retired, one run of material 0 holding the tile's paths and no record; the tile's
+            // ballots and barriers are skipped (k stays: the count buffers alternate per barrier)
+            const int lp0 = idx - tid - it_base, nb = ((it_end - it_base) + 63) >> 6;
+            uint32_t any = 0u;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                const int b = (lp0 >> 6) + w;
+                any |= b < nb ? A.cmask[b] : 0u;
+            }
+            if (any == 0u) {
+                if (idx < it_end) {
+                    PathReg z;
+                    z.c = F3(0.0f, 0.0f, 0.0f);
+                    z.slot = idx;
+                    retire<SPP1>(A, z);
+                }
+                if (tid < nmats) {
+                    const size_t e = sort_hidx(t0, t1, nmats, t, tid);
+                    SA.hist[e] = tid == 0 ? min(kBlock, it_end - (idx - tid)) : 0;
+                    SA.hist2[e] = 0;
+                    SA.hslot[e] = t * kBlock;
+                }
+                --k;
+                continue;
+            }
+        }
         bool skip = false;
         if (FIRST && PT_SKIP_MISS_WAVES && !VERIFY && A.cmask) {
             const int lp0 = __builtin_amdgcn_readfirstlane(idx - it_base);
