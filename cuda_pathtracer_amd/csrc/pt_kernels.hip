@@ -4406,7 +4406,12 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
                           b == 0 ? PT_KIND_FIRST_BOUNCE : PT_KIND_BOUNCE, A);
             if (rc) return rc;
             if (!last) {
-                if ((rc = launch_k(c, k_compact_paths, c->grid_compact, st, PT_KIND_COMPACT, A))) return rc;
+                // batched passes: the previous pass's finalize (side stream) may hold CUs while this
+                // look-back runs, so its static co-resident schedule is not guaranteed — tiles are
+                // claimed instead (lookback.h; the split pipeline is the diagnostic one)
+                KArgs Ac = A;
+                if (!spp1) Ac.fl.claimed = 1;
+                if ((rc = launch_k(c, k_compact_paths, c->grid_compact, st, PT_KIND_COMPACT, Ac))) return rc;
                 ++c->compact_launches;
                 cur ^= 1;
             }

@@ -180,6 +180,29 @@ def test_batched_pass_equals_sequential_passes(cornell_path, monkeypatch, kw, pi
     assert stb["bounce_live"] == sts["bounce_live"]
 
 
+def test_split_pipeline_back_to_back_batched_passes(cornell_path, monkeypatch):
+    """The split (diagnostic) pipeline's look-back compaction while the previous pass's finalize still
+    runs on its side stream: large batched passes back to back complete without a device error (its
+    tiles are claimed, not statically co-resident, in batched passes) and equal the fused pipeline."""
+    from cuda_pathtracer_amd import PathTracer
+    s, _ = _pair(cornell_path, (320, 240))
+    out = []
+    for pipeline in ("split", "fused"):
+        if pipeline == "split":
+            monkeypatch.setenv("PT_PIPELINE", "split")
+        else:
+            monkeypatch.delenv("PT_PIPELINE", raising=False)
+        pt = PathTracer(s, _gui(), spp=32)
+        for k in range(4):
+            pt.render_pass(1 + 32 * k)
+        st = pt.stats()
+        out.append((pt.image(), st["bounce_live"], st["device_error"]))
+        pt.free()
+    assert out[0][2] == 0 and out[1][2] == 0
+    _assert_bitexact(out[0][0], out[1][0], "split vs fused, 4 x 32 iterations")
+    assert out[0][1] == out[1][1]
+
+
 def test_rng_key_pixel_shards_equal_single_gpu(cornell_path):
     """§8e's shard-invariant mode on the device: with rngKeyPixel the 3-way row shards, assembled,
     equal the 1-GPU image bit for bit — and so does the material-sorted pipeline."""
