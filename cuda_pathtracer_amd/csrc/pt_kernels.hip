@@ -3066,6 +3066,15 @@ struct pt_ctx {
     hipEvent_t ev_pass[2] = {}, ev_fin[2] = {};
     bool fin_out[2] = {false, false};
     int col_half = 0, last_fin = -1;
+    // Context-scoped synchronisation (no hipDeviceSynchronize, no synchronous copy on the legacy
+    // default stream): ev_done is recorded after the last work this context enqueued (a pass ends
+    // with it on the stream that finishes the pass: the caller's, or the finalize stream, which the
+    // lanes join); the synchronous entry points wait for that event alone and move data on io_stream,
+    // a non-blocking stream of their own.  So reading one context's image does not wait for another
+    // context's passes, nor for unrelated work elsewhere on the GPU.
+    hipStream_t io_stream = nullptr;
+    hipEvent_t ev_done = nullptr;
+    bool done_recorded = false;
 
     ~pt_ctx() {
         for (auto& e : events) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
@@ -3074,6 +3083,8 @@ struct pt_ctx {
             if (ev_fin[h]) (void)hipEventDestroy(ev_fin[h]);
         }
         if (fin_stream) (void)hipStreamDestroy(fin_stream);
+        if (io_stream) (void)hipStreamDestroy(io_stream);
+        if (ev_done) (void)hipEventDestroy(ev_done);
         if (ev_fork) (void)hipEventDestroy(ev_fork);
         for (int l = 0; l < kMaxLanes; ++l) {
             if (ev_join[l]) (void)hipEventDestroy(ev_join[l]);
@@ -3094,6 +3105,26 @@ struct pt_ctx {
 };
 
 namespace {
+
+// Synchronous copy on the context's own non-blocking stream (pt_ctx::io_stream): unlike hipMemcpy,
+// which runs on the legacy default stream, it waits for nothing but itself.
+hipError_t io_copy(pt_ctx* c, void* dst, const void* src, size_t bytes, hipMemcpyKind kind) {
+    if (!c->io_stream) return hipMemcpy(dst, src, bytes, kind);   // (pt_create, before the stream exists)
+    hipError_t e = hipMemcpyAsync(dst, src, bytes, kind, c->io_stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->io_stream);
+    return e;
+}
+
+// Wait for everything this context has enqueued so far (pt_ctx::ev_done).
+int wait_ctx(pt_ctx* c) {
+    if (c->done_recorded) HIP_TRY(hipEventSynchronize(c->ev_done));
+    return PT_OK;
+}
+int mark_ctx(pt_ctx* c, hipStream_t s) {
+    HIP_TRY(hipEventRecord(c->ev_done, s));
+    c->done_recorded = true;
+    return PT_OK;
+}
 
 void set_flags_dev(pt_ctx* c, const pt_flags& f) {
     c->flags = f;
@@ -3396,7 +3427,7 @@ int build_cmask(pt_ctx* c) {
             std::fprintf(stderr, "[pt_amd] camera masks: %zu blocks, %.2f of %d geoms per block\n", nblk, tot / (double)nblk, ng);
         }
     }
-    hipError_t e = hipMemcpy(c->d_cmask, mask.data(), nblk * sizeof(uint32_t), hipMemcpyHostToDevice);
+    hipError_t e = io_copy(c, c->d_cmask, mask.data(), nblk * sizeof(uint32_t), hipMemcpyHostToDevice);
     if (e != hipSuccess) return pt::fail(PT_ERR_HIP, std::string("camera masks: ") + hipGetErrorString(e));
     A.cmask = c->d_cmask;
     size_t empty = 0;
@@ -3797,7 +3828,7 @@ int upload_bound_order(pt_ctx* c) {
     }
     bk[5] = (int32_t)b.size();
     if (b.size() != c->hgeoms.size()) return pt::fail(PT_ERR_ARG, "geom with an unknown bound kind");
-    HIP_TRY(hipMemcpy(c->d_bgeoms, b.data(), b.size() * sizeof(DGeom), hipMemcpyHostToDevice));
+    HIP_TRY(io_copy(c, c->d_bgeoms, b.data(), b.size() * sizeof(DGeom), hipMemcpyHostToDevice));
     c->args.S.bgeoms = c->d_bgeoms;
     for (int k = 0; k < 6; ++k) c->args.S.bk[k] = bk[k];
     return PT_OK;
@@ -4109,6 +4140,9 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
         if (const char* rf = std::getenv("PT_AMD_REFILL")) A.refill_min = std::max(1, std::min(64, std::atoi(rf)));
     }
     if (int rc = c->alloc(&A.image, (size_t)npix * 3)) return bail(rc);
+    if ((e = hipStreamCreateWithFlags(&c->io_stream, hipStreamNonBlocking)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming)) != hipSuccess)
+        return bail(pt::fail(PT_ERR_HIP, std::string("context stream: ") + hipGetErrorString(e)));
     if (sh.spp > 1) {
         if (int rc = c->alloc(&c->colbuf, 2 * (size_t)P)) return bail(rc);
         A.colbuf = c->colbuf;
@@ -4202,8 +4236,12 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
 }
 
 int pt_destroy(pt_ctx* c) {
-    if (c) {
-        (void)hipDeviceSynchronize();
+    if (c) {   // the context's own queued work only (its streams, and the last pass on the caller's)
+        (void)wait_ctx(c);
+        if (c->fin_stream) (void)hipStreamSynchronize(c->fin_stream);
+        for (int l = 1; l < kMaxLanes; ++l)
+            if (c->lane_stream[l]) (void)hipStreamSynchronize(c->lane_stream[l]);
+        if (c->io_stream) (void)hipStreamSynchronize(c->io_stream);
         delete c;
     }
     return PT_OK;
@@ -4224,13 +4262,13 @@ int pt_set_flags(pt_ctx* c, const pt_flags* f) {
     set_flags_dev(c, *f);
     if (!rays) return PT_OK;
     ++c->n_flag_syncs;
+    // (this context's queued passes still read the old bounds and masks; nothing else is waited for)
+    if (int rc = wait_ctx(c)) return rc;
     if (lens) {   // the camera lens bounds the ray origins: re-derive the widened bounds
         update_bounds(c, f->aperture);
-        HIP_TRY(hipDeviceSynchronize());
-        HIP_TRY(hipMemcpy(c->d_geoms, c->hgeoms.data(), c->hgeoms.size() * sizeof(DGeom), hipMemcpyHostToDevice));
+        HIP_TRY(io_copy(c, c->d_geoms, c->hgeoms.data(), c->hgeoms.size() * sizeof(DGeom), hipMemcpyHostToDevice));
         if (int rc = upload_bound_order(c)) return rc;
     }
-    HIP_TRY(hipDeviceSynchronize());   // (queued first bounces still read the old masks)
     return build_cmask(c);   // SSAA / DoF / aperture / focal distance bound the camera rays
 }
 
@@ -4431,13 +4469,17 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
         c->fin_out[h] = true;
         c->last_fin = h;
         c->col_half = h ^ 1;
+        return mark_ctx(c, c->fin_stream);   // (the finalize waited for every lane of the pass)
     }
-    return PT_OK;
+    return mark_ctx(c, st);
 }
 
-// Work on `st` that reads or writes the image first waits for the last deferred finalize.
+// Work on `st` that reads or writes the image first waits for this context's last enqueued work
+// (the last deferred finalize of a batched pass, or an image call on another stream), and is then
+// itself the work the synchronous entry points wait for (mark_ctx).
 static int wait_finalize(pt_ctx* c, hipStream_t st) {
-    if (c->last_fin >= 0) HIP_TRY(hipStreamWaitEvent(st, c->ev_fin[c->last_fin], 0));
+    if (c->done_recorded) HIP_TRY(hipStreamWaitEvent(st, c->ev_done, 0));
+    else if (c->last_fin >= 0) HIP_TRY(hipStreamWaitEvent(st, c->ev_fin[c->last_fin], 0));
     return PT_OK;
 }
 
@@ -4448,7 +4490,7 @@ int pt_preview_rgba(pt_ctx* c, int32_t iter, uint8_t* d_rgba, void* stream) {
     hipLaunchKernelGGL(k_preview, dim3(std::min((npix + 255) / 256, 4096)), dim3(256), 0, (hipStream_t)stream,
                        (const float*)c->args.image, d_rgba, npix, iter);
     HIP_TRY(hipGetLastError());
-    return PT_OK;
+    return mark_ctx(c, (hipStream_t)stream);
 }
 
 int pt_render_iteration(pt_ctx* c, int32_t iter, uint8_t* d_rgba, void* stream) {
@@ -4470,17 +4512,42 @@ int pt_tile_info(const pt_ctx* c, int32_t* width, int32_t* rows, int32_t* npix, 
 
 int pt_get_image(pt_ctx* c, float* host_rgb) {
     if (!c || !host_rgb) return pt::fail(PT_ERR_ARG, "null argument");
-    HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipMemcpy(host_rgb, c->args.image, (size_t)c->args.tile.npix * 3 * sizeof(float), hipMemcpyDeviceToHost));
+    if (int rc = wait_ctx(c)) return rc;   // this context's passes only (pathtrace.cu:524's copy)
+    HIP_TRY(io_copy(c, host_rgb, c->args.image, (size_t)c->args.tile.npix * 3 * sizeof(float), hipMemcpyDeviceToHost));
     return PT_OK;
 }
 
 int pt_get_accum(pt_ctx* c, float* host_rgb) { return pt_get_image(c, host_rgb); }
 
+int pt_host_register(void* host, uint64_t bytes) {
+    if (!host || !bytes) return pt::fail(PT_ERR_ARG, "null argument");
+    HIP_TRY(hipHostRegister(host, (size_t)bytes, hipHostRegisterDefault));
+    return PT_OK;
+}
+
+int pt_host_unregister(void* host) {
+    if (!host) return pt::fail(PT_ERR_ARG, "null argument");
+    HIP_TRY(hipHostUnregister(host));
+    return PT_OK;
+}
+
+int pt_stream_create(void** stream) {
+    if (!stream) return pt::fail(PT_ERR_ARG, "null argument");
+    hipStream_t s = nullptr;
+    HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    *stream = s;
+    return PT_OK;
+}
+
+int pt_stream_destroy(void* stream) {
+    if (stream) HIP_TRY(hipStreamDestroy((hipStream_t)stream));
+    return PT_OK;
+}
+
 int pt_set_accum(pt_ctx* c, const float* host_rgb) {
     if (!c || !host_rgb) return pt::fail(PT_ERR_ARG, "null argument");
-    HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipMemcpy(c->args.image, host_rgb, (size_t)c->args.tile.npix * 3 * sizeof(float), hipMemcpyHostToDevice));
+    if (int rc = wait_ctx(c)) return rc;
+    HIP_TRY(io_copy(c, c->args.image, host_rgb, (size_t)c->args.tile.npix * 3 * sizeof(float), hipMemcpyHostToDevice));
     return PT_OK;
 }
 
@@ -4489,27 +4556,27 @@ int pt_copy_image(pt_ctx* c, float* d_rgb, void* stream) {
     if (int rc = wait_finalize(c, (hipStream_t)stream)) return rc;
     HIP_TRY(hipMemcpyAsync(d_rgb, c->args.image, (size_t)c->args.tile.npix * 3 * sizeof(float),
                            hipMemcpyDeviceToDevice, (hipStream_t)stream));
-    return PT_OK;
+    return mark_ctx(c, (hipStream_t)stream);
 }
 
 int pt_reset_image(pt_ctx* c, void* stream) {
     if (!c) return pt::fail(PT_ERR_ARG, "null context");
     if (int rc = wait_finalize(c, (hipStream_t)stream)) return rc;
     HIP_TRY(hipMemsetAsync(c->args.image, 0, (size_t)c->args.tile.npix * 3 * sizeof(float), (hipStream_t)stream));
-    return PT_OK;
+    return mark_ctx(c, (hipStream_t)stream);
 }
 
 int pt_stats(pt_ctx* c, pt_stats_t* out) {
     if (!c || !out) return pt::fail(PT_ERR_ARG, "null argument");
-    HIP_TRY(hipDeviceSynchronize());
+    if (int rc = wait_ctx(c)) return rc;
     DevStats s;
-    HIP_TRY(hipMemcpy(&s, c->stats, sizeof s, hipMemcpyDeviceToHost));
+    HIP_TRY(io_copy(c, &s, c->stats, sizeof s, hipMemcpyDeviceToHost));
     std::vector<unsigned long long> slots((size_t)64 * c->args.emit_stride);
-    HIP_TRY(hipMemcpy(slots.data(), c->args.emit_slots, slots.size() * sizeof(unsigned long long),
-                      hipMemcpyDeviceToHost));
+    HIP_TRY(io_copy(c, slots.data(), c->args.emit_slots, slots.size() * sizeof(unsigned long long),
+                    hipMemcpyDeviceToHost));
     for (int l = 1; l < c->lanes; ++l) {   // the other lanes' per-workgroup counts
         std::vector<unsigned long long> l1(slots.size());
-        HIP_TRY(hipMemcpy(l1.data(), c->lemit[l], l1.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        HIP_TRY(io_copy(c, l1.data(), c->lemit[l], l1.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
         for (size_t j = 0; j < slots.size(); ++j) slots[j] += l1[j];
     }
     std::memset(out, 0, sizeof *out);

@@ -10,6 +10,11 @@ namespace {
 GuiDataContainer* g_gui = nullptr;
 Scene* g_scene = nullptr;
 pt_ctx* g_ctx = nullptr;
+// The context's passes run on a non-blocking stream of its own, and the host image is page-locked
+// while the context lives: pathtrace()'s per-iteration image copy (pathtrace.cu:524) then waits for
+// this context alone and runs at the link's DMA rate (pt_host_register).
+void* g_stream = nullptr;
+void* g_pinned = nullptr;
 
 // checkCUDAError (utilities / common.cu:3-15 pattern): print and exit.
 void check(int rc, const char* what) {
@@ -81,12 +86,20 @@ void pathtraceInit(Scene* scene) {
     g_scene = scene;
     const pt_flags f = flags_of(g_gui);
     check(pt_create(scene->handle(), &f, nullptr, &g_ctx), "pathtraceInit");
+    check(pt_stream_create(&g_stream), "pathtraceInit stream");
     std::fill(scene->state.image.begin(), scene->state.image.end(), vec3f{0.f, 0.f, 0.f});
+    if (!scene->state.image.empty() &&
+        pt_host_register(scene->state.image.data(), scene->state.image.size() * sizeof(vec3f)) == PT_OK)
+        g_pinned = scene->state.image.data();   // (not page-locked: the copy still works, staged)
 }
 
 void pathtraceFree() {
     if (g_ctx) check(pt_destroy(g_ctx), "pathtraceFree");
     g_ctx = nullptr;
+    if (g_stream) (void)pt_stream_destroy(g_stream);
+    g_stream = nullptr;
+    if (g_pinned) (void)pt_host_unregister(g_pinned);
+    g_pinned = nullptr;
 }
 
 pt_ctx* pathtraceContext() { return g_ctx; }
@@ -99,8 +112,8 @@ void pathtrace(uchar4* pbo, int frame, int iteration) {
     }
     const pt_flags f = flags_of(g_gui);   // the reference re-reads the GUI flags every call
     check(pt_set_flags(g_ctx, &f), "flags");
-    check(pt_render_pass(g_ctx, iteration, nullptr), "pathtrace");
-    if (pbo) check(pt_preview_rgba(g_ctx, iteration, reinterpret_cast<uint8_t*>(pbo), nullptr), "sendImageToPBO");
+    check(pt_render_pass(g_ctx, iteration, g_stream), "pathtrace");
+    if (pbo) check(pt_preview_rgba(g_ctx, iteration, reinterpret_cast<uint8_t*>(pbo), g_stream), "sendImageToPBO");
     if (g_gui) g_gui->TracedDepth = g_scene->state.traceDepth;
     check(pt_get_image(g_ctx, reinterpret_cast<float*>(g_scene->state.image.data())), "image copy");
 }

@@ -275,6 +275,19 @@ int pt_reset_image(pt_ctx* c, void* stream);
  * indices reproduces an uninterrupted render bit for bit. */
 int pt_set_accum(pt_ctx* c, const float* host_rgb);
 int pt_stats(pt_ctx* c, pt_stats_t* out);                   /* synchronises the context stream */
+/* The synchronous calls above (pt_get_image, pt_get_accum, pt_set_accum, pt_stats, and pt_set_flags
+ * when it rebuilds device data) and pt_destroy wait for THIS context's enqueued work only — an event
+ * recorded after its last pass or image call — and move data on a non-blocking stream of the
+ * context's own: another context's passes, or other work on the GPU, are not waited for.
+ *
+ * Drop-in helpers (host/pathtrace.cpp, the pathtrace.h mirror): page-lock a host buffer that
+ * pt_get_image copies into every iteration (the reference's Scene::state.image, pathtrace.cu:524),
+ * so the copy runs at the link's DMA rate; and a non-blocking stream for a context's passes, so they
+ * neither wait for nor hold up the legacy default stream. */
+int pt_host_register(void* host, uint64_t bytes);
+int pt_host_unregister(void* host);
+int pt_stream_create(void** stream);
+int pt_stream_destroy(void* stream);
 /* Per-kernel device timing with hipEvents recorded on the launch stream (for the roofline).  When
  * enabled, pt_render_pass brackets every launch with pooled events; pt_profile_read synchronises
  * and returns, per kernel kind, the summed milliseconds and launch counts since the last read. */

@@ -14,7 +14,7 @@ pytestmark = pytest.mark.gpu
 ROOT = Path(__file__).resolve().parent.parent
 
 
-@pytest.mark.parametrize("size_log2", [12, 20, 24])
+@pytest.mark.parametrize("size_log2", [12, 20, 24, 28])   # 28: SIZE = 1 << 28 (stream_compaction/src/main.cpp:8)
 def test_reference_shaped_stream_compaction_selftest(size_log2):
     exe = ROOT / "tests" / "cpp" / "build" / "test_stream_compaction"
     res = subprocess.run([str(exe), str(size_log2)], capture_output=True, text=True, timeout=300)

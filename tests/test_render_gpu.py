@@ -675,9 +675,10 @@ def test_resume_from_checkpoint_is_bitexact(cornell_path, tmp_path):
 
 
 def test_full_size_cornell_batched_equals_sequential(cornell_path):
-    """BASELINE configs[1] at full size (800x800, DEPTH 8): the bench's 16-iteration pass equals 16
-    one-iteration passes bit for bit, and the live-path counts agree (size-independent check
-    of the per-iteration keys, segment layout and buffer capacity at the benchmarked size)."""
+    """BASELINE configs[1] at full size (800x800, DEPTH 8): a 16-iteration pass equals 16
+    one-iteration passes bit for bit, and the live-path counts agree (per-iteration keys and the
+    segment layout against the reference's one-iteration pathtrace() calls; the bench's own pass of
+    256 iterations is checked against two of 128 in test_benched_pass_size_equals_two_half_passes)."""
     from cuda_pathtracer_amd import PathTracer, Scene
     s = Scene(cornell_path)
     pb = PathTracer(s, _gui(), spp=16)
@@ -990,27 +991,36 @@ def test_config5_full_size_bitexact(tmp_path):
     assert st["bounce_live"] == live and live[0] == 3840 * 2160 and r.sum() > 0
 
 
-@pytest.mark.parametrize("config", ["multi_object_4k", "random_triangles_100k"])
-def test_benched_pass_size_equals_two_half_passes(tmp_path, config):
-    """Configs 4 and 5 at the pass size bench.py runs them: one pass of 128 iterations at 3840x2160
-    (1.06 G paths; ~120 GB of path state, walk records and colours for config 5) against two passes
-    of 64 — a size-independent property (batched passes equal sequential ones): the
-    same image bit for bit, the same live-path and emission counts per bounce, no device error."""
+@pytest.mark.parametrize("config,spp,res,sort", [
+    ("multi_object_4k", 128, (3840, 2160), False),
+    ("random_triangles_100k", 128, (3840, 2160), False),
+    ("cornell_hd_sorted", 256, (1920, 1080), True),
+    ("cornell", 256, (800, 800), False),
+])
+def test_benched_pass_size_equals_two_half_passes(tmp_path, cornell_path, config, spp, res, sort):
+    """Every BASELINE workload at the pass size bench.py runs it — configs 4 and 5: one pass of 128
+    iterations at 3840x2160 (1.06 G paths; ~120 GB of path state, walk records and colours for config
+    5); config 3: one pass of 256 iterations at 1920x1080, DEPTH 16, material-sorted, over the default
+    three lanes (530.8 M paths: the sorted pipeline's largest record, histogram, work-list and byte
+    offsets); the headline Cornell 800x800: one pass of 256 (163.8 M paths) — against two passes of
+    half the size.  A size-independent property (batched passes equal sequential ones, DESIGN.md §3;
+    pathtrace.cu:423-528): the same image bit for bit, the same live-path and emission counts per
+    bounce, no device error."""
     from cuda_pathtracer_amd import PathTracer, Scene, scenes
-    path = scenes.CONFIGS[config](tmp_path)
+    path = cornell_path if scenes.CONFIGS[config] is None else scenes.CONFIGS[config](tmp_path)
     scene = Scene(path)
     out = []
-    for spp, passes in ((128, 1), (64, 2)):
-        pt = PathTracer(scene, _gui(), spp=spp)
+    for n, passes in ((spp, 1), (spp // 2, 2)):
+        pt = PathTracer(scene, _gui(sortbyMaterial=sort), spp=n)
         it = 1
         for _ in range(passes):
             pt.render_pass(it)
-            it += spp
+            it += n
         st = pt.stats()
-        assert st["device_error"] == 0 and st["bounce_live"][0] == 128 * 3840 * 2160
+        assert st["device_error"] == 0 and st["bounce_live"][0] == spp * res[0] * res[1]
         out.append((pt.image(), st["bounce_live"], st["bounce_emit"]))
         pt.free()
-    _assert_bitexact(out[0][0], out[1][0], f"{config}: one pass of 128 vs two of 64")
+    _assert_bitexact(out[0][0], out[1][0], f"{config}: one pass of {spp} vs two of {spp // 2}")
     assert out[0][1:] == out[1][1:]
     assert np.isfinite(out[0][0]).all() and out[0][0].sum() > 0
 
@@ -1036,3 +1046,48 @@ def test_sorted_paths_that_all_end_early(cornell_path, spp, look):
         assert live[0] == 3 * 48 * 32 and sum(live[1:]) == 0 and r.sum() == 0
     else:
         assert r.sum() > 0 and live[1] < live[0]
+
+
+def test_context_synchronisation_is_scoped(cornell_path):
+    """pt_get_image / pt_stats wait for their own context only (an event after its last pass, copies
+    on a non-blocking stream of its own), not for the device: with long batched passes of another
+    context queued, a small context's image and statistics are read while those passes are still
+    running (checked with an event queued after them), and both images stay bit-exact.
+    The streams in use are kept to the box's 4 hardware queues per process (GPU_MAX_HW_QUEUES: HIP
+    maps further streams onto shared queues, whose work then runs in submission order): the big
+    context's passes on the legacy default stream, its finalize stream, and the two contexts' copy
+    streams."""
+    import time
+    import torch
+    from cuda_pathtracer_amd import PathTracer, Scene
+    s, o = _pair(cornell_path, (32, 24))
+    small = PathTracer(s, _gui())
+    small.render_pass(1)
+    ref, _ = O.render_pass(o, _oflags(_gui()), 1)
+    _assert_bitexact(small.image(), ref, "small context, first read")
+    import os
+    os.environ["PT_AMD_LANES"] = "1"
+    try:
+        big = PathTracer(Scene(cornell_path), _gui(), spp=64)
+    finally:
+        os.environ.pop("PT_AMD_LANES", None)
+    big.render_pass(1)                    # warm-up pass (first launches, code objects)
+    big.stats()
+    ev = torch.cuda.Event()
+    t0 = time.perf_counter()
+    for k in range(1, 9):                 # 8 x 64 iterations of 800x800: tens of ms of GPU work
+        big.render_pass(1 + 64 * k)
+    ev.record()
+    img = small.image()
+    st = small.stats()
+    t_small = time.perf_counter() - t0
+    running = not ev.query()
+    torch.cuda.synchronize()
+    t_big = time.perf_counter() - t0
+    _assert_bitexact(img, ref, "small context read during the other context's passes")
+    assert st["bounce_live"][0] == 32 * 24 and st["device_error"] == 0
+    assert running, f"the small context's reads waited for the other context ({t_small * 1e3:.2f} of {t_big * 1e3:.2f} ms)"
+    bst = big.stats()
+    assert bst["device_error"] == 0 and bst["bounce_live"][0] == 9 * 64 * 800 * 800
+    big.free()
+    small.free()

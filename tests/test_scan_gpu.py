@@ -180,7 +180,8 @@ def test_large_inputs_match_oracle(gpu_device, n):
 
 @pytest.mark.slow
 def test_reference_size_2e28_properties(gpu_device):
-    """SIZE = 1<<28 and NPOT = SIZE-3 (main.cpp:8-9): size-independent checks on the device."""
+    """SIZE = 1<<28 and NPOT = SIZE-3 (main.cpp:8-9): the whole scan against the oracle, plus the
+    size-independent checks on the device (difference identity, compaction count and order)."""
     import torch
     from cuda_pathtracer_amd import compact_device, scan_device
     for n in ((1 << 28), (1 << 28) - 3):
@@ -192,10 +193,10 @@ def test_reference_size_2e28_properties(gpu_device):
         assert int(s[0].item()) == 0
         diff = (s[1:] - s[:-1])
         assert bool(torch.equal(diff, a[:-1]))
-        # spot-check against the oracle on a prefix and a window
-        head = a[:100000].cpu().numpy()
-        np.testing.assert_array_equal(s[:100000].cpu().numpy(), O.scan(head))
-        del s, diff
+        # the whole array against the oracle (O.scan: ~0.1 s on the host at 2^28)
+        ah = a.cpu().numpy()
+        np.testing.assert_array_equal(s.cpu().numpy(), O.scan(ah))
+        del s, diff, ah
         f = (a % 4).to(torch.int32)
         out, cnt = compact_device(f)
         nz = int((f != 0).sum().item())
