@@ -752,6 +752,9 @@ __device__ __forceinline__ float exact_geom(const LGeom& L, f3 r_o, f3 r_d, int&
 // camera-ray masks, pt_ctx::cmask) and are skipped; a geom no ray can hit is never a candidate
 // whose absence changes the result (every geom that can be hit is still bounded and tested).
 __device__ __forceinline__ uint32_t ng_all_mask(int n) { return n >= 32 ? ~0u : (1u << n) - 1u; }
+#if defined(PT_DUP)
+__device__ uint32_t g_dup_sink;
+#endif
 template <bool SEL, bool PRE = false>
 __device__ __forceinline__ Hit intersect_bounded(const SceneDev& S, const FlagsDev& fl, const LGeom* s_geoms, f3 ro,
                                                  f3 rd, const MeshHit* mh = nullptr, uint32_t gmask = ~0u) {
@@ -809,6 +812,42 @@ __device__ __forceinline__ Hit intersect_bounded(const SceneDev& S, const FlagsD
             if ((gmask >> B[j].orig) & 1u) insert(bound_geom<1, SEL>(B[j], ro, rd, invd, rl, rinf), B[j].orig);
         for (int j = S.bk[2]; j < S.bk[3]; ++j)
             if ((gmask >> B[j].orig) & 1u) insert(bound_geom<2, SEL>(B[j], ro, rd, invd, rl, rinf), B[j].orig);
+#if defined(PT_DUP) && PT_DUP == 4   // diagnostic: the bounds pass again on an opaque origin
+        if (SEL) {
+            f3 r2 = ro;
+            asm volatile("" : "+v"(r2.x), "+v"(r2.y), "+v"(r2.z));
+            float m1 = kInf, m2 = kInf, m3 = kInf;
+            int h1 = -1;
+            auto ins2 = [&](float lo, int i) {
+                lo -= S.abs_slack;
+                const bool c1 = lo < m1, c2 = lo < m2, c3 = lo < m3;
+                m3 = c2 ? m2 : (c3 ? lo : m3);
+                m2 = c1 ? m1 : (c2 ? lo : m2);
+                m1 = c1 ? lo : m1;
+                h1 = c1 ? i : h1;
+            };
+            for (int j = S.bk[3]; j < S.bk[4]; ++j)
+                if ((gmask >> B[j].orig) & 1u) ins2(bound_geom<3, SEL>(B[j], r2, rd, invd, rl, rinf), B[j].orig);
+            for (int j = S.bk[4]; j < S.bk[5]; ++j)
+                if ((gmask >> B[j].orig) & 1u) ins2(bound_geom<4, SEL>(B[j], r2, rd, invd, rl, rinf), B[j].orig);
+            for (int j = S.bk[1]; j < S.bk[2]; ++j)
+                if ((gmask >> B[j].orig) & 1u) ins2(bound_geom<1, SEL>(B[j], r2, rd, invd, rl, rinf), B[j].orig);
+            for (int j = S.bk[2]; j < S.bk[3]; ++j)
+                if ((gmask >> B[j].orig) & 1u) ins2(bound_geom<2, SEL>(B[j], r2, rd, invd, rl, rinf), B[j].orig);
+            if (__float_as_uint(m1 + m2 + m3) == 0x7f7ffffeu || h1 == 12345) atomicAdd(&g_dup_sink, 1u);
+        }
+#endif
+#if defined(PT_DUP) && PT_DUP == 5   // diagnostic: the first candidate's exact test again
+        if (SEL && g1 >= 0) {
+            f3 r2 = ro;
+            asm volatile("" : "+v"(r2.x), "+v"(r2.y), "+v"(r2.z));
+            int code2;
+            f3 obj2 = F3(0, 0, 0);
+            bool out2;
+            const float t2 = exact_geom(s_geoms[g1], r2, rd, code2, obj2, out2);
+            if (__float_as_uint(t2) == 0x7f7ffffeu) atomicAdd(&g_dup_sink, 1u);
+        }
+#endif
         // pass 2: exact tests in increasing-bound order while a bound does not exceed the best hit
         auto take = [&](int gi) {
             int code;
@@ -2242,6 +2281,33 @@ __global__ __launch_bounds__(kBlock, FIRST || MESH ? 1 : PT_LATER_WAVES) void k_
             // every path entering bounce b has b bounces behind it: a wave-uniform value, so the
             // shading RNG's (iteration, remaining depth) hash is computed once per wave on the SALU
             p.bounces = A.bounce;
+#if defined(PT_DUP)   // diagnostic builds (scripts/valu_phases.sh): a phase run twice on opaque copies of
+            // its inputs, so SQ_INSTS_VALU's increase is that phase's dynamic cost (divergence included)
+            if (!FIRST && MESH == 0) {
+                f3 o2 = p.o;
+                asm volatile("" : "+v"(o2.x), "+v"(o2.y), "+v"(o2.z));
+                if (PT_DUP == 1) {
+                    const Hit h2 = closest_hit<false, false, true>(A.S, A.fl, s_geoms, o2, p.d, &A.stats->bound_mismatch, ~0u);
+                    if (__float_as_uint(h2.t) == 0x7f7ffffeu) atomicAdd(&A.stats->bound_mismatch, 7u);
+                } else if (PT_DUP == 2) {
+                    PathReg p2 = p;
+                    p2.o = o2;
+                    Hit hh = h;
+                    int key2 = key;
+                    asm volatile("" : "+v"(p2.d.x), "+v"(p2.d.y), "+v"(p2.d.z), "+v"(key2));
+                    asm volatile("" : "+v"(hh.n.x), "+v"(hh.n.y), "+v"(hh.n.z), "+v"(hh.t), "+v"(hh.mat), "+v"(hh.frame));
+                    const bool a2 = lds_mats ? shade(A.S, A.fl, A.tile.depth, iter, key2, p2, hh, s_mats, frames)
+                                             : shade(A.S, A.fl, A.tile.depth, iter, key2, p2, hh, A.S.mats, frames);
+                    if (a2 && __float_as_uint(p2.c.x) == 0x7f7ffffeu) atomicAdd(&A.stats->bound_mismatch, 7u);
+                } else if (PT_DUP == 3) {
+                    PathReg p2;
+                    int q2 = q;
+                    asm volatile("" : "+v"(q2));
+                    load_path(A.in, q2, A.bounce, p2);
+                    if (__float_as_uint(p2.o.x) == 0x7f7ffffeu) atomicAdd(&A.stats->bound_mismatch, 7u);
+                }
+            }
+#endif
             alive = lds_mats ? shade(A.S, A.fl, A.tile.depth, iter, key, p, h, s_mats, frames)
                              : shade(A.S, A.fl, A.tile.depth, iter, key, p, h, A.S.mats, frames);
             if (!alive) {
