@@ -294,8 +294,8 @@ def _pmc_leg(args, scene_path, spp_pass, sorted_, avg_ms, kernel_prefix, seg_per
             "aggregate_frac": valu * launches / (busy_ms * 1e-3) / VALU_PEAK if busy_ms > 0 else None,
             "salu_per_launch": m.get("SQ_INSTS_SALU"),
             "effective_clock_ghz": m["GRBM_GUI_ACTIVE"] / 8.0 / dur if dur > 0 and "GRBM_GUI_ACTIVE" in m else None,
-            "definition": "SQ_INSTS_VALU per launch / HIP-event average launch duration / (256 CUs x 4 SIMDs x "
-                          "2.4 GHz / 2 cycles per wave64 VALU instruction)"}
+            "definition": "SQ_INSTS_VALU per launch / the kernel's time per launch (roofline.effective_launch_ms) "
+                          "/ (256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU instruction)"}
         out["wave_states"] = {"issuing": act, "waiting_on_issue": wi, "waiting_on_memory_or_barrier": wa,
                               "waves_per_launch": m.get("SQ_WAVES")}
         out["limiter"] = (f"VALU issue + latency, not bandwidth: waves issue {act:.0%} of their cycles, wait on "
@@ -539,7 +539,13 @@ def main() -> None:
     k_ms, k_n, k_busy = (t_ms, t_n, t_busy) if walk else (b_ms, b_n, b_busy)
     per_launch_bytes = SEGMENT_BYTES * seg_bounce / max(k_n, 1)
     avg_ms = k_ms / max(k_n, 1)
-    achieved = per_launch_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    # The lanes' launches overlap (two streams), so a launch's own duration is shared with the other
+    # lane's work: launches x avg_ms exceeds the step.  The kernel's time per launch that fits the
+    # step is the union of its launch intervals / launches (launches x eff_ms = union <= the step):
+    # that is the roofline's duration; the HIP-event average (= rocprofv3's) is reported beside it.
+    eff_ms = k_busy / max(k_n, 1) if k_busy > 0 else avg_ms
+    achieved = per_launch_bytes / (eff_ms * 1e-3) / 1e9 if eff_ms > 0 else 0.0
+    achieved_overlapped = per_launch_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     # pt_kernels.hip pt_create: 3 lanes for large sorted passes (kThreeLanePaths), 1 with the BVH walk
     default_lanes = 3 if sorted_ and pt.npaths >= (48 << 20) else (1 if quads else 2)
     lanes = min(int(os.environ.get("PT_AMD_LANES", str(default_lanes))), spp, 4) \
@@ -548,10 +554,21 @@ def main() -> None:
     # byte metric at step level (near 1.0 it is saturated and stops being evidence; VALU issue is
     # the limiter then, roofline.valu_issue)
     step_seg = seg / max(args.steps, 1)
+    prof_steps = prof_passes / max(passes_per_step, 1)
     roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                "definition": "184 B (SURVEY.md §8d) x segments per launch / HIP-event average launch duration",
-                "kernel": kernel_name, "avg_launch_ms": avg_ms, "launches": k_n, "lanes": lanes,
+                "definition": "184 B (SURVEY.md §8d) x segments per launch / the kernel's time per launch "
+                              "(union of its launch intervals over the profiled passes / launches, HIP events "
+                              "on the launch streams: launches x that time fits the step)",
+                "kernel": kernel_name, "effective_launch_ms": eff_ms, "avg_launch_ms": avg_ms, "launches": k_n,
+                "lanes": lanes,
+                "launches_per_step": k_n / max(prof_steps, 1e-9),
+                "kernel_ms_per_step": k_busy / max(prof_steps, 1e-9),
+                "overlapped": {"avg_launch_ms": avg_ms, "achieved": achieved_overlapped,
+                               "frac": achieved_overlapped / HBM_PEAK_GBS,
+                               "definition": "the same bytes / the HIP-event average launch duration (= rocprofv3 "
+                                             "--kernel-trace --stats' average; each launch shares the GPU with the "
+                                             "other lane's, so launches x this exceeds the step)"},
                 "segments_per_launch": seg_bounce / max(k_n, 1),
                 "algorithmic_bytes_per_launch": per_launch_bytes,
                 "step_frac": SEGMENT_BYTES * step_seg / (elapsed / max(args.steps, 1)) / 1e9 / HBM_PEAK_GBS
@@ -582,6 +599,10 @@ def main() -> None:
         if rows_all is not None:
             full = D.assemble([t.cpu().numpy() for t in rows_all], scene.camera().res[1], world)
             assert np.isfinite(full).all()
+        if world > 1:   # the N-GPU line's parts (the driver's scaling run): every rank's segments, the gather
+            assert gather_ms is not None and gather_ms_min is not None, "N > 1: the tile gather was not timed"
+            assert seg_all >= seg > 0 and rows_all is not None and len(rows_all) == world, \
+                "N > 1: per-rank segment sums or gathered tiles missing"
         value = seg_all / t_max / 1e6
         strong = args.scaling == "strong"
         desc = (f"cornell.json 800x800 DEPTH 8 default flags; a step = {args.samples} samples per pixel of the whole "
@@ -647,7 +668,7 @@ def main() -> None:
             result["dropin"] = {"error": repr(e)}
     if rank == 0 and world == 1 and not args.no_pmc:
         try:
-            extra = _pmc_leg(args, scene_path, spp, sorted_, avg_ms, kprefix, seg_bounce / max(k_n, 1), k_busy, k_n,
+            extra = _pmc_leg(args, scene_path, spp, sorted_, eff_ms, kprefix, seg_bounce / max(k_n, 1), k_busy, k_n,
                              walk=walk)
         except Exception as e:   # profiling is evidence, not the measurement: never fail the bench line
             extra = {"pmc_error": repr(e)}

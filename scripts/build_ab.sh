@@ -9,5 +9,5 @@ cp $R/cuda_pathtracer_amd/csrc/*.h $B/ab/
 /opt/rocm/bin/hipcc -x hip --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-slp-vectorize -I $R/include -I $R/cuda_pathtracer_amd/csrc \
     -c $B/ab/pt_kernels.hip -o $B/ab/pt_kernels.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $B/libpt_amd_ab.so $B/ab/pt_kernels.o \
-    $B/sc_kernels.hip.o $B/bvh_build.hip.o $B/pt_scene.cpp.o $B/pt_mesh.cpp.o $B/pt_image.cpp.o $B/pt_jpeg.cpp.o -lz
+    $B/sc_kernels.hip.o $B/sc_variants.hip.o $B/bvh_build.hip.o $B/pt_scene.cpp.o $B/pt_mesh.cpp.o $B/pt_image.cpp.o $B/pt_jpeg.cpp.o -lz
 echo $B/libpt_amd_ab.so

@@ -46,7 +46,9 @@ def _worker(rank, world, port, out_dir):
         for it in (1, 2):   # two passes accumulate into the tile
             tile, _ = O.render_pass(sc, fl, iter_first=it, rank=rank, world=world, image=tile)
         assert tile.shape == (D.shard_rows(H, rank, world), W, 3)
-        img = D.gather_image(torch, dist, torch.from_numpy(tile), H)
+        # bench.py's own calls: one gather_tiles of the rank's tile, then assemble on rank 0
+        tiles = D.gather_tiles(torch, dist, torch.from_numpy(tile), H)
+        img = D.assemble([t.cpu().numpy() for t in tiles], H, world) if tiles is not None else None
         t = D.max_over_ranks(torch, dist, 1.0 + rank, torch.device("cpu"))
         n = D.sum_over_ranks(torch, dist, 10 * (rank + 1), torch.device("cpu"))
         if rank == 0:
