@@ -1406,6 +1406,14 @@ constexpr int kFoldBatch = PT_FOLD_BATCH;   // k_traverse4: task results read pe
 #ifndef PT_T4_ASSIGN
 #define PT_T4_ASSIGN 0   // k_traverse4 leaf tasks: 0 owner tag + ballot + ds_bpermute; 1 task slots written by owners
 #endif
+#ifndef PT_T4_TASKS
+#define PT_T4_TASKS 2    // k_traverse4 leaf tasks: K consecutive triangles of one leaf per lane per trip
+#endif                   // (a leaf's remaining count rounded up to a multiple of K: 64 K triangle tests per trip)
+// Measured (config 5, 64 iterations per pass, same box, two alternations; profiles/r05_walk_ab.txt):
+// K = 1 / 2 / 3 / 4: 822 / 929 / 793 / 723 Mray/s.  K = 2 halves the trips the triangle tasks need
+// (112 per ray at 64 per trip: they, not the 56 interior steps, bounded a ray's trips) at 122 VGPRs,
+// still 4 waves per SIMD; K = 3 and 4 take 132 / 141 VGPRs and drop to 3 waves.
+constexpr int kT4K = PT_T4_TASKS;
 #ifndef PT_T4_COOP
 #define PT_T4_COOP 0     // k_traverse4 quad fetch: 0 each interior lane loads its own 112 B (7 loads);
                          // 1 the wave loads the quads cooperatively, 8 lanes per 128-B row, register-
@@ -1687,6 +1695,8 @@ __global__ __launch_bounds__(kBlock, PT_T4_WAVES) void k_traverse4(const KArgs A
     // then overwritten by the task's result (t or NaN = no hit, bx, by, -)
 #if PT_T4_ASSIGN == 1
     __shared__ v4f s_task[2 * kBlock];
+#elif PT_T4_TASKS > 1
+    __shared__ v4f s_task[kT4K * kBlock];   // kT4K task results per lane
 #else
     __shared__ v4f s_task[kBlock];      // task results only (index 2j + 1 -> j below)
 #endif
@@ -1738,6 +1748,9 @@ __global__ __launch_bounds__(kBlock, PT_T4_WAVES) void k_traverse4(const KArgs A
 #if PT_T4_ASSIGN == 1
     v4f* task = s_task + wave * 128;
 #define PT_RES(j) task[2 * (j) + 1]
+#elif PT_T4_TASKS > 1
+    v4f* task = s_task + wave * (64 * kT4K);
+#define PT_RES(j) task[(j)]
 #else
     v4f* task = s_task + wave * 64;
 #define PT_RES(j) task[(j)]
@@ -1847,10 +1860,20 @@ __global__ __launch_bounds__(kBlock, PT_T4_WAVES) void k_traverse4(const KArgs A
         };
         // ---- leaf tasks: the remaining triangles of the leaf lanes, one per lane of the wave ----
         const int cnt = (have && leaf) ? te - ti : 0;
+#if PT_T4_TASKS > 1
+        // task slots come in groups of kT4K consecutive triangles of one leaf (one lane tests the
+        // group): counted in group units
+        const int pcnt = (cnt + kT4K - 1) / kT4K;
+        const int incl = (int)lb::wave_inclusive_scan((uint32_t)pcnt);
+        const int pre = incl - pcnt;   // first group of this lane's leaf
+        const int T = __builtin_amdgcn_readlane(incl, 63);
+        const int cov = (pcnt > 0 && pre < 64) ? min(cnt, kT4K * (64 - pre)) : 0;   // triangles covered this trip
+#else
         const int incl = (int)lb::wave_inclusive_scan((uint32_t)cnt);
         const int pre = incl - cnt;
         const int T = __builtin_amdgcn_readlane(incl, 63);
         const int cov = (cnt > 0 && pre < 64) ? min(cnt, 64 - pre) : 0;   // this trip's tasks of this lane
+#endif
         const bool is_task = lane < T;
         bool inner = have && !leaf;
 #if PT_T4_OVERLAP
@@ -1920,6 +1943,7 @@ __global__ __launch_bounds__(kBlock, PT_T4_WAVES) void k_traverse4(const KArgs A
         if (S.qcull && inner) cw = *reinterpret_cast<const v4u*>(S.qcull + 4 * (size_t)(cur & kQuadIdxMask));
         f3 to = F3(0, 0, 0), td = F3(0, 0, 0);
         int tidx = 0;
+        int ntask = 1;   // (PT_T4_TASKS > 1) triangles tidx .. tidx + ntask - 1 of this task lane
         if (T > 0) {   // (wave-uniform)
 #if PT_T4_ASSIGN == 1   // owners write (ray, triangle index) into each of their task slots
             for (int k = 0; k < cov; ++k) {
@@ -1947,7 +1971,12 @@ __global__ __launch_bounds__(kBlock, PT_T4_WAVES) void k_traverse4(const KArgs A
             const uint64_t le = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
             const int pos = is_task ? 63 - (int)__clzll(heads & le) : lane;   // the owner's first task
             const int ow = __shfl(v, pos) & 63;
+#if PT_T4_TASKS > 1
+            tidx = __shfl(ti, ow) + kT4K * (lane - pos);
+            ntask = min(kT4K, __shfl(te, ow) - tidx);   // (the leaf's triangles left in this group)
+#else
             tidx = __shfl(ti, ow) + (lane - pos);
+#endif
             to = F3(__shfl(o.x, ow), __shfl(o.y, ow), __shfl(o.z, ow));
             td = F3(__shfl(d.x, ow), __shfl(d.y, ow), __shfl(d.z, ow));
 #endif
@@ -1956,6 +1985,9 @@ __global__ __launch_bounds__(kBlock, PT_T4_WAVES) void k_traverse4(const KArgs A
 #endif
         }
         v4f t0, t1, t2;
+#if PT_T4_TASKS > 1
+        v4f u[kT4K - 1][3];   // the group's further triangles
+#endif
 #ifndef PT_T4_TRI_PACK
 #define PT_T4_TRI_PACK 1
 #endif
@@ -1967,6 +1999,18 @@ __global__ __launch_bounds__(kBlock, PT_T4_WAVES) void k_traverse4(const KArgs A
             const v3f a = *reinterpret_cast<const v3f*>(p), b = *reinterpret_cast<const v3f*>(p + 3),
                       c = *reinterpret_cast<const v3f*>(p + 6);
             t0 = v4f{a[0], a[1], a[2], 0.f}; t1 = v4f{b[0], b[1], b[2], 0.f}; t2 = v4f{c[0], c[1], c[2], 0.f};
+#if PT_T4_TASKS > 1
+#pragma unroll
+            for (int j = 1; j < kT4K; ++j)
+                if (j < ntask) {
+                    const float* pj = p + 9 * j;
+                    const v3f a2 = *reinterpret_cast<const v3f*>(pj), b2 = *reinterpret_cast<const v3f*>(pj + 3),
+                              c2 = *reinterpret_cast<const v3f*>(pj + 6);
+                    u[j - 1][0] = v4f{a2[0], a2[1], a2[2], 0.f};
+                    u[j - 1][1] = v4f{b2[0], b2[1], b2[2], 0.f};
+                    u[j - 1][2] = v4f{c2[0], c2[1], c2[2], 0.f};
+                }
+#endif
 #else
             const v4f* tsrc = reinterpret_cast<const v4f*>(S.tris + tidx);   // (non-task lanes: triangle 0)
             t0 = tsrc[0]; t1 = tsrc[1]; t2 = tsrc[2];
@@ -2068,7 +2112,18 @@ __global__ __launch_bounds__(kBlock, PT_T4_WAVES) void k_traverse4(const KArgs A
 #endif
             float bx = 0.f, by = 0.f, bz = 0.f;
             const bool h = ray_tri(DTri{t0, t1, t2}, to, td, bx, by, bz);
+#if PT_T4_TASKS > 1
+            PT_RES(kT4K * lane) = v4f{h ? bz : __builtin_nanf(""), bx, by, 0.f};
+#pragma unroll
+            for (int j = 1; j < kT4K; ++j)
+                if (j < ntask) {
+                    float cx = 0.f, cy = 0.f, cz = 0.f;
+                    const bool h2 = ray_tri(DTri{u[j - 1][0], u[j - 1][1], u[j - 1][2]}, to, td, cx, cy, cz);
+                    PT_RES(kT4K * lane + j) = v4f{h2 ? cz : __builtin_nanf(""), cx, cy, 0.f};
+                }
+#else
             PT_RES(lane) = v4f{h ? bz : __builtin_nanf(""), bx, by, 0.f};
+#endif
         }
         if (T > 0) {
             wave_sync();   // the task results
@@ -2077,7 +2132,7 @@ __global__ __launch_bounds__(kBlock, PT_T4_WAVES) void k_traverse4(const KArgs A
                     v4f x[kFoldBatch];
 #pragma unroll
                     for (int k = 0; k < kFoldBatch; ++k)
-                        if (k0 + k < cov) x[k] = PT_RES(pre + k0 + k);
+                        if (k0 + k < cov) x[k] = PT_RES(kT4K * pre + k0 + k);
 #pragma unroll
                     for (int k = 0; k < kFoldBatch; ++k)
                         if (k0 + k < cov) fold(x[k], ti + k0 + k);
