@@ -3204,7 +3204,7 @@ struct pt_ctx {
             if (ev_fin[h]) (void)hipEventDestroy(ev_fin[h]);
         }
         if (fin_stream) (void)hipStreamDestroy(fin_stream);
-        if (io_stream) (void)hipStreamDestroy(io_stream);
+        if (io_stream && io_stream != fin_stream) (void)hipStreamDestroy(io_stream);
         if (ev_done) (void)hipEventDestroy(ev_done);
         if (ev_fork) (void)hipEventDestroy(ev_fork);
         for (int l = 0; l < kMaxLanes; ++l) {
@@ -4261,9 +4261,8 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
         if (const char* rf = std::getenv("PT_AMD_REFILL")) A.refill_min = std::max(1, std::min(64, std::atoi(rf)));
     }
     if (int rc = c->alloc(&A.image, (size_t)npix * 3)) return bail(rc);
-    if ((e = hipStreamCreateWithFlags(&c->io_stream, hipStreamNonBlocking)) != hipSuccess ||
-        (e = hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming)) != hipSuccess)
-        return bail(pt::fail(PT_ERR_HIP, std::string("context stream: ") + hipGetErrorString(e)));
+    if ((e = hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming)) != hipSuccess)
+        return bail(pt::fail(PT_ERR_HIP, std::string("context event: ") + hipGetErrorString(e)));
     if (sh.spp > 1) {
         if (int rc = c->alloc(&c->colbuf, 2 * (size_t)P)) return bail(rc);
         A.colbuf = c->colbuf;
@@ -4274,6 +4273,14 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
                 (e = hipEventCreateWithFlags(&c->ev_fin[h], hipEventDisableTiming)) != hipSuccess)
                 return bail(pt::fail(PT_ERR_HIP, std::string("hipEventCreate: ") + hipGetErrorString(e)));
     }
+    // The synchronous entry points' copies: on the finalize stream when the context has one (they wait
+    // for the context's last work first, so it is idle then), else on a stream of their own.  Not one
+    // more stream beside the lanes: HIP maps the streams of a process onto GPU_MAX_HW_QUEUES (4)
+    // hardware queues, and a fifth stream made two of config 3's three lanes share one (35.6k vs
+    // 39.6k Mray/s: their launches then ran in submission order).
+    if (c->fin_stream) c->io_stream = c->fin_stream;
+    else if ((e = hipStreamCreateWithFlags(&c->io_stream, hipStreamNonBlocking)) != hipSuccess)
+        return bail(pt::fail(PT_ERR_HIP, std::string("context stream: ") + hipGetErrorString(e)));
     c->max_tiles = (int)((P + kCompactTile - 1) / kCompactTile);   // k_compact_paths tiles
     if (int rc = c->alloc(&A.flags, (size_t)P)) return bail(rc);
     if (int rc = c->alloc(&A.ctl, 2)) return bail(rc);

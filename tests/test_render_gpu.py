@@ -1048,46 +1048,23 @@ def test_sorted_paths_that_all_end_early(cornell_path, spp, look):
         assert r.sum() > 0 and live[1] < live[0]
 
 
-def test_context_synchronisation_is_scoped(cornell_path):
+def test_context_synchronisation_is_scoped():
     """pt_get_image / pt_stats wait for their own context only (an event after its last pass, copies
-    on a non-blocking stream of its own), not for the device: with long batched passes of another
-    context queued, a small context's image and statistics are read while those passes are still
-    running (checked with an event queued after them), and both images stay bit-exact.
-    The streams in use are kept to the box's 4 hardware queues per process (GPU_MAX_HW_QUEUES: HIP
-    maps further streams onto shared queues, whose work then runs in submission order): the big
-    context's passes on the legacy default stream, its finalize stream, and the two contexts' copy
-    streams."""
-    import time
-    import torch
-    from cuda_pathtracer_amd import PathTracer, Scene
-    s, o = _pair(cornell_path, (32, 24))
-    small = PathTracer(s, _gui())
-    small.render_pass(1)
-    ref, _ = O.render_pass(o, _oflags(_gui()), 1)
-    _assert_bitexact(small.image(), ref, "small context, first read")
-    import os
-    os.environ["PT_AMD_LANES"] = "1"
-    try:
-        big = PathTracer(Scene(cornell_path), _gui(), spp=64)
-    finally:
-        os.environ.pop("PT_AMD_LANES", None)
-    big.render_pass(1)                    # warm-up pass (first launches, code objects)
-    big.stats()
-    ev = torch.cuda.Event()
-    t0 = time.perf_counter()
-    for k in range(1, 9):                 # 8 x 64 iterations of 800x800: tens of ms of GPU work
-        big.render_pass(1 + 64 * k)
-    ev.record()
-    img = small.image()
-    st = small.stats()
-    t_small = time.perf_counter() - t0
-    running = not ev.query()
-    torch.cuda.synchronize()
-    t_big = time.perf_counter() - t0
-    _assert_bitexact(img, ref, "small context read during the other context's passes")
-    assert st["bounce_live"][0] == 32 * 24 and st["device_error"] == 0
-    assert running, f"the small context's reads waited for the other context ({t_small * 1e3:.2f} of {t_big * 1e3:.2f} ms)"
-    bst = big.stats()
-    assert bst["device_error"] == 0 and bst["bounce_live"][0] == 9 * 64 * 800 * 800
-    big.free()
-    small.free()
+    on a non-blocking stream of the context's own), not for the device: with long batched passes of
+    another context queued, a small context's image and statistics are read while those passes are
+    still running (checked with an event queued after them), and both images stay bit-exact.
+    Run in a fresh process (tests/ctx_sync_worker.py): HIP maps a process's streams onto 4 hardware
+    queues (GPU_MAX_HW_QUEUES) and streams beyond that share queues in submission order, so the test
+    keeps its own streams the only ones on the device."""
+    import json
+    import subprocess
+    import sys
+    from pathlib import Path
+    worker = Path(__file__).resolve().parent / "ctx_sync_worker.py"
+    res = subprocess.run([sys.executable, str(worker)], capture_output=True, text=True, timeout=240)
+    assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-3000:]
+    r = json.loads(res.stdout.strip().splitlines()[-1])
+    assert r["first_ok"] and r["second_ok"], r
+    assert r["small_live0"] == 32 * 24 and r["small_err"] == 0, r
+    assert r["big_live0"] == 9 * 64 * 800 * 800 and r["big_err"] == 0, r
+    assert r["running"], f"the small context's reads waited for the other context: {r}"
