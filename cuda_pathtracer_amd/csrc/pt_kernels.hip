@@ -2290,6 +2290,15 @@ __global__ __launch_bounds__(kBlock, FIRST || MESH ? 1 : PT_LATER_WAVES) void k_
             int q = i;   // physical index of the path (and of its k_traverse record)
             if (FIRST) {
                 raygen_at(A.cam, A.fl, A.tile, i, my_it, i - it_base, p);   // (a workgroup holds one iteration)
+#if defined(PT_DUP) && PT_DUP == 6   // diagnostic: raygen again on an opaque pixel index
+                {
+                    PathReg p2;
+                    int i2 = i;
+                    asm volatile("" : "+v"(i2));
+                    raygen_at(A.cam, A.fl, A.tile, i2, my_it, i2 - it_base, p2);
+                    if (__float_as_uint(p2.d.x + p2.o.y) == 0x7f7ffffeu) atomicAdd(&A.stats->bound_mismatch, 7u);
+                }
+#endif
             } else {
                 const int s = seg_walk(s_pre, nseg_in, seg, i);
                 q = s * chunk_in + (i - s_pre[s]);
@@ -2330,6 +2339,14 @@ __global__ __launch_bounds__(kBlock, FIRST || MESH ? 1 : PT_LATER_WAVES) void k_
                     gm = A.cmask[lp0 >> 6];
                 }
                 h = closest_hit<MESH == kMeshInline, false, !FIRST>(A.S, A.fl, s_geoms, p.o, p.d, &A.stats->bound_mismatch, gm);
+#if defined(PT_DUP) && PT_DUP == 7   // diagnostic: the camera ray's closest hit again on an opaque origin
+                if (FIRST) {
+                    f3 o2 = p.o;
+                    asm volatile("" : "+v"(o2.x), "+v"(o2.y), "+v"(o2.z));
+                    const Hit h2 = closest_hit<MESH == kMeshInline, false, !FIRST>(A.S, A.fl, s_geoms, o2, p.d, &A.stats->bound_mismatch, gm);
+                    if (__float_as_uint(h2.t) == 0x7f7ffffeu) atomicAdd(&A.stats->bound_mismatch, 7u);
+                }
+#endif
             }
             STAMP(t2);
             const int key = A.fl.rng_pixel ? slot_pixel(A.cam, A.tile, p.slot) : i - it_base;
