@@ -1408,11 +1408,15 @@ constexpr int kFoldBatch = PT_FOLD_BATCH;   // k_traverse4: task results read pe
 #endif
 #ifndef PT_T4_TASKS
 #define PT_T4_TASKS 2    // k_traverse4 leaf tasks: K consecutive triangles of one leaf per lane per trip
-#endif                   // (a leaf's remaining count rounded up to a multiple of K: 64 K triangle tests per trip)
+#endif                   // (a leaf's remaining count rounded up to a multiple of K: 64 K triangle tests per trip),
+                         // for walks without the exact t-cull; with it, K = 1 (pt_ctx::walk_k)
 // Measured (config 5, 64 iterations per pass, same box, two alternations; profiles/r05_walk_ab.txt):
 // K = 1 / 2 / 3 / 4: 822 / 929 / 793 / 723 Mray/s.  K = 2 halves the trips the triangle tasks need
 // (112 per ray at 64 per trip: they, not the 56 interior steps, bounded a ray's trips) at 122 VGPRs,
-// still 4 waves per SIMD; K = 3 and 4 take 132 / 141 VGPRs and drop to 3 waves.
+// still 4 waves per SIMD; K = 3 and 4 take 132 / 141 VGPRs and drop to 3 waves.  Where the exact t-cull is on
+// (the tessellated workload, room.json) the cull leaves few triangles per reached leaf, the trips are
+// bound by the interior steps, and the second slot only adds divergent work: K = 2 5,542 vs K = 1
+// 5,755 Mray/s on the tessellated workload (same box) — so those walks run K = 1.
 constexpr int kT4K = PT_T4_TASKS;
 #ifndef PT_T4_COOP
 #define PT_T4_COOP 0     // k_traverse4 quad fetch: 0 each interior lane loads its own 112 B (7 loads);
@@ -1686,7 +1690,7 @@ __device__ __forceinline__ void wave_sync() {
 #ifndef PT_T4_WAVES
 #define PT_T4_WAVES 1   // (A/B knob: minimum waves per SIMD of k_traverse4)
 #endif
-template <bool FIRST>
+template <bool FIRST, int K>
 __global__ __launch_bounds__(kBlock, PT_T4_WAVES) void k_traverse4(const KArgs A) {
     extern __shared__ int s_tstack[];   // stack_rows entries per thread, column layout
     __shared__ int32_t s_pre[FIRST ? 1 : kMaxSeg + 1];
@@ -1695,10 +1699,8 @@ __global__ __launch_bounds__(kBlock, PT_T4_WAVES) void k_traverse4(const KArgs A
     // then overwritten by the task's result (t or NaN = no hit, bx, by, -)
 #if PT_T4_ASSIGN == 1
     __shared__ v4f s_task[2 * kBlock];
-#elif PT_T4_TASKS > 1
-    __shared__ v4f s_task[kT4K * kBlock];   // kT4K task results per lane
 #else
-    __shared__ v4f s_task[kBlock];      // task results only (index 2j + 1 -> j below)
+    __shared__ v4f s_task[K * kBlock];  // task results only (K per lane)
 #endif
 #if PT_T4_ASSIGN == 0
     __shared__ int32_t s_own[kBlock];   // leaf tasks: tag << 6 | owner lane, at the owner's first task
@@ -1748,11 +1750,8 @@ __global__ __launch_bounds__(kBlock, PT_T4_WAVES) void k_traverse4(const KArgs A
 #if PT_T4_ASSIGN == 1
     v4f* task = s_task + wave * 128;
 #define PT_RES(j) task[2 * (j) + 1]
-#elif PT_T4_TASKS > 1
-    v4f* task = s_task + wave * (64 * kT4K);
-#define PT_RES(j) task[(j)]
 #else
-    v4f* task = s_task + wave * 64;
+    v4f* task = s_task + wave * (64 * K);
 #define PT_RES(j) task[(j)]
 #endif
 #if PT_T4_ASSIGN == 0
@@ -1860,20 +1859,13 @@ __global__ __launch_bounds__(kBlock, PT_T4_WAVES) void k_traverse4(const KArgs A
         };
         // ---- leaf tasks: the remaining triangles of the leaf lanes, one per lane of the wave ----
         const int cnt = (have && leaf) ? te - ti : 0;
-#if PT_T4_TASKS > 1
-        // task slots come in groups of kT4K consecutive triangles of one leaf (one lane tests the
+        // task slots come in groups of K consecutive triangles of one leaf (one lane tests the
         // group): counted in group units
-        const int pcnt = (cnt + kT4K - 1) / kT4K;
+        const int pcnt = (cnt + K - 1) / K;
         const int incl = (int)lb::wave_inclusive_scan((uint32_t)pcnt);
         const int pre = incl - pcnt;   // first group of this lane's leaf
         const int T = __builtin_amdgcn_readlane(incl, 63);
-        const int cov = (pcnt > 0 && pre < 64) ? min(cnt, kT4K * (64 - pre)) : 0;   // triangles covered this trip
-#else
-        const int incl = (int)lb::wave_inclusive_scan((uint32_t)cnt);
-        const int pre = incl - cnt;
-        const int T = __builtin_amdgcn_readlane(incl, 63);
-        const int cov = (cnt > 0 && pre < 64) ? min(cnt, 64 - pre) : 0;   // this trip's tasks of this lane
-#endif
+        const int cov = (pcnt > 0 && pre < 64) ? min(cnt, K * (64 - pre)) : 0;   // triangles covered this trip
         const bool is_task = lane < T;
         bool inner = have && !leaf;
 #if PT_T4_OVERLAP
@@ -1943,7 +1935,7 @@ __global__ __launch_bounds__(kBlock, PT_T4_WAVES) void k_traverse4(const KArgs A
         if (S.qcull && inner) cw = *reinterpret_cast<const v4u*>(S.qcull + 4 * (size_t)(cur & kQuadIdxMask));
         f3 to = F3(0, 0, 0), td = F3(0, 0, 0);
         int tidx = 0;
-        int ntask = 1;   // (PT_T4_TASKS > 1) triangles tidx .. tidx + ntask - 1 of this task lane
+        int ntask = 1;   // (K > 1) triangles tidx .. tidx + ntask - 1 of this task lane
         if (T > 0) {   // (wave-uniform)
 #if PT_T4_ASSIGN == 1   // owners write (ray, triangle index) into each of their task slots
             for (int k = 0; k < cov; ++k) {
@@ -1971,12 +1963,8 @@ __global__ __launch_bounds__(kBlock, PT_T4_WAVES) void k_traverse4(const KArgs A
             const uint64_t le = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
             const int pos = is_task ? 63 - (int)__clzll(heads & le) : lane;   // the owner's first task
             const int ow = __shfl(v, pos) & 63;
-#if PT_T4_TASKS > 1
-            tidx = __shfl(ti, ow) + kT4K * (lane - pos);
-            ntask = min(kT4K, __shfl(te, ow) - tidx);   // (the leaf's triangles left in this group)
-#else
-            tidx = __shfl(ti, ow) + (lane - pos);
-#endif
+            tidx = __shfl(ti, ow) + K * (lane - pos);
+            if (K > 1) ntask = min(K, __shfl(te, ow) - tidx);   // (the leaf's triangles left in this group)
             to = F3(__shfl(o.x, ow), __shfl(o.y, ow), __shfl(o.z, ow));
             td = F3(__shfl(d.x, ow), __shfl(d.y, ow), __shfl(d.z, ow));
 #endif
@@ -1985,9 +1973,7 @@ __global__ __launch_bounds__(kBlock, PT_T4_WAVES) void k_traverse4(const KArgs A
 #endif
         }
         v4f t0, t1, t2;
-#if PT_T4_TASKS > 1
-        v4f u[kT4K - 1][3];   // the group's further triangles
-#endif
+        v4f u[K > 1 ? K - 1 : 1][3];   // the group's further triangles
 #ifndef PT_T4_TRI_PACK
 #define PT_T4_TRI_PACK 1
 #endif
@@ -1999,9 +1985,8 @@ __global__ __launch_bounds__(kBlock, PT_T4_WAVES) void k_traverse4(const KArgs A
             const v3f a = *reinterpret_cast<const v3f*>(p), b = *reinterpret_cast<const v3f*>(p + 3),
                       c = *reinterpret_cast<const v3f*>(p + 6);
             t0 = v4f{a[0], a[1], a[2], 0.f}; t1 = v4f{b[0], b[1], b[2], 0.f}; t2 = v4f{c[0], c[1], c[2], 0.f};
-#if PT_T4_TASKS > 1
 #pragma unroll
-            for (int j = 1; j < kT4K; ++j)
+            for (int j = 1; j < K; ++j)
                 if (j < ntask) {
                     const float* pj = p + 9 * j;
                     const v3f a2 = *reinterpret_cast<const v3f*>(pj), b2 = *reinterpret_cast<const v3f*>(pj + 3),
@@ -2010,7 +1995,6 @@ __global__ __launch_bounds__(kBlock, PT_T4_WAVES) void k_traverse4(const KArgs A
                     u[j - 1][1] = v4f{b2[0], b2[1], b2[2], 0.f};
                     u[j - 1][2] = v4f{c2[0], c2[1], c2[2], 0.f};
                 }
-#endif
 #else
             const v4f* tsrc = reinterpret_cast<const v4f*>(S.tris + tidx);   // (non-task lanes: triangle 0)
             t0 = tsrc[0]; t1 = tsrc[1]; t2 = tsrc[2];
@@ -2112,18 +2096,14 @@ __global__ __launch_bounds__(kBlock, PT_T4_WAVES) void k_traverse4(const KArgs A
 #endif
             float bx = 0.f, by = 0.f, bz = 0.f;
             const bool h = ray_tri(DTri{t0, t1, t2}, to, td, bx, by, bz);
-#if PT_T4_TASKS > 1
-            PT_RES(kT4K * lane) = v4f{h ? bz : __builtin_nanf(""), bx, by, 0.f};
+            PT_RES(K * lane) = v4f{h ? bz : __builtin_nanf(""), bx, by, 0.f};
 #pragma unroll
-            for (int j = 1; j < kT4K; ++j)
+            for (int j = 1; j < K; ++j)
                 if (j < ntask) {
                     float cx = 0.f, cy = 0.f, cz = 0.f;
                     const bool h2 = ray_tri(DTri{u[j - 1][0], u[j - 1][1], u[j - 1][2]}, to, td, cx, cy, cz);
-                    PT_RES(kT4K * lane + j) = v4f{h2 ? cz : __builtin_nanf(""), cx, cy, 0.f};
+                    PT_RES(K * lane + j) = v4f{h2 ? cz : __builtin_nanf(""), cx, cy, 0.f};
                 }
-#else
-            PT_RES(lane) = v4f{h ? bz : __builtin_nanf(""), bx, by, 0.f};
-#endif
         }
         if (T > 0) {
             wave_sync();   // the task results
@@ -2132,7 +2112,7 @@ __global__ __launch_bounds__(kBlock, PT_T4_WAVES) void k_traverse4(const KArgs A
                     v4f x[kFoldBatch];
 #pragma unroll
                     for (int k = 0; k < kFoldBatch; ++k)
-                        if (k0 + k < cov) x[k] = PT_RES(kT4K * pre + k0 + k);
+                        if (k0 + k < cov) x[k] = PT_RES(K * pre + k0 + k);
 #pragma unroll
                     for (int k = 0; k < kFoldBatch; ++k)
                         if (k0 + k < cov) fold(x[k], ti + k0 + k);
@@ -3200,6 +3180,7 @@ struct pt_ctx {
     int quad_occ = 0;                    // k_traverse4: bound on its stack occupancy (build_quads)
     double tcull_frac = 0.0;             // share of quad slots whose exact t-cull margin can pay (build_qcull)
     bool trav_quads = false;             // mesh mode 2 walks the 4-wide layout (PT_AMD_TRAV=pairs: off)
+    int walk_k = kT4K;                   // k_traverse4's triangle tasks per lane: kT4K, 1 with the exact t-cull
     hipStream_t fin_stream = nullptr;
     hipEvent_t ev_pass[2] = {}, ev_fin[2] = {};
     bool fin_out[2] = {false, false};
@@ -3695,8 +3676,11 @@ int launch_bounce(pt_ctx* c, bool first, bool spp1, int mesh, hipStream_t st, co
         if (int rc = prof_begin(c, st, first ? PT_KIND_FIRST_TRAVERSE : PT_KIND_TRAVERSE, &ev)) return rc;
         const size_t lds = (size_t)a.stack_rows * kBlock * sizeof(int);
         const bool quad = c->trav_quads && !a.fl.bvh_cull;
-        if (quad && first) hipLaunchKernelGGL(k_traverse4<true>, dim3(c->grid_traverse4), dim3(kBlock), lds, st, a);
-        else if (quad) hipLaunchKernelGGL(k_traverse4<false>, dim3(c->grid_traverse4), dim3(kBlock), lds, st, a);
+        if (quad && c->walk_k == 1) {
+            if (first) hipLaunchKernelGGL((k_traverse4<true, 1>), dim3(c->grid_traverse4), dim3(kBlock), lds, st, a);
+            else hipLaunchKernelGGL((k_traverse4<false, 1>), dim3(c->grid_traverse4), dim3(kBlock), lds, st, a);
+        } else if (quad && first) hipLaunchKernelGGL((k_traverse4<true, kT4K>), dim3(c->grid_traverse4), dim3(kBlock), lds, st, a);
+        else if (quad) hipLaunchKernelGGL((k_traverse4<false, kT4K>), dim3(c->grid_traverse4), dim3(kBlock), lds, st, a);
         else if (first) hipLaunchKernelGGL(k_traverse<true>, dim3(c->grid_traverse), dim3(kBlock), lds, st, a);
         else hipLaunchKernelGGL(k_traverse<false>, dim3(c->grid_traverse), dim3(kBlock), lds, st, a);
         HIP_TRY(hipGetLastError());
@@ -3949,6 +3933,10 @@ int build_quads(pt_ctx* c, const std::vector<DNode>& nodes, const std::vector<pt
         HIP_TRY(hipMemcpy(d_q, qcull.data(), qcull.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
         c->args.S.qcull = d_q;
     }
+    // triangle tasks per lane: kT4K, or 1 where the t-cull leaves few triangles per reached leaf
+    // (PT_AMD_WALK_TASKS=1/2 forces one; the results are the same bits)
+    c->walk_k = on ? 1 : kT4K;
+    if (const char* wt = std::getenv("PT_AMD_WALK_TASKS")) c->walk_k = std::atoi(wt) == 1 ? 1 : kT4K;
     return PT_OK;
 }
 
@@ -4268,7 +4256,8 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
             per_cu = 4;
         c->grid_traverse = cus * per_cu;
         per_cu = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_traverse4<false>, kBlock, slds) != hipSuccess ||
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, c->walk_k == 1 ? k_traverse4<false, 1> : k_traverse4<false, kT4K>,
+                                                         kBlock, slds) != hipSuccess ||
             per_cu <= 0)
             per_cu = 4;
         c->grid_traverse4 = cus * per_cu;

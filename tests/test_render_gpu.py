@@ -608,10 +608,14 @@ def test_exact_tcull_records_equal_reference_walk(room_path, config_scenes, tmp_
     assert total > 400_000
 
 
-def test_tessellated_meshes_bitexact_with_tcull(tmp_path):
+@pytest.mark.parametrize("tasks", [None, "2"])
+def test_tessellated_meshes_bitexact_with_tcull(tmp_path, monkeypatch, tasks):
     """The exact t-cull's own workload (100k small triangles on a sphere and a torus): the GPU image
-    equals the oracle's (which walks the whole reference tree, no cull) bit for bit, batched and not."""
+    equals the oracle's (which walks the whole reference tree, no cull) bit for bit, batched and not;
+    with the t-cull the walk deals one triangle task per lane, and two when forced (PT_AMD_WALK_TASKS)."""
     from cuda_pathtracer_amd import PathTracer, Scene, scenes
+    if tasks is not None:
+        monkeypatch.setenv("PT_AMD_WALK_TASKS", tasks)
     path = scenes.tessellated_meshes(tmp_path, res=(160, 90), depth=16)
     s = Scene(path)
     assert PathTracer(s, _gui()).walk_info()["tcull"]
@@ -961,12 +965,15 @@ def test_sorted_multitile_histogram_scan(cornell_path):
     assert st["bounce_live"] == live
 
 
-@pytest.mark.parametrize("kw", [dict(), dict(sortbyMaterial=True)])
-def test_config5_100k_triangles_bitexact(tmp_path, kw):
+@pytest.mark.parametrize("kw,tasks", [(dict(), None), (dict(), "1"), (dict(), "2"), (dict(sortbyMaterial=True), None)])
+def test_config5_100k_triangles_bitexact(tmp_path, monkeypatch, kw, tasks):
     """BASELINE.json config 5's geometry at full size — 100k random triangles through OBJ + SAH BVH
     (depth-22 tree, child-pair layout, LDS stack), DEPTH 32 — at a reduced resolution: GPU == oracle
-    bit for bit (the benchmarked tree itself, not the 3000-triangle parity scene)."""
+    bit for bit (the benchmarked tree itself, not the 3000-triangle parity scene); the 4-wide walk
+    with one and with two triangle tasks per lane (PT_AMD_WALK_TASKS)."""
     from cuda_pathtracer_amd import Scene, scenes
+    if tasks is not None:
+        monkeypatch.setenv("PT_AMD_WALK_TASKS", tasks)
     path = scenes.random_triangles(tmp_path, n=100_000, res=(160, 90), depth=32)
     g, r, st, live = _run(Scene(path), O.OracleScene.from_json(path), _gui(**kw), iters=2, spp=2)
     _assert_bitexact(g, r, f"config 5 100k triangles {kw}")
