@@ -1690,8 +1690,11 @@ __device__ __forceinline__ void wave_sync() {
 #ifndef PT_T4_WAVES
 #define PT_T4_WAVES 1   // (A/B knob: minimum waves per SIMD of k_traverse4)
 #endif
+#ifndef PT_T4_WAVES_FIRST
+#define PT_T4_WAVES_FIRST 4   // (A/B knob: minimum waves per SIMD of the camera-ray walk: 138 -> 128 VGPRs, +1%)
+#endif
 template <bool FIRST, int K>
-__global__ __launch_bounds__(kBlock, PT_T4_WAVES) void k_traverse4(const KArgs A) {
+__global__ __launch_bounds__(kBlock, FIRST ? PT_T4_WAVES_FIRST : PT_T4_WAVES) void k_traverse4(const KArgs A) {
     extern __shared__ int s_tstack[];   // stack_rows entries per thread, column layout
     __shared__ int32_t s_pre[FIRST ? 1 : kMaxSeg + 1];
     __shared__ uint32_t s_wsum[4];
@@ -1977,11 +1980,31 @@ __global__ __launch_bounds__(kBlock, PT_T4_WAVES) void k_traverse4(const KArgs A
 #ifndef PT_T4_TRI_PACK
 #define PT_T4_TRI_PACK 1
 #endif
+#ifndef PT_T4_TRI_X4
+#define PT_T4_TRI_X4 1   // (A/B knob: K = 2 groups loaded as 4 x 16 B + 8 B)
+#endif
         auto load_tri = [&]() {
 #if PT_T4_TRI_PACK
             // 36 bytes per triangle: a leaf's consecutive triangles cover fewer cache lines
             typedef float v3f __attribute__((ext_vector_type(3)));
             const float* p = S.tpack + 9 * (size_t)tidx;
+#if PT_T4_TRI_X4
+            if (K == 2) {
+                // the group's 72 contiguous bytes in five loads (4 x 16 B + 8 B, dword-aligned) instead
+                // of six 12-byte ones: 5.4 instead of 6.4 cache-line accesses per lane on average (the
+                // address path's cost); the pack is padded, so a group of one reads a neighbour
+                typedef float v4a __attribute__((ext_vector_type(4), aligned(4)));
+                typedef float v2a __attribute__((ext_vector_type(2), aligned(4)));
+                const v4a q0 = *reinterpret_cast<const v4a*>(p), q1 = *reinterpret_cast<const v4a*>(p + 4),
+                          q2 = *reinterpret_cast<const v4a*>(p + 8), q3 = *reinterpret_cast<const v4a*>(p + 12);
+                const v2a q4 = *reinterpret_cast<const v2a*>(p + 16);
+                t0 = v4f{q0[0], q0[1], q0[2], 0.f}; t1 = v4f{q0[3], q1[0], q1[1], 0.f};
+                t2 = v4f{q1[2], q1[3], q2[0], 0.f};
+                u[0][0] = v4f{q2[1], q2[2], q2[3], 0.f}; u[0][1] = v4f{q3[0], q3[1], q3[2], 0.f};
+                u[0][2] = v4f{q3[3], q4[0], q4[1], 0.f};
+                return;
+            }
+#endif
             const v3f a = *reinterpret_cast<const v3f*>(p), b = *reinterpret_cast<const v3f*>(p + 3),
                       c = *reinterpret_cast<const v3f*>(p + 6);
             t0 = v4f{a[0], a[1], a[2], 0.f}; t1 = v4f{b[0], b[1], b[2], 0.f}; t2 = v4f{c[0], c[1], c[2], 0.f};
@@ -4092,7 +4115,7 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
             std::memcpy(at[i].n, t.n, sizeof at[i].n);
             std::memcpy(at[i].uv, t.uv, sizeof at[i].uv);
         }
-        std::vector<float> pack(9 * tr.size());
+        std::vector<float> pack(9 * tr.size() + 16);   // (+16: k_traverse4's group loads may read past the last)
         for (size_t i = 0; i < tr.size(); ++i)
             for (int k = 0; k < 3; ++k) {
                 pack[9 * i + k] = tr[i].a[k];
