@@ -221,9 +221,12 @@ def dropin_bench(scene_path: str, iters: int = 50, warmup: int = 3) -> dict:
         return {"error": f"pt_dropin_bench rc={rc}"}
     return {"value": seg.value / (ms.value * 1e-3) / 1e6, "unit": "Mray/s", "calls": iters,
             "ms_per_call": ms.value / iters, "segments": seg.value, "flag_syncs": syncs.value,
+            "render_ahead": os.environ.get("PT_AMD_AHEAD", "1") != "0",
             "definition": f"{iters} calls of the C++ mirror's pathtrace(nullptr, 0, it) on the same scene (one "
                           "iteration each: per-call pt_set_flags, pt_render_pass, synchronous 7.7 MB image copy "
-                          f"to the host, as pathtrace.cu:438-524), after {warmup} warm-up calls; segments / wall time"}
+                          f"to the host, as pathtrace.cu:438-524), after {warmup} warm-up calls; segments / wall time. "
+                          "Each call queues the next iteration's bounces before its copy (pt_render_ahead), and "
+                          "the next call claims them; segments count claimed iterations only"}
 
 
 def _pmc_leg(args, scene_path, spp_pass, sorted_, avg_ms, kernel_prefix, seg_per_launch, busy_ms, launches,

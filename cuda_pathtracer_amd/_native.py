@@ -140,6 +140,7 @@ SIGNATURES = {
     "pt_ctx_counters": (_I, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "pt_ctx_walk_info": (_I, [_P, C.POINTER(_I), C.POINTER(_I), C.POINTER(C.c_double)]),
     "pt_render_pass": (_I, [_P, _I, _P]),
+    "pt_render_ahead": (_I, [_P, _I, _P]),
     "pt_host_register": (_I, [_P, C.c_uint64]),
     "pt_host_unregister": (_I, [_P]),
     "pt_stream_create": (_I, [C.POINTER(_P)]),

@@ -3069,6 +3069,36 @@ __global__ void k_finalize_spp(float* __restrict__ image, const v4f* __restrict_
     }
 }
 
+// Render-ahead claim (add != 0: the iteration's colours into the image — k_finalize_spp with one
+// sample — and its counts into the context's) or drop (add == 0: the counts zeroed, device errors
+// kept).  Emissive counts: `rows` bounces of `stride` per-workgroup slots.
+__global__ void k_ahead_settle(float* __restrict__ image, const v4f* __restrict__ col, int npix, DevStats* __restrict__ st,
+                               DevStats* __restrict__ ast, unsigned long long* __restrict__ emit,
+                               unsigned long long* __restrict__ aemit, int nemit, int add) {
+    const int gid = blockIdx.x * blockDim.x + threadIdx.x, gsz = gridDim.x * blockDim.x;
+    if (add)
+        for (int lp = gid; lp < npix; lp += gsz) {
+            const v4f c = PT_LD(col + lp);
+            image[3 * (size_t)lp] += c[0]; image[3 * (size_t)lp + 1] += c[1]; image[3 * (size_t)lp + 2] += c[2];
+        }
+    for (int j = gid; j < nemit; j += gsz) {
+        const unsigned long long v = aemit[j];
+        if (v) {
+            if (add) emit[j] += v;
+            aemit[j] = 0ull;
+        }
+    }
+    if (gid < 66) {   // segments, passes, bounce_live[64]
+        unsigned long long* a = &ast->segments + gid;
+        if (add) (&st->segments)[gid] += *a;
+        *a = 0ull;
+    } else if (gid == 66) {
+        st->err |= ast->err;
+        st->bound_mismatch += ast->bound_mismatch;
+        ast->err = 0u;
+        ast->bound_mismatch = 0u;
+    }
+}
 
 // sendImageToPBO (pathtrace.cu:64-86)
 __global__ void k_preview(const float* __restrict__ image, uint8_t* __restrict__ rgba, int npix, int iter) {
@@ -3217,6 +3247,18 @@ struct pt_ctx {
     hipStream_t io_stream = nullptr;
     hipEvent_t ev_done = nullptr;
     bool done_recorded = false;
+    // Render-ahead (one-iteration contexts, pt_render_ahead): the bounces of iteration ahead_iter,
+    // queued before the call that asks for it, keep their colours in ahead_col and their counts in
+    // ahead_stats / ahead_emit until pt_render_pass claims them (the same iteration and flags: the
+    // colours are added into the image then, as finalGather would) or drops them (anything else).
+    // Every later pass on any stream is ordered after them (ev_ahead).
+    v4f* ahead_col = nullptr;
+    DevStats* ahead_stats = nullptr;
+    unsigned long long* ahead_emit = nullptr;
+    hipEvent_t ev_ahead = nullptr;
+    bool ahead_recorded = false, ahead_valid = false;
+    int32_t ahead_iter = 0;
+    pt_flags ahead_flags{};
 
     ~pt_ctx() {
         for (auto& e : events) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
@@ -3227,6 +3269,7 @@ struct pt_ctx {
         if (fin_stream) (void)hipStreamDestroy(fin_stream);
         if (io_stream && io_stream != fin_stream) (void)hipStreamDestroy(io_stream);
         if (ev_done) (void)hipEventDestroy(ev_done);
+        if (ev_ahead) (void)hipEventDestroy(ev_ahead);
         if (ev_fork) (void)hipEventDestroy(ev_fork);
         for (int l = 0; l < kMaxLanes; ++l) {
             if (ev_join[l]) (void)hipEventDestroy(ev_join[l]);
@@ -4395,6 +4438,7 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
 int pt_destroy(pt_ctx* c) {
     if (c) {   // the context's own queued work only (its streams, and the last pass on the caller's)
         (void)wait_ctx(c);
+        if (c->ahead_recorded) (void)hipEventSynchronize(c->ev_ahead);
         if (c->fin_stream) (void)hipStreamSynchronize(c->fin_stream);
         for (int l = 1; l < kMaxLanes; ++l)
             if (c->lane_stream[l]) (void)hipStreamSynchronize(c->lane_stream[l]);
@@ -4421,6 +4465,7 @@ int pt_set_flags(pt_ctx* c, const pt_flags* f) {
     ++c->n_flag_syncs;
     // (this context's queued passes still read the old bounds and masks; nothing else is waited for)
     if (int rc = wait_ctx(c)) return rc;
+    if (c->ahead_recorded) HIP_TRY(hipEventSynchronize(c->ev_ahead));   // (and is dropped: flags differ)
     if (lens) {   // the camera lens bounds the ray origins: re-derive the widened bounds
         update_bounds(c, f->aperture);
         HIP_TRY(io_copy(c, c->d_geoms, c->hgeoms.data(), c->hgeoms.size() * sizeof(DGeom), hipMemcpyHostToDevice));
@@ -4452,23 +4497,28 @@ int pt_ctx_counters(const pt_ctx* c, uint64_t* mask_builds, uint64_t* flag_syncs
     return PT_OK;
 }
 
-int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
-    if (!c) return pt::fail(PT_ERR_ARG, "null context");
-    if (iter_first < 0) return pt::fail(PT_ERR_ARG, "iteration index must be >= 0");
-    hipStream_t st = (hipStream_t)stream;
+static int wait_finalize(pt_ctx* c, hipStream_t st);
+
+// One pass on st; ahead: a render-ahead pass (one-iteration context) whose colours and counts go to
+// the ahead buffers and that neither finalizes nor marks the context (pt_render_ahead).
+static int render_pass(pt_ctx* c, int32_t iter_first, hipStream_t st, bool ahead) {
     KArgs A = c->args;
     A.tile.iter_first = iter_first;
-    const bool spp1 = A.tile.spp == 1;
+    const bool spp1 = A.tile.spp == 1 && !ahead;
     const bool sorted = c->flags.sort_by_material != 0;
     const bool mesh = A.S.ntris > 0;
     const int mmode = mesh_mode(c);   // k_bounce's mesh mode (fused pipeline)
     int cur = 0;   // paths start in buf[0]
     const int h = c->col_half;
-    if (!spp1) {
+    if (ahead) {
+        A.colbuf = c->ahead_col;
+        A.stats = c->ahead_stats;
+        A.emit_slots = c->ahead_emit;
+    } else if (!spp1) {
         A.colbuf = c->colbuf + (size_t)h * (size_t)A.tile.P;
         if (c->fin_out[h]) HIP_TRY(hipStreamWaitEvent(st, c->ev_fin[h], 0));   // pass p-2's finalize
     }
-    const bool laned = (sorted || c->fused) && c->lanes >= 2 && !spp1;
+    const bool laned = (sorted || c->fused) && c->lanes >= 2 && !spp1 && !ahead;
     // One bounce b of the material-sorted pipeline on stream s, for the lane whose buffers are `bufs`
     // (current one: lcur), launch counter `lc` and sort buffers `ss`: [the first bounce's producer],
     // histogram scan, scatter, producer (shade b + intersect b + 1).  Every producer flips the buffers.
@@ -4615,6 +4665,7 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
         }
     }
 
+    if (ahead) return PT_OK;
     if (!spp1) {
         const int npix = A.tile.npix;
         HIP_TRY(hipEventRecord(c->ev_pass[h], st));
@@ -4629,6 +4680,66 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
         return mark_ctx(c, c->fin_stream);   // (the finalize waited for every lane of the pass)
     }
     return mark_ctx(c, st);
+}
+
+static int settle_ahead(pt_ctx* c, hipStream_t st, bool add) {
+    const int npix = c->args.tile.npix;
+    const int nemit = std::min(c->depth, 64) * c->args.emit_stride;
+    hipLaunchKernelGGL(k_ahead_settle, dim3(add ? std::min((npix + 255) / 256, 4096) : 64), dim3(256), 0, st,
+                       c->args.image, (const v4f*)c->ahead_col, npix, c->stats, c->ahead_stats, c->args.emit_slots,
+                       c->ahead_emit, nemit, add ? 1 : 0);
+    HIP_TRY(hipGetLastError());
+    c->ahead_valid = false;
+    return PT_OK;
+}
+
+int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
+    if (!c) return pt::fail(PT_ERR_ARG, "null context");
+    if (iter_first < 0) return pt::fail(PT_ERR_ARG, "iteration index must be >= 0");
+    hipStream_t st = (hipStream_t)stream;
+    if (c->ahead_recorded) {
+        HIP_TRY(hipStreamWaitEvent(st, c->ev_ahead, 0));   // its path buffers, counts and colours
+        if (c->ahead_valid) {
+            if (iter_first == c->ahead_iter && c->args.tile.spp == 1 &&
+                std::memcmp(&c->flags, &c->ahead_flags, sizeof c->flags) == 0) {
+                // the iteration was traced ahead with these flags: only its colours are left to add
+                if (int rc = wait_finalize(c, st)) return rc;
+                if (int rc = settle_ahead(c, st, true)) return rc;
+                return mark_ctx(c, st);
+            }
+            if (int rc = settle_ahead(c, st, false)) return rc;
+        }
+    }
+    return render_pass(c, iter_first, st, false);
+}
+
+// The bounces of iteration `iter` queued now, for the pt_render_pass(iter) that follows (pt_amd.h).
+int pt_render_ahead(pt_ctx* c, int32_t iter, void* stream) {
+    if (!c) return pt::fail(PT_ERR_ARG, "null context");
+    if (iter < 0) return pt::fail(PT_ERR_ARG, "iteration index must be >= 0");
+    if (c->args.tile.spp != 1) return pt::fail(PT_ERR_ARG, "render-ahead needs a context of one iteration per pass");
+    hipStream_t st = (hipStream_t)stream;
+    if (!c->ev_ahead) {   // first use: the ahead buffers
+        const size_t nemit = (size_t)64 * c->args.emit_stride;
+        if (int rc = c->alloc(&c->ahead_col, (size_t)c->args.tile.P)) return rc;
+        if (int rc = c->alloc(&c->ahead_stats, 1)) return rc;
+        if (int rc = c->alloc(&c->ahead_emit, nemit)) return rc;
+        HIP_TRY(hipMemsetAsync(c->ahead_stats, 0, sizeof(DevStats), c->io_stream));
+        HIP_TRY(hipMemsetAsync(c->ahead_emit, 0, nemit * sizeof(unsigned long long), c->io_stream));
+        HIP_TRY(hipStreamSynchronize(c->io_stream));
+        HIP_TRY(hipEventCreateWithFlags(&c->ev_ahead, hipEventDisableTiming));
+    }
+    if (c->ahead_recorded) {
+        HIP_TRY(hipStreamWaitEvent(st, c->ev_ahead, 0));
+        if (c->ahead_valid)
+            if (int rc = settle_ahead(c, st, false)) return rc;   // never claimed: dropped
+    }
+    if (int rc = render_pass(c, iter, st, true)) return rc;
+    HIP_TRY(hipEventRecord(c->ev_ahead, st));
+    c->ahead_recorded = c->ahead_valid = true;
+    c->ahead_iter = iter;
+    c->ahead_flags = c->flags;
+    return PT_OK;
 }
 
 // Work on `st` that reads or writes the image first waits for this context's last enqueued work

@@ -15,6 +15,10 @@ pt_ctx* g_ctx = nullptr;
 // this context alone and runs at the link's DMA rate (pt_host_register).
 void* g_stream = nullptr;
 void* g_pinned = nullptr;
+// Render-ahead (pt_render_ahead): each call queues the next iteration's bounces before its image copy,
+// so they run during the copy; the next call claims them (same iteration and flags: the same image
+// bits) or they are dropped.  Not past the scene's last iteration.  PT_AMD_AHEAD=0 turns it off.
+bool g_ahead = true;
 
 // checkCUDAError (utilities / common.cu:3-15 pattern): print and exit.
 void check(int rc, const char* what) {
@@ -87,6 +91,8 @@ void pathtraceInit(Scene* scene) {
     const pt_flags f = flags_of(g_gui);
     check(pt_create(scene->handle(), &f, nullptr, &g_ctx), "pathtraceInit");
     check(pt_stream_create(&g_stream), "pathtraceInit stream");
+    const char* ah = std::getenv("PT_AMD_AHEAD");
+    g_ahead = !(ah && ah[0] == '0');
     std::fill(scene->state.image.begin(), scene->state.image.end(), vec3f{0.f, 0.f, 0.f});
     if (!scene->state.image.empty() &&
         pt_host_register(scene->state.image.data(), scene->state.image.size() * sizeof(vec3f)) == PT_OK)
@@ -115,5 +121,7 @@ void pathtrace(uchar4* pbo, int frame, int iteration) {
     check(pt_render_pass(g_ctx, iteration, g_stream), "pathtrace");
     if (pbo) check(pt_preview_rgba(g_ctx, iteration, reinterpret_cast<uint8_t*>(pbo), g_stream), "sendImageToPBO");
     if (g_gui) g_gui->TracedDepth = g_scene->state.traceDepth;
+    if (g_ahead && iteration >= 1 && (unsigned)iteration < g_scene->state.iterations)
+        (void)pt_render_ahead(g_ctx, iteration + 1, g_stream);   // (a failure only costs the overlap)
     check(pt_get_image(g_ctx, reinterpret_cast<float*>(g_scene->state.image.data())), "image copy");
 }

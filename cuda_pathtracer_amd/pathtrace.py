@@ -319,6 +319,11 @@ class PathTracer:
         """pathtrace(): iterations [iter_first, iter_first + spp) for this tile, asynchronous."""
         check_pt(lib().pt_render_pass(self._h, int(iter_first), _stream_ptr(stream)))
 
+    def render_ahead(self, iteration: int, stream=None) -> None:
+        """One-iteration contexts: queue iteration `iteration`'s bounces now (pt_render_ahead); the
+        render_pass(iteration) that follows with the same flags only adds their colours."""
+        check_pt(lib().pt_render_ahead(self._h, int(iteration), _stream_ptr(stream)))
+
     def image(self) -> np.ndarray:
         """Tile accumulator (sum of radiance over iterations), shape (rows, width, 3) float32."""
         out = np.empty((self.rows, self.width, 3), dtype=np.float32)

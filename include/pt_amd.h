@@ -259,6 +259,14 @@ int pt_ctx_walk_info(const pt_ctx* c, int32_t* quad_walk, int32_t* tcull_on, dou
  * wait for the last finalize on their stream) or the synchronising calls; issue the passes of one
  * context on one stream, or synchronise between streams. */
 int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream);
+/* Render-ahead for a one-iteration context (spp 1; the drop-in pathtrace() loop): queues the bounces
+ * of iteration `iter` on `stream` now, without touching the image, so they run while the caller
+ * copies the previous image to the host (pathtrace.cu:524's copy).  A later pt_render_pass(c, iter)
+ * with the same flags claims them and only adds their colours into the image (the same bits as
+ * rendering then); any other pass — another iteration, changed flags — drops them first.  Counts
+ * (pt_stats) include an iteration once it is claimed.  Not synchronising; pt_get_image and the
+ * other synchronising calls do not wait for unclaimed ahead work. */
+int pt_render_ahead(pt_ctx* c, int32_t iter, void* stream);
 /* sendImageToPBO (pathtrace.cu:64-86) for the tile: d_rgba = npix * 4 bytes on the device. */
 int pt_preview_rgba(pt_ctx* c, int32_t iter, uint8_t* d_rgba, void* stream);
 /* pathtrace(pbo, frame, iteration) (pathtrace.h:9, pathtrace.cu:437-525) as one call, under the

@@ -887,6 +887,60 @@ def test_set_flags_unchanged_is_cheap(cornell_path):
     pt.free()
 
 
+@pytest.mark.parametrize("scene", ["cornell", "cornell_sorted", "room"])
+def test_render_ahead_claimed_and_dropped_bitexact(cornell_path, room_path, scene):
+    """pt_render_ahead (the drop-in loop's overlap of iteration i + 1's bounces with iteration i's
+    image copy): every pathtrace()-shaped step — set_flags, render_pass(it), render_ahead(it + 1),
+    image read — equals the oracle bit for bit, whether the iteration traced ahead is claimed (same
+    iteration, same flags), dropped for changed flags, dropped for another iteration, or claimed
+    after the image was reset or replaced; the counts include claimed iterations only."""
+    from cuda_pathtracer_amd import PathTracer
+    if scene == "room":
+        s, o = _room_pair(room_path, (40, 32))
+    else:
+        s, o = _pair(cornell_path, (48, 40))
+    base = dict(sortbyMaterial=True) if scene == "cornell_sorted" else dict()
+    # (iteration, flag overrides, image action before the pass)
+    plan = [(1, {}, None), (2, {}, None), (3, {}, None), (4, dict(russianRoulette=False), None),
+            (5, dict(russianRoulette=False), None), (7, dict(russianRoulette=False), None),
+            (8, dict(russianRoulette=False), "reset"), (9, dict(russianRoulette=False), "set"),
+            (10, dict(russianRoulette=False, SSAA=False), None), (11, dict(russianRoulette=False, SSAA=False), None)]
+    stats = []
+    for ahead in (False, True):
+        pt = PathTracer(s, _gui(**base))
+        ref, live_ref = None, [0] * o.depth
+        for it, kw, action in plan:
+            g = _gui(**base, **kw)
+            pt.set_flags(g)
+            if action == "reset":
+                pt.reset_image()
+                ref = np.zeros_like(ref)
+            elif action == "set":
+                ref = (ref * np.float32(0.5)).astype(np.float32)
+                pt.set_image(ref)
+            pt.render_pass(it)
+            ref, live = O.render_pass(o, _oflags(g), it, image=ref)
+            live_ref = [a + b for a, b in zip(live_ref, live)]
+            if ahead:
+                pt.render_ahead(it + 1)
+            _assert_bitexact(pt.image(), ref, f"{scene} ahead={ahead} iteration {it} {kw} {action}")
+        st = pt.stats()
+        assert st["device_error"] == 0
+        assert st["bounce_live"] == live_ref
+        stats.append(st)
+        pt.free()
+    assert stats[0] == stats[1]   # segments, passes, per-bounce live and emissive counts
+
+
+def test_render_ahead_needs_one_iteration_context(cornell_path):
+    from cuda_pathtracer_amd import PathTracer
+    s, _ = _pair(cornell_path, (16, 16))
+    pt = PathTracer(s, _gui(), spp=2)
+    with pytest.raises(Exception, match="one iteration"):
+        pt.render_ahead(3)
+    pt.free()
+
+
 @pytest.mark.parametrize("sort", [False, True])
 def test_async_lanes_stream_ordered_reads(cornell_path, sort):
     """Async lanes: a batched pass does not make the caller's stream wait for every lane, so the
