@@ -1731,6 +1731,18 @@ __global__ __launch_bounds__(kBlock, FIRST ? PT_T4_WAVES_FIRST : PT_T4_WAVES) vo
     int32_t* const qlist = s_qlist + wave * 64;
     v4f* const stage = s_stage + wave * (PT_T4_COOP_ROWS * 8);
 #endif
+#ifndef PT_T4_SEGCUR
+#define PT_T4_SEGCUR 1   // (A/B knob: refills find their segment from the chunk's, not by a binary search each)
+#endif
+    auto seg_of = [&](int k) -> int {   // the last segment starting at or before k (binary search)
+        int lo = 0, hi = nseg - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (s_pre[mid] <= k) lo = mid; else hi = mid - 1;
+        }
+        return lo;
+    };
+    int wseg = 0;   // (!FIRST, PT_T4_SEGCUR) the segment of the wave's current chunk start
     auto ray = [&](int k, f3& o, f3& d) -> int {   // as k_traverse
         if (FIRST) {
             PathReg p;
@@ -1739,11 +1751,14 @@ __global__ __launch_bounds__(kBlock, FIRST ? PT_T4_WAVES_FIRST : PT_T4_WAVES) vo
             d = p.d;
             return k;
         }
-        int lo = 0, hi = nseg - 1;
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (s_pre[mid] <= k) lo = mid; else hi = mid - 1;
-        }
+#if PT_T4_SEGCUR
+        // a chunk spans a few hundred rays and a segment is a bounce workgroup's survivors: a step
+        // or two from the chunk start's segment instead of ~11 dependent LDS reads per refill
+        int lo = wseg;
+        while (lo + 1 < nseg && s_pre[lo + 1] <= k) ++lo;
+#else
+        const int lo = seg_of(k);
+#endif
         const int q = lo * chunk + (k - s_pre[lo]);
         const v4f a = PT_LD(A.in.a + q), b = PT_LD(A.in.b + q);
         o = F3(a[0], a[1], a[2]);
@@ -1805,7 +1820,13 @@ __global__ __launch_bounds__(kBlock, FIRST ? PT_T4_WAVES_FIRST : PT_T4_WAVES) vo
                 if (lane == 0) base = (int)atomicAdd(ticket, (uint32_t)csz);
                 base = __shfl(base, 0);
                 if (base >= N) exhausted = true;
-                else { cnext = base; cend = min(base + csz, N); }
+                else {
+                    cnext = base;
+                    cend = min(base + csz, N);
+#if PT_T4_SEGCUR
+                    if (!FIRST) wseg = __builtin_amdgcn_readfirstlane(seg_of(base));
+#endif
+                }
             }
             if (!exhausted) {
                 const uint32_t rank =

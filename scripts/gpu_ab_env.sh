@@ -1,15 +1,17 @@
-# A/B of environment settings of one library build, alternating on one box:
-# VARIANTS="name1:VAR=x,VAR2=y name2:" (empty assignment list = defaults); BENCH_ARGS for bench.py.
+# Alternating bench runs of (library, environment) variants on one box:
+#   CASES="new:-: bs:bs: r8:-:PT_AMD_REFILL=8" BENCH_ARGS="--config random_triangles_100k" RUNS=2
+# each case is name:lib:env (lib "-" = the tree's library, else build/libpt_amd_<lib>.so; env: A=1,B=2).
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-cd "$R"; mkdir -p gpurun_out/abenv
-O=gpurun_out/abenv
-for k in $(seq 1 ${RUNS:-3}); do
-  for v in ${VARIANTS:-base:}; do
-    name=${v%%:*}; assigns=${v#*:}
-    ( IFS=','; for a in $assigns; do export "$a"; done; unset IFS
-      timeout -k 10 300 python -u bench.py --steps ${STEPS:-20} --warmup 3 --no-cpu-baseline --no-scan --no-pmc --no-dropin ${BENCH_ARGS:-} \
-          > $O/b_${name}_$k.json 2> $O/b_${name}_$k.err ) || { echo "bench $name failed"; tail -5 $O/b_${name}_$k.err; exit 1; }
-    python -c "import json;d=json.load(open('$O/b_${name}_$k.json'));r=d['roofline'];print('$name', round(d['value'],1), round(d['ms_per_step'],3), 'k_bounce', round(r['avg_launch_ms']*1e3,1), 'us')"
+cd "$R"; O=gpurun_out/abe; mkdir -p $O
+for k in $(seq 1 ${RUNS:-2}); do
+  for c in $CASES; do
+    name=${c%%:*}; rest=${c#*:}; lib=${rest%%:*}; envs=${rest#*:}
+    if [ "$lib" = - ]; then unset PT_AMD_LIB; else export PT_AMD_LIB=$R/cuda_pathtracer_amd/build/libpt_amd_$lib.so; fi
+    envline=$(echo "$envs" | tr ',' ' ')
+    env $envline timeout -k 10 300 python -u bench.py --steps ${STEPS:-3} --warmup 1 --no-cpu-baseline --no-scan --no-pmc \
+        --no-walk-counters --no-dropin ${BENCH_ARGS:-} > $O/b_${name}_$k.json 2> $O/b_${name}_$k.err \
+        || { echo "bench $name failed"; tail -5 $O/b_${name}_$k.err; exit 1; }
+    python -c "import json;d=json.load(open('$O/b_${name}_$k.json'));r=d['roofline'];print('$name', round(d['value'],1), round(d['ms_per_step'],2), 'ms/step', r.get('kernel'), round(r.get('avg_launch_ms',0),3), round(r.get('first_traverse_avg_ms',0) or 0,2))"
   done
 done
