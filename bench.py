@@ -531,10 +531,11 @@ def main() -> None:
         _native_lib().pt_scene_bvh_quads(scene.handle, None, 0, None, None) > 0
     # k_bounce<FIRST, SPP1, MESH mode>: mesh scenes run mode 2 (closest mesh hit from k_traverse)
     bprefix = f"k_bounce<false, {'true' if spp == 1 else 'false'}, {2 if mesh else 0}>"
-    wprefix = "k_traverse4<false>" if quads else "k_traverse<false>"
+    # (k_traverse4<FIRST, K>: K triangle tasks per lane, 2, or 1 where the exact t-cull is on)
+    wprefix = "k_traverse4<false," if quads else "k_traverse<false>"
     kprefix = wprefix if walk else bprefix
     kernel_name = ("material-sorted pipeline (k_sort_produce: shade + compact + intersect / histogram scan + permutation)"
-                   if sorted_ else kprefix)
+                   if sorted_ else ("k_traverse4<false, K>" if kprefix == "k_traverse4<false," else kprefix))
     kernel_min = 0
     for b in range(1, depth):
         n_out = plive[b + 1] if b + 1 < depth else 0

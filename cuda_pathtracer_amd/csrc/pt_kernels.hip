@@ -1993,7 +1993,10 @@ __global__ __launch_bounds__(kBlock, FIRST ? PT_T4_WAVES_FIRST : PT_T4_WAVES) vo
             td = F3(__shfl(d.x, ow), __shfl(d.y, ow), __shfl(d.z, ow));
 #endif
 #ifdef PT_TRAV_STATS
-            if (lane == 0) { ++t_leaf; n_tris += (uint32_t)min(T, 64); }
+            {   // triangles dealt this trip (K per task lane at most)
+                const uint32_t tt = __builtin_amdgcn_readlane(lb::wave_inclusive_scan((uint32_t)cov), 63);
+                if (lane == 0) { ++t_leaf; n_tris += tt; }
+            }
 #endif
         }
         v4f t0, t1, t2;

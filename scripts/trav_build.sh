@@ -7,5 +7,5 @@ python -c "import sys; sys.path.insert(0, '$R'); from cuda_pathtracer_amd import
 /opt/rocm/bin/hipcc -x hip --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-slp-vectorize -DPT_TRAV_STATS -I $R/include \
     -c $R/cuda_pathtracer_amd/csrc/pt_kernels.hip -o $B/pt_kernels_trav.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $B/libpt_amd_trav.so $B/pt_kernels_trav.o \
-    $B/sc_kernels.hip.o $B/bvh_build.hip.o $B/pt_scene.cpp.o $B/pt_mesh.cpp.o $B/pt_image.cpp.o $B/pt_jpeg.cpp.o -lz
+    $B/sc_kernels.hip.o $B/sc_variants.hip.o $B/bvh_build.hip.o $B/pt_scene.cpp.o $B/pt_mesh.cpp.o $B/pt_image.cpp.o $B/pt_jpeg.cpp.o -lz
 echo $B/libpt_amd_trav.so

@@ -3,9 +3,11 @@ scripts/trav_build.sh): rays, interior fetches and triangle tests per ray, and h
 the wave do useful work.  Usage: trav_stats.py scene.json [spp] (PT_AMD_TRAV=pairs: round 2's walk).
 
 Definitions (one 'trip' = one iteration of the walk loop by one wave with at least one ray):
+  trips_per_ray = lane-trips holding a ray / rays: the trips a ray spends in the walk [k_traverse4]
   busy       = lane-trips holding a ray / (64 x trips)                      [k_traverse4]
   inner_eff  = interior steps / (64 x trips that ran the interior branch)   [k_traverse4]
-  task_eff   = triangle tests / (64 x trips that ran the triangle branch)   [k_traverse4]
+  task_eff   = triangle tests / (64 x K x trips that ran the triangle branch), K triangle tasks
+               per lane                                                       [k_traverse4]
   lane_eff   = useful lane-steps / (64 x branch executions), the two branches weighted by their
                VALU cost (interior step = 1, triangle test = 1): the fraction of the lanes issued
                in the walk's two branches that carried work.  For k_traverse (both branches every
@@ -39,9 +41,12 @@ out = {"walk": "k_traverse4 (quads, leaf tasks)" if quad else "k_traverse (pairs
        "trips_per_wave": round(trips / max(waves, 1), 1),
        "r02_metric": round((inner + tris) / max(trips * rays / max(waves, 1), 1), 3)}
 if quad:
-    out.update({"busy": round(busy / max(64 * trips, 1), 3),
+    # triangle tasks per lane: 2, or 1 where the exact t-cull is on (PT_AMD_WALK_TASKS forces it)
+    K = int(os.environ.get("PT_AMD_WALK_TASKS") or (1 if pt.walk_info()["tcull"] else 2))
+    out.update({"tasks_per_lane": K, "trips_per_ray": round(busy / R, 1),
+                "busy": round(busy / max(64 * trips, 1), 3),
                 "inner_eff": round(inner / max(64 * t_inner, 1), 3),
-                "task_eff": round(tris / max(64 * t_leaf, 1), 3),
+                "task_eff": round(tris / max(64 * K * t_leaf, 1), 3),
                 "lane_eff": round((inner + tris) / max(64 * (t_inner + t_leaf), 1), 3)})
 else:
     out.update({"simd_eff": round((inner + tris) / max(64 * trips, 1), 3),

@@ -1,4 +1,4 @@
-"""The exact t-cull forced on (PT_AMD_TCULL=1) with the device re-walk verification
+"""The exact t-cull forced on (PT_AMD_TCULL=1; TCULL=auto: each scene's default walk) with the device re-walk verification
 (PT_AMD_VERIFY_BOUNDS=1: every mesh ray's record is compared with the reference's node-at-a-time
 BVHIntersectionTest) over >= 1 G segments of config 5 at its benched 3840x2160, then the tessellated
 workload (cull on by default there).  Prints segments and mismatches per pass."""
@@ -8,7 +8,9 @@ import tempfile
 import time
 from pathlib import Path
 os.environ["PT_AMD_VERIFY_BOUNDS"] = "1"
-os.environ["PT_AMD_TCULL"] = "1"
+# TCULL=auto: the walk each scene gets by default (config 5: no cull, two triangle tasks per lane)
+if os.environ.get("TCULL", "1") != "auto":
+    os.environ["PT_AMD_TCULL"] = os.environ.get("TCULL", "1")
 sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
 import cuda_pathtracer_amd as P  # noqa: E402
 from cuda_pathtracer_amd import scenes  # noqa: E402

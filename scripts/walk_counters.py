@@ -19,7 +19,7 @@ groups = tuple(sys.argv[3:]) or ("sq", "stall1", "stall2", "tcp", "ta", "l2", "v
 scene = scenes.random_triangles(out / "scene", n=100_000)
 res = pmc.collect(["1", f"spp={spp}", f"scene={scene}"], out / "pmc", timeout=240, groups=groups)
 summ = {"passes": res["_passes"], "segments": res.get("segments"), "spp": spp}
-for name in ("k_traverse4<false>", "k_traverse<false>", "k_traverse4<true>", "k_traverse<true>"):
+for name in ("k_traverse4<false,", "k_traverse<false>", "k_traverse4<true,", "k_traverse<true>"):   # (k_traverse4<FIRST, K>)
     m = pmc.pick(res, name)
     if not m:
         continue
