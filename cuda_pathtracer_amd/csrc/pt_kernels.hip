@@ -785,7 +785,20 @@ __device__ __forceinline__ Hit intersect_bounded(const SceneDev& S, const FlagsD
             if (G[i].type == PT_GEOM_MESH && mh->id >= G[i].tri_start && mh->id < G[i].tri_end) { mesh_geom = i; break; }
         if (mesh_geom >= 0 && mh->t > 0.0f) { t_min = mh->t; hit_geom = mesh_geom; }
     }
-    if (!plain) {
+#ifndef PT_ONE_GEOM_MASK
+#define PT_ONE_GEOM_MASK 1   // (A/B knob: a wave whose camera-ray mask holds one geom tests it without bounds)
+#endif
+    // A wave whose rays can hit only one geom (the first bounce's camera-ray mask, wave-uniform): that
+    // geom's exact test is the closest hit — the bounds pass would make it the only candidate.
+    const uint32_t gone = gmask & ng_all_mask(S.ngeoms);
+    if (PT_ONE_GEOM_MASK && !PRE && !plain && gone != 0u && (gone & (gone - 1u)) == 0u) {
+        const int gi = __builtin_ctz(gone);
+        int code;
+        f3 obj = F3(0, 0, 0);
+        bool outside;
+        const float t = exact_geom(s_geoms[gi], ro, rd, code, obj, outside);
+        if (t > 0.0f) { t_min = t; hit_geom = gi; best_code = code; best_obj = obj; best_outside = outside; }
+    } else if (!plain) {
         // pass 1: the three smallest lower bounds (scene data wave-uniform: scalar loads)
         float lo1 = kInf, lo2 = kInf, lo3 = kInf;
         int g1 = -1, g2 = -1;
