@@ -932,6 +932,27 @@ def test_render_ahead_claimed_and_dropped_bitexact(cornell_path, room_path, scen
     assert stats[0] == stats[1]   # segments, passes, per-bounce live and emissive counts
 
 
+def test_render_ahead_across_streams(cornell_path):
+    """The iteration traced ahead on one stream and claimed (or dropped) by a pass on another: the
+    claiming pass waits for the ahead work's event, so the image equals the oracle's either way."""
+    import torch
+    from cuda_pathtracer_amd import PathTracer
+    s, o = _pair(cornell_path, (40, 32))
+    pt = PathTracer(s, _gui())
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    ref = None
+    for it in range(1, 7):
+        run_on = sa if it % 2 else sb
+        pt.render_pass(it, run_on)
+        ref, _ = O.render_pass(o, _oflags(_gui()), it, image=ref)
+        nxt = it + 1 if it != 4 else it + 2   # (after 4, iteration 6 is traced ahead: the pass of 5 drops it)
+        pt.render_ahead(nxt, sb if it % 2 else sa)
+    torch.cuda.synchronize()
+    _assert_bitexact(pt.image(), ref, "render-ahead across streams")
+    assert pt.stats()["device_error"] == 0
+    pt.free()
+
+
 def test_render_ahead_needs_one_iteration_context(cornell_path):
     from cuda_pathtracer_amd import PathTracer
     s, _ = _pair(cornell_path, (16, 16))
