@@ -3126,8 +3126,9 @@ __global__ void k_ahead_settle(float* __restrict__ image, const v4f* __restrict_
         }
     }
     if (gid < 66) {   // segments, passes, bounce_live[64]
-        unsigned long long* a = &ast->segments + gid;
-        if (add) (&st->segments)[gid] += *a;
+        unsigned long long* a = gid == 0 ? &ast->segments : (gid == 1 ? &ast->passes : &ast->bounce_live[gid - 2]);
+        unsigned long long* b = gid == 0 ? &st->segments : (gid == 1 ? &st->passes : &st->bounce_live[gid - 2]);
+        if (add) *b += *a;
         *a = 0ull;
     } else if (gid == 66) {
         st->err |= ast->err;
