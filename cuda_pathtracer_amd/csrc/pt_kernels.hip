@@ -1399,6 +1399,8 @@ __device__ __forceinline__ int seg_walk(const int32_t* s_pre, int nseg, int s, i
 constexpr int kMeshInline = 1;   // k_bounce MESH modes: 0 no mesh, 1 traversal inside k_bounce,
 constexpr int kMeshPre = 2;      // 2 closest mesh hit precomputed by k_traverse,
 constexpr int kAnalyticSkip = 3; // 3 no mesh, first bounce: waves with an empty camera mask skip raygen + hit
+constexpr int kAnalyticGM = 4;   // 4 no mesh, more materials than the LDS table holds (read from global memory);
+                                 //   modes 0 and 3 read them from LDS only (no second inlined shade)
 constexpr int kTravChunk = 256;  // rays per ticket grab
 constexpr int kRefillMin = 16;   // idle lanes that trigger a refill
 constexpr int kTravLdsRows = 32; // LDS stack entries per thread (HybStack; the rest in scratch)
@@ -2262,7 +2264,8 @@ __global__ __launch_bounds__(kBlock, FIRST || MESH ? 1 : PT_LATER_WAVES) void k_
         stage_frames(A.S, s_frm);
     }
     stage_materials(A, s_mats);   // (its barrier publishes the staged tables)
-    const bool lds_mats = A.S.nmats <= kLdsMats;
+    // (analytic modes 0 / 3 run only where every material fits the LDS table: launch_bounce)
+    const bool lds_mats = (MESH == 0 || MESH == kAnalyticSkip) ? true : (MESH == kAnalyticGM ? false : A.S.nmats <= kLdsMats);
     const float* frames = ng_lds > 0 ? s_frm : nullptr;
     count_bounce(A, N);
     const int it_base = __builtin_amdgcn_readfirstlane(s_ib[my_it]);
@@ -2285,7 +2288,7 @@ __global__ __launch_bounds__(kBlock, FIRST || MESH ? 1 : PT_LATER_WAVES) void k_
 #endif
     for (int base = first; base < last; base += kBlock, ++k) {
         const int i = base + tid;
-        if (FIRST && MESH == 0 && PT_SKIP_EMPTY_TILES && A.cmask) {
+        if (FIRST && (MESH == 0 || MESH == kAnalyticGM) && PT_SKIP_EMPTY_TILES && A.cmask) {
             // a tile whose four camera-mask blocks are all empty: every ray misses — shade's miss exit
             // (colour 0, no random number) without raygen, closest hit or the tile's ballots and
             // barrier (workgroup-uniform; k stays, so the count buffers keep alternating per barrier)
@@ -3729,7 +3732,12 @@ int mesh_mode(const pt_ctx* c) {
 }
 
 using KernelFn = void (*)(const KArgs);
-KernelFn bounce_kernel(bool first, bool spp1, int mesh, bool skip = false) {   // mesh: 0, kMeshInline, kMeshPre
+KernelFn bounce_kernel(bool first, bool spp1, int mesh, bool skip = false, bool gmats = false) {   // mesh: 0, kMeshInline, kMeshPre
+    if (mesh == 0 && gmats) {   // (more materials than kLdsMats)
+        static const KernelFn gm[4] = {k_bounce<false, false, kAnalyticGM>, k_bounce<false, true, kAnalyticGM>,
+                                       k_bounce<true, false, kAnalyticGM>, k_bounce<true, true, kAnalyticGM>};
+        return gm[(first ? 2 : 0) + (spp1 ? 1 : 0)];
+    }
     if (first && skip && mesh == 0) return spp1 ? k_bounce<true, true, kAnalyticSkip> : k_bounce<true, false, kAnalyticSkip>;
     static const KernelFn table[12] = {
         k_bounce<false, false, 0>, k_bounce<false, false, 1>, k_bounce<false, false, 2>,
@@ -3791,7 +3799,7 @@ int launch_bounce(pt_ctx* c, bool first, bool spp1, int mesh, hipStream_t st, co
         if (int rc = prof_end(ev, st)) return rc;
     }
     if (int rc = prof_begin(c, st, first ? PT_KIND_FIRST_BOUNCE : PT_KIND_BOUNCE, &ev)) return rc;
-    hipLaunchKernelGGL(bounce_kernel(first, spp1, mesh, first && c->cmask_skip), dim3(c->grid_bounce[first]), dim3(kBlock),
+    hipLaunchKernelGGL(bounce_kernel(first, spp1, mesh, first && c->cmask_skip, a.S.nmats > kLdsMats), dim3(c->grid_bounce[first]), dim3(kBlock),
                        bounce_lds_bytes(a.S, mesh), st, a);
     HIP_TRY(hipGetLastError());
     return prof_end(ev, st);
@@ -4318,7 +4326,7 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
     for (int f = 0; f < 2; ++f) {   // k_bounce: any grid is correct; one full wave of equal-work
         int per_cu = 0;              // workgroups avoids a half-empty second wave
         const int mm = A.S.ntris > 0 ? kMeshPre : 0;   // (any grid is correct for either mesh mode)
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bounce_kernel(f, sh.spp == 1, mm), kBlock,
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bounce_kernel(f, sh.spp == 1, mm, false, A.S.nmats > kLdsMats), kBlock,
                                                          bounce_lds_bytes(A.S, mm)) != hipSuccess || per_cu <= 0)
             per_cu = 4;
         // > 2 spp workgroups: the per-iteration layout of k_bounce needs grid - spp >= spp

@@ -449,6 +449,19 @@ def test_sorted_many_materials_bitexact(tmp_path, nmat):
         assert r.sum() > 0
 
 
+@pytest.mark.parametrize("nmat", [70, 200])
+def test_fused_many_materials_bitexact(tmp_path, nmat):
+    """The fused bounce kernel with the materials in its LDS table (70 + the scene's) and with more
+    than the table holds (200: the analytic instantiation that reads them from global memory,
+    k_bounce mode kAnalyticGM), spp 1 and 3, bit-exact against the oracle."""
+    from cuda_pathtracer_amd import Scene, scenes
+    path = scenes.random_primitives(tmp_path, n=120, res=(48, 36), seed=5, extra_materials=nmat)
+    for spp in (1, 3):
+        g, r, _, _ = _run(Scene(path), O.OracleScene.from_json(path), _gui(), iters=3, spp=spp)
+        _assert_bitexact(g, r, f"fused, {nmat} materials, spp={spp}")
+        assert r.sum() > 0
+
+
 @pytest.mark.parametrize("rows", ["1", "3"])
 def test_mesh_traversal_stack_spill_bitexact(room_path, config_scenes, monkeypatch, rows):
     """k_traverse keeps the first PT_AMD_STACK_ROWS stack entries per lane in LDS and the rest in
