@@ -2679,7 +2679,9 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_w, u
 // VERIFY: the PT_AMD_VERIFY_BOUNDS=1 build of the producer (the plain-loop re-run of every closest
 // hit compiled in); the default one carries no diagnostic code (round 4: the later producer's 8-byte
 // register spill went away with it).
-template <bool FIRST, bool SPP1, bool MESH, bool VERIFY>
+// LDSM: every material is in the LDS table (launch: nmats <= kLdsMats), so shading reads it only there
+// (one inlined shade instead of a uniform branch between an LDS and a global-memory copy).
+template <bool FIRST, bool SPP1, bool MESH, bool VERIFY, bool LDSM = false>
 __global__ __launch_bounds__(kBlock, MESH ? 1 : (FIRST ? PT_PRODUCE_WAVES_FIRST : PT_PRODUCE_WAVES))
 void k_sort_produce(const KArgs A, const SortArgs SA) {
     __shared__ DMaterial s_mats[kLdsMats];
@@ -2736,7 +2738,7 @@ void k_sort_produce(const KArgs A, const SortArgs SA) {
     if (!MESH) stage_geoms(A.S, s_geoms);
     if (!MESH && !FIRST) stage_frames(A.S, s_frm);
     stage_materials(A, s_mats);   // (its barrier publishes the staged tables)
-    const bool lds_mats = nmats <= kLdsMats;
+    const bool lds_mats = LDSM || nmats <= kLdsMats;
     const bool lds_geoms = !MESH && A.S.ngeoms <= kLdsGeoms;   // (stage_geoms / stage_frames ran)
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     uint32_t emit_cnt = 0, emit_next = 0;
@@ -3755,7 +3757,15 @@ KernelFn trace_kernel(bool first, bool spp1, bool mesh) {
 }
 
 using SortKernelFn = void (*)(const KArgs, const SortArgs);
-SortKernelFn produce_kernel(bool first, bool spp1, bool mesh, bool verify) {
+SortKernelFn produce_kernel(bool first, bool spp1, bool mesh, bool verify, bool ldsm = false) {
+    if (ldsm && !verify) {
+        static const SortKernelFn lt[8] = {
+            k_sort_produce<false, false, false, false, true>, k_sort_produce<false, false, true, false, true>,
+            k_sort_produce<false, true, false, false, true>,  k_sort_produce<false, true, true, false, true>,
+            k_sort_produce<true, false, false, false, true>,  k_sort_produce<true, false, true, false, true>,
+            k_sort_produce<true, true, false, false, true>,   k_sort_produce<true, true, true, false, true>};
+        return lt[(first ? 4 : 0) + (spp1 ? 2 : 0) + (mesh ? 1 : 0)];
+    }
     static const SortKernelFn table[16] = {
         k_sort_produce<false, false, false, false>, k_sort_produce<false, false, true, false>,
         k_sort_produce<false, true, false, false>,  k_sort_produce<false, true, true, false>,
@@ -4580,7 +4590,8 @@ static int render_pass(pt_ctx* c, int32_t iter_first, hipStream_t st, bool ahead
 #ifndef PT_PRODUCER_ALWAYS_VERIFY
 #define PT_PRODUCER_ALWAYS_VERIFY 0   // (A/B knob: the diagnostic producer build for every run, round 3's form)
 #endif
-            hipLaunchKernelGGL(produce_kernel(first, spp1, mesh, a.fl.verify != 0 || PT_PRODUCER_ALWAYS_VERIFY),
+            hipLaunchKernelGGL(produce_kernel(first, spp1, mesh, a.fl.verify != 0 || PT_PRODUCER_ALWAYS_VERIFY,
+                                              c->nmats <= kLdsMats),
                                dim3(c->grid_bounce[0]), dim3(kBlock),
                                (size_t)16 * c->nmats * sizeof(uint32_t), s, a, sa);
             HIP_TRY(hipGetLastError());
