@@ -921,10 +921,12 @@ __device__ __forceinline__ Hit intersect_bounded(const SceneDev& S, const FlagsD
 // The closest hit of the kernels: bounded for analytic scenes that fit the LDS geom table.
 // CHECK: compiled-in diagnostic re-run (k_trace and the sorted pipeline only, so the fused
 // kernel's code stays small): verify with PT_PIPELINE=split, whose rays are the fused kernel's.
-template <bool MESH, bool CHECK, bool SEL = false>
+// LDSG: the launch guarantees ngeoms <= kLdsGeoms (the geom table is in LDS), so the plain loop over a
+// larger table is not compiled in.
+template <bool MESH, bool CHECK, bool SEL = false, bool LDSG = false>
 __device__ __forceinline__ Hit closest_hit(const SceneDev& S, const FlagsDev& fl, const LGeom* s_geoms, f3 ro, f3 rd,
                                            uint32_t* mismatch, uint32_t gmask = ~0u) {
-    if (MESH || S.ngeoms > kLdsGeoms) return intersect_scene<MESH>(S, fl, ro, rd);
+    if (MESH || (!LDSG && S.ngeoms > kLdsGeoms)) return intersect_scene<MESH>(S, fl, ro, rd);
     const Hit h = intersect_bounded<SEL>(S, fl, s_geoms, ro, rd, nullptr, gmask);
     if (CHECK && fl.verify) {
         const Hit r = intersect_scene<false>(S, fl, ro, rd);
@@ -1399,8 +1401,9 @@ __device__ __forceinline__ int seg_walk(const int32_t* s_pre, int nseg, int s, i
 constexpr int kMeshInline = 1;   // k_bounce MESH modes: 0 no mesh, 1 traversal inside k_bounce,
 constexpr int kMeshPre = 2;      // 2 closest mesh hit precomputed by k_traverse,
 constexpr int kAnalyticSkip = 3; // 3 no mesh, first bounce: waves with an empty camera mask skip raygen + hit
-constexpr int kAnalyticGM = 4;   // 4 no mesh, more materials than the LDS table holds (read from global memory);
-                                 //   modes 0 and 3 read them from LDS only (no second inlined shade)
+constexpr int kAnalyticGM = 4;   // 4 no mesh, more materials or geoms than the LDS tables hold (read from global
+                                 //   memory); modes 0 and 3 read both from LDS only (no second inlined shade,
+                                 //   no plain per-geom loop for a large table)
 constexpr int kTravChunk = 256;  // rays per ticket grab
 constexpr int kRefillMin = 16;   // idle lanes that trigger a refill
 constexpr int kTravLdsRows = 32; // LDS stack entries per thread (HybStack; the rest in scratch)
@@ -2219,7 +2222,8 @@ __global__ __launch_bounds__(kBlock, FIRST || MESH ? 1 : PT_LATER_WAVES) void k_
     // scene tables sized to the scene (dynamic LDS, bounce_lds_bytes): geom rows, then materials
     extern __shared__ __align__(16) uint8_t s_dyn[];
     LGeom* s_geoms = reinterpret_cast<LGeom*>(s_dyn);
-    const int ng_lds = MESH == kMeshInline || A.S.ngeoms > kLdsGeoms ? 0 : A.S.ngeoms;
+    constexpr bool kLdsAll = MESH == 0 || MESH == kAnalyticSkip;   // (launch: materials and geoms fit LDS)
+    const int ng_lds = kLdsAll ? A.S.ngeoms : (MESH == kMeshInline || A.S.ngeoms > kLdsGeoms ? 0 : A.S.ngeoms);
     DMaterial* s_mats = reinterpret_cast<DMaterial*>(s_dyn + ng_lds * sizeof(LGeom));
     float* s_frm = reinterpret_cast<float*>(s_mats + min(A.S.nmats, kLdsMats));   // [ng_lds * 6][6]
     __shared__ int32_t s_pre[FIRST ? 1 : kMaxSeg + 1];
@@ -2381,7 +2385,7 @@ __global__ __launch_bounds__(kBlock, FIRST || MESH ? 1 : PT_LATER_WAVES) void k_
                     const int lp0 = __builtin_amdgcn_readfirstlane(i - it_base);
                     gm = A.cmask[lp0 >> 6];
                 }
-                h = closest_hit<MESH == kMeshInline, false, !FIRST>(A.S, A.fl, s_geoms, p.o, p.d, &A.stats->bound_mismatch, gm);
+                h = closest_hit<MESH == kMeshInline, false, !FIRST, kLdsAll>(A.S, A.fl, s_geoms, p.o, p.d, &A.stats->bound_mismatch, gm);
 #if defined(PT_DUP) && PT_DUP == 7   // diagnostic: the camera ray's closest hit again on an opaque origin
                 if (FIRST) {
                     f3 o2 = p.o;
@@ -2679,8 +2683,9 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_w, u
 // VERIFY: the PT_AMD_VERIFY_BOUNDS=1 build of the producer (the plain-loop re-run of every closest
 // hit compiled in); the default one carries no diagnostic code (round 4: the later producer's 8-byte
 // register spill went away with it).
-// LDSM: every material is in the LDS table (launch: nmats <= kLdsMats), so shading reads it only there
-// (one inlined shade instead of a uniform branch between an LDS and a global-memory copy).
+// LDSM: every material and geom is in the LDS tables (launch: nmats <= kLdsMats, ngeoms <= kLdsGeoms), so
+// shading reads materials only there (one inlined shade instead of a uniform branch between an LDS and a
+// global-memory copy) and the closest hit has no plain loop over a larger geom table.
 template <bool FIRST, bool SPP1, bool MESH, bool VERIFY, bool LDSM = false>
 __global__ __launch_bounds__(kBlock, MESH ? 1 : (FIRST ? PT_PRODUCE_WAVES_FIRST : PT_PRODUCE_WAVES))
 void k_sort_produce(const KArgs A, const SortArgs SA) {
@@ -2739,7 +2744,7 @@ void k_sort_produce(const KArgs A, const SortArgs SA) {
     if (!MESH && !FIRST) stage_frames(A.S, s_frm);
     stage_materials(A, s_mats);   // (its barrier publishes the staged tables)
     const bool lds_mats = LDSM || nmats <= kLdsMats;
-    const bool lds_geoms = !MESH && A.S.ngeoms <= kLdsGeoms;   // (stage_geoms / stage_frames ran)
+    const bool lds_geoms = !MESH && (LDSM || A.S.ngeoms <= kLdsGeoms);   // (stage_geoms / stage_frames ran)
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     uint32_t emit_cnt = 0, emit_next = 0;
     int k = 0, it = 0;
@@ -2861,7 +2866,7 @@ void k_sort_produce(const KArgs A, const SortArgs SA) {
                 gm = A.cmask[lp0 >> 6];
             }
             if (alive) {
-                h = closest_hit<MESH, VERIFY, !FIRST>(A.S, A.fl, s_geoms, p.o, p.d, &A.stats->bound_mismatch, gm);
+                h = closest_hit<MESH, VERIFY, !FIRST, LDSM && !MESH>(A.S, A.fl, s_geoms, p.o, p.d, &A.stats->bound_mismatch, gm);
                 PathReg e = p;   // (only the verdict here; the colour below)
                 ends = lds_mats ? shade_ends(h, s_mats, e) : shade_ends(h, A.S.mats, e);
             }
@@ -3809,7 +3814,8 @@ int launch_bounce(pt_ctx* c, bool first, bool spp1, int mesh, hipStream_t st, co
         if (int rc = prof_end(ev, st)) return rc;
     }
     if (int rc = prof_begin(c, st, first ? PT_KIND_FIRST_BOUNCE : PT_KIND_BOUNCE, &ev)) return rc;
-    hipLaunchKernelGGL(bounce_kernel(first, spp1, mesh, first && c->cmask_skip, a.S.nmats > kLdsMats), dim3(c->grid_bounce[first]), dim3(kBlock),
+    hipLaunchKernelGGL(bounce_kernel(first, spp1, mesh, first && c->cmask_skip, a.S.nmats > kLdsMats || a.S.ngeoms > kLdsGeoms),
+                       dim3(c->grid_bounce[first]), dim3(kBlock),
                        bounce_lds_bytes(a.S, mesh), st, a);
     HIP_TRY(hipGetLastError());
     return prof_end(ev, st);
@@ -4336,7 +4342,7 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
     for (int f = 0; f < 2; ++f) {   // k_bounce: any grid is correct; one full wave of equal-work
         int per_cu = 0;              // workgroups avoids a half-empty second wave
         const int mm = A.S.ntris > 0 ? kMeshPre : 0;   // (any grid is correct for either mesh mode)
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bounce_kernel(f, sh.spp == 1, mm, false, A.S.nmats > kLdsMats), kBlock,
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bounce_kernel(f, sh.spp == 1, mm, false, A.S.nmats > kLdsMats || A.S.ngeoms > kLdsGeoms), kBlock,
                                                          bounce_lds_bytes(A.S, mm)) != hipSuccess || per_cu <= 0)
             per_cu = 4;
         // > 2 spp workgroups: the per-iteration layout of k_bounce needs grid - spp >= spp
@@ -4591,7 +4597,7 @@ static int render_pass(pt_ctx* c, int32_t iter_first, hipStream_t st, bool ahead
 #define PT_PRODUCER_ALWAYS_VERIFY 0   // (A/B knob: the diagnostic producer build for every run, round 3's form)
 #endif
             hipLaunchKernelGGL(produce_kernel(first, spp1, mesh, a.fl.verify != 0 || PT_PRODUCER_ALWAYS_VERIFY,
-                                              c->nmats <= kLdsMats),
+                                              c->nmats <= kLdsMats && a.S.ngeoms <= kLdsGeoms),
                                dim3(c->grid_bounce[0]), dim3(kBlock),
                                (size_t)16 * c->nmats * sizeof(uint32_t), s, a, sa);
             HIP_TRY(hipGetLastError());
