@@ -788,20 +788,17 @@ __device__ __forceinline__ Hit intersect_bounded(const SceneDev& S, const FlagsD
 #ifndef PT_ONE_GEOM_MASK
 #define PT_ONE_GEOM_MASK 1   // (A/B knob: a wave whose camera-ray mask holds one geom tests it without bounds)
 #endif
+    float lo1 = kInf, lo2 = kInf, lo3 = kInf;
+    int g1 = -1, g2 = -1;
+    uint32_t rest = 0u;   // geoms tested after the candidates regardless of bounds
     // A wave whose rays can hit only one geom (the first bounce's camera-ray mask, wave-uniform): that
     // geom's exact test is the closest hit — the bounds pass would make it the only candidate.
     const uint32_t gone = gmask & ng_all_mask(S.ngeoms);
-    if (PT_ONE_GEOM_MASK && !PRE && !plain && gone != 0u && (gone & (gone - 1u)) == 0u) {
-        const int gi = __builtin_ctz(gone);
-        int code;
-        f3 obj = F3(0, 0, 0);
-        bool outside;
-        const float t = exact_geom(s_geoms[gi], ro, rd, code, obj, outside);
-        if (t > 0.0f) { t_min = t; hit_geom = gi; best_code = code; best_obj = obj; best_outside = outside; }
+    const bool one = PT_ONE_GEOM_MASK && !PRE && !plain && gone != 0u && (gone & (gone - 1u)) == 0u;
+    if (one) {
+        g1 = __builtin_ctz(gone);
     } else if (!plain) {
         // pass 1: the three smallest lower bounds (scene data wave-uniform: scalar loads)
-        float lo1 = kInf, lo2 = kInf, lo3 = kInf;
-        int g1 = -1, g2 = -1;
         const float rinf = fmaxf(fmaxf(fabsf(ro.x), fabsf(ro.y)), fabsf(ro.z));
         const f3 invd = F3(__builtin_amdgcn_rcpf(rd.x), __builtin_amdgcn_rcpf(rd.y), __builtin_amdgcn_rcpf(rd.z));
         // one branch-free loop per bound kind (geoms sorted by kind on the host), so the scalar
@@ -861,7 +858,15 @@ __device__ __forceinline__ Hit intersect_bounded(const SceneDev& S, const FlagsD
             if (__float_as_uint(t2) == 0x7f7ffffeu) atomicAdd(&g_dup_sink, 1u);
         }
 #endif
-        // pass 2: exact tests in increasing-bound order while a bound does not exceed the best hit
+    } else if (!PRE) {
+        rest = ng_all_mask(S.ngeoms);   // a direction the bounds do not cover: the reference's loop over every geom
+    }
+    if (PRE && plain) return intersect_scene<PRE, PRE>(S, fl, ro, rd, mh);
+    {   // pass 2, one loop over the candidates (so the kernels carry one inlined exact test): the first;
+        // the second while its bound does not exceed the best hit; then, if the third-smallest bound does
+        // not, every other geom the wave may hit (one with no finite bound misses exactly, so testing it
+        // changes nothing; rare: 0 rays on Cornell and config 4).  The selection is order-independent
+        // (minimum t, lowest index on ties).
         auto take = [&](int gi) {
             int code;
             f3 obj = F3(0, 0, 0);
@@ -871,8 +876,24 @@ __device__ __forceinline__ Hit intersect_bounded(const SceneDev& S, const FlagsD
                 t_min = t; hit_geom = gi; best_code = code; best_obj = obj; best_outside = outside;
             }
         };
-        if (g1 >= 0) take(g1);
-        if (g2 >= 0 && lo2 <= t_min) take(g2);
+        int gi = g1;
+        int stage = (one || plain) ? 2 : 0;
+        uint32_t m = rest;
+        for (;;) {
+            if (gi >= 0) take(gi);
+            if (stage == 0) {
+                stage = 1;
+                if (g2 >= 0 && lo2 <= t_min) { gi = g2; continue; }
+            }
+            if (stage == 1) {
+                stage = 2;
+                m = lo3 <= t_min ? (ng_all_mask(S.ngeoms) & gmask) & ~(1u << g1) & ~(1u << g2) : 0u;
+            }
+            if (m == 0u) break;
+            gi = __builtin_ctz(m);
+            m &= m - 1u;
+        }
+    }
 #ifdef PT_STAMPS
         {
             const uint64_t m2 = __ballot(g2 >= 0 && lo2 <= t_min), m3 = __ballot(lo3 <= t_min);
@@ -889,17 +910,7 @@ __device__ __forceinline__ Hit intersect_bounded(const SceneDev& S, const FlagsD
             }
         }
 #endif
-        if (lo3 <= t_min) {   // a third candidate (rare: 0 rays on Cornell and config 4): the exact test of
-            // every other geom the wave may hit (one with no finite bound misses exactly, so testing it
-            // changes nothing; not tracking the candidate set saves 4 VALU per geom and ray)
-            uint32_t m = (ng_all_mask(S.ngeoms) & gmask) & ~(1u << g1) & ~(1u << g2);
-            while (m) {
-                take(__builtin_ctz(m));
-                m &= m - 1u;
-            }
-        }
-    }
-    if (plain) return intersect_scene<PRE, PRE>(S, fl, ro, rd, mh);
+
     Hit h;
     if (hit_geom < 0) {
         h.t = -1.0f;
