@@ -2223,11 +2223,12 @@ __global__ __launch_bounds__(kBlock, FIRST ? PT_T4_WAVES_FIRST : PT_T4_WAVES) vo
 
 // [raygen] -> intersect -> shade -> segmented compaction (above).
 #ifndef PT_LATER_WAVES
-#define PT_LATER_WAVES 1   // (A/B knob: minimum waves per SIMD of the later-bounce kernels)
+#define PT_LATER_WAVES 8   // (A/B knob: minimum waves per SIMD of the later-bounce kernels)
 #endif
-// At 60 VGPRs the later bounces' occupancy is set by their 106 SGPRs (7 waves per SIMD of 800).
-// PT_LATER_WAVES=8 caps them at 78 SGPRs (8 waves, 2048 workgroups): later bounces 713 -> 708 us
-// but the first bounce running beside them 1567 -> 1604 us, -0.3% overall (same box): not shipped.
+// At ~60 VGPRs the later bounces' occupancy is set by their SGPRs: 106 give 7 waves per SIMD (of 800).
+// 8 waves (SGPRs capped) lost 0.3% in round 4; after round 5's code-size cuts (LDS-only tables, one
+// inlined exact test: 9,473 -> 5,408 ISA lines) they gain: Cornell +0.5%, config 4 +1.5%
+// (profiles/r05_later_waves8_ab.txt).
 template <bool FIRST, bool SPP1, int MESH>
 __global__ __launch_bounds__(kBlock, FIRST || MESH ? 1 : PT_LATER_WAVES) void k_bounce(const KArgs A) {
     // scene tables sized to the scene (dynamic LDS, bounce_lds_bytes): geom rows, then materials
