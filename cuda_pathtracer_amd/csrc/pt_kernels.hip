@@ -2229,8 +2229,12 @@ __global__ __launch_bounds__(kBlock, FIRST ? PT_T4_WAVES_FIRST : PT_T4_WAVES) vo
 // 8 waves (SGPRs capped) lost 0.3% in round 4; after round 5's code-size cuts (LDS-only tables, one
 // inlined exact test: 9,473 -> 5,408 ISA lines) they gain: Cornell +0.5%, config 4 +1.5%
 // (profiles/r05_later_waves8_ab.txt).
+#ifndef PT_FIRST_WAVES
+#define PT_FIRST_WAVES 1   // (A/B knob: minimum waves per SIMD of the analytic first-bounce kernels)
+#endif
 template <bool FIRST, bool SPP1, int MESH>
-__global__ __launch_bounds__(kBlock, FIRST || MESH ? 1 : PT_LATER_WAVES) void k_bounce(const KArgs A) {
+__global__ __launch_bounds__(kBlock, (MESH != 0 && MESH != kAnalyticSkip) ? 1 : (FIRST ? PT_FIRST_WAVES : PT_LATER_WAVES))
+void k_bounce(const KArgs A) {
     // scene tables sized to the scene (dynamic LDS, bounce_lds_bytes): geom rows, then materials
     extern __shared__ __align__(16) uint8_t s_dyn[];
     LGeom* s_geoms = reinterpret_cast<LGeom*>(s_dyn);
