@@ -138,6 +138,7 @@ SIGNATURES = {
     "pt_set_flags": (_I, [_P, C.POINTER(Flags)]),
     "pt_ctx_cmask_info": (_I, [_P, _IP, C.POINTER(C.c_double), _IP]),
     "pt_ctx_counters": (_I, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    "pt_ctx_stream_info": (_I, [_P] + [C.POINTER(C.c_int32)] * 5),
     "pt_ctx_walk_info": (_I, [_P, C.POINTER(_I), C.POINTER(_I), C.POINTER(C.c_double)]),
     "pt_render_pass": (_I, [_P, _I, _P]),
     "pt_render_ahead": (_I, [_P, _I, _P]),

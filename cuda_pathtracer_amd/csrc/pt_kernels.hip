@@ -24,6 +24,7 @@
 
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <cstdio>
 #include <cmath>
 #include <cstdlib>
@@ -3227,6 +3228,15 @@ struct ProfEv {
 
 }  // namespace
 
+// Compute streams held by the live contexts of this process (pt_ctx::busy_streams), against the
+// hardware queues HIP gives one priority level of a process (GPU_MAX_HW_QUEUES, default 4).
+static std::atomic<int> g_busy_streams{0};
+static int stream_budget() {
+    const char* q = std::getenv("GPU_MAX_HW_QUEUES");
+    const int n = q ? std::atoi(q) : 0;
+    return n > 0 ? n : 4;
+}
+
 struct pt_ctx {
     int device = 0;
     int depth = 8;
@@ -3311,11 +3321,17 @@ struct pt_ctx {
     hipStream_t io_stream = nullptr;
     hipEvent_t ev_done = nullptr;
     bool done_recorded = false;
+    hipStream_t done_stream = nullptr;   // the stream ev_done was last recorded on
+    int busy_streams = 0;                // compute streams this context holds (stream budget, below)
+    bool lanes_capped = false;           // pt_create gave it fewer lanes than it would alone
+    hipStream_t pass_stream = nullptr;   // the caller's stream of the last pass or render-ahead
     // Render-ahead (one-iteration contexts, pt_render_ahead): the bounces of iteration ahead_iter,
     // queued before the call that asks for it, keep their colours in ahead_col and their counts in
     // ahead_stats / ahead_emit until pt_render_pass claims them (the same iteration and flags: the
     // colours are added into the image then, as finalGather would) or drops them (anything else).
-    // Every later pass on any stream is ordered after them (ev_ahead).
+    // Ordering, on any mix of streams: an ahead pass first waits for the context's last work
+    // (ev_done: the last pass, claim settle or image call) when that was on another stream, and every
+    // later pass — and the next ahead pass, whose drop settle rewrites ahead_col — waits for ev_ahead.
     v4f* ahead_col = nullptr;
     DevStats* ahead_stats = nullptr;
     unsigned long long* ahead_emit = nullptr;
@@ -3325,13 +3341,14 @@ struct pt_ctx {
     pt_flags ahead_flags{};
 
     ~pt_ctx() {
+        g_busy_streams.fetch_sub(busy_streams);
         for (auto& e : events) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
         for (int h = 0; h < 2; ++h) {
             if (ev_pass[h]) (void)hipEventDestroy(ev_pass[h]);
             if (ev_fin[h]) (void)hipEventDestroy(ev_fin[h]);
         }
         if (fin_stream) (void)hipStreamDestroy(fin_stream);
-        if (io_stream && io_stream != fin_stream) (void)hipStreamDestroy(io_stream);
+        if (io_stream) (void)hipStreamDestroy(io_stream);
         if (ev_done) (void)hipEventDestroy(ev_done);
         if (ev_ahead) (void)hipEventDestroy(ev_ahead);
         if (ev_fork) (void)hipEventDestroy(ev_fork);
@@ -3372,6 +3389,14 @@ int wait_ctx(pt_ctx* c) {
 int mark_ctx(pt_ctx* c, hipStream_t s) {
     HIP_TRY(hipEventRecord(c->ev_done, s));
     c->done_recorded = true;
+    c->done_stream = s;
+    return PT_OK;
+}
+// Work about to be queued on st that shares the context's path buffers, control words or ahead
+// buffers waits for everything the context queued before, when that went to another stream (on
+// the same stream, stream order already holds).
+int order_after_ctx(pt_ctx* c, hipStream_t st) {
+    if (c->done_recorded && c->done_stream != st) HIP_TRY(hipStreamWaitEvent(st, c->ev_done, 0));
     return PT_OK;
 }
 
@@ -4423,14 +4448,19 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
                 (e = hipEventCreateWithFlags(&c->ev_fin[h], hipEventDisableTiming)) != hipSuccess)
                 return bail(pt::fail(PT_ERR_HIP, std::string("hipEventCreate: ") + hipGetErrorString(e)));
     }
-    // The synchronous entry points' copies: on the finalize stream when the context has one (they wait
-    // for the context's last work first, so it is idle then), else on a stream of their own.  Not one
-    // more stream beside the lanes: HIP maps the streams of a process onto GPU_MAX_HW_QUEUES (4)
-    // hardware queues, and a fifth stream made two of config 3's three lanes share one (35.6k vs
-    // 39.6k Mray/s: their launches then ran in submission order).
-    if (c->fin_stream) c->io_stream = c->fin_stream;
-    else if ((e = hipStreamCreateWithFlags(&c->io_stream, hipStreamNonBlocking)) != hipSuccess)
-        return bail(pt::fail(PT_ERR_HIP, std::string("context stream: ") + hipGetErrorString(e)));
+    // The synchronous entry points' copies run on a stream of their own at the greatest priority.
+    // HIP maps the streams of a process onto GPU_MAX_HW_QUEUES (4) hardware queues PER PRIORITY, and
+    // streams beyond that share a queue and run in submission order: a fifth normal-priority stream
+    // made two of config 3's three lanes share one (35.6k vs 39.6k Mray/s), and a copy stream that
+    // shares a queue with another context's busy stream waits behind its passes.  The high-priority
+    // pool holds only these copy streams, so they take no queue from the compute streams and no
+    // compute stream can sit in front of them.
+    {
+        int least = 0, greatest = 0;
+        if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) greatest = 0;
+        if ((e = hipStreamCreateWithPriority(&c->io_stream, hipStreamNonBlocking, greatest)) != hipSuccess)
+            return bail(pt::fail(PT_ERR_HIP, std::string("context stream: ") + hipGetErrorString(e)));
+    }
     c->max_tiles = (int)((P + kCompactTile - 1) / kCompactTile);   // k_compact_paths tiles
     if (int rc = c->alloc(&A.flags, (size_t)P)) return bail(rc);
     if (int rc = c->alloc(&A.ctl, 2)) return bail(rc);
@@ -4454,7 +4484,17 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
         const bool walk = c->flags.sort_by_material == 0 && mesh_mode(c) == kMeshPre && c->trav_quads &&
                           c->flags.bvh_cull == 0;   // (the pair walk with bvh_cull: 790 at two lanes vs 730 at one)
         const int want = lv ? std::max(1, std::min(kMaxLanes, std::atoi(lv))) : (three ? 3 : (walk ? 1 : 2));
-        const int L = std::min(want, sh.spp);
+        int L = std::min(want, sh.spp);
+        // Stream budget: a batched context keeps the caller's stream, L - 1 lane streams and the
+        // finalize stream busy.  Unless PT_AMD_LANES asks for a count, the lanes are capped so that the
+        // busy streams of all live contexts stay within the hardware queues (stream_budget()): lanes
+        // beyond it would share queues with other contexts' streams and serialise behind them.
+        if (!lv && L > 1) {
+            const int room = stream_budget() - g_busy_streams.load() - 2;   // - caller - finalize
+            const int capped = std::max(1, std::min(L, room + 1));
+            c->lanes_capped = capped < L;
+            L = capped;
+        }
         if (L >= 2) {
             if ((e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming)) != hipSuccess)
                 return bail(pt::fail(PT_ERR_HIP, std::string("lane setup: ") + hipGetErrorString(e)));
@@ -4480,6 +4520,8 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
             c->lanes = L;
         }
     }
+    c->busy_streams = 1 + (c->lanes - 1) + (c->fin_stream ? 1 : 0);   // caller + lanes + finalize
+    g_busy_streams.fetch_add(c->busy_streams);
     if ((e = hipMemset(A.image, 0, (size_t)npix * 3 * sizeof(float))) != hipSuccess ||
         (e = hipMemset(A.ctl, 0, 2 * sizeof(Ctl))) != hipSuccess ||
         (e = hipMemset(A.seg, 0, (size_t)2 * kMaxSeg * sizeof(int32_t))) != hipSuccess ||
@@ -4565,6 +4607,17 @@ int pt_ctx_cmask_info(const pt_ctx* c, int32_t* on, double* empty_frac, int32_t*
     if (on) *on = c->args.cmask != nullptr ? 1 : 0;
     if (empty_frac) *empty_frac = c->cmask_empty;
     if (skip_fused) *skip_fused = c->cmask_skip ? 1 : 0;
+    return PT_OK;
+}
+
+int pt_ctx_stream_info(const pt_ctx* c, int32_t* lanes, int32_t* busy_streams, int32_t* process_busy,
+                       int32_t* hw_queues, int32_t* lanes_capped) {
+    if (!c) return pt::fail(PT_ERR_ARG, "null context");
+    if (lanes) *lanes = c->lanes;
+    if (busy_streams) *busy_streams = c->busy_streams;
+    if (process_busy) *process_busy = g_busy_streams.load();
+    if (hw_queues) *hw_queues = stream_budget();
+    if (lanes_capped) *lanes_capped = c->lanes_capped ? 1 : 0;
     return PT_OK;
 }
 
@@ -4776,6 +4829,12 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
     if (!c) return pt::fail(PT_ERR_ARG, "null context");
     if (iter_first < 0) return pt::fail(PT_ERR_ARG, "iteration index must be >= 0");
     hipStream_t st = (hipStream_t)stream;
+    // A pass on another stream than the previous one first waits for all of the context's queued
+    // work (its lanes and finalize included); consecutive passes on one stream keep their overlap
+    // (the next pass starts during the previous one's finalize tail).
+    if (c->pass_stream && c->pass_stream != st)
+        if (int rc = order_after_ctx(c, st)) return rc;
+    c->pass_stream = st;
     if (c->ahead_recorded) {
         HIP_TRY(hipStreamWaitEvent(st, c->ev_ahead, 0));   // its path buffers, counts and colours
         if (c->ahead_valid) {
@@ -4793,11 +4852,24 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream) {
 }
 
 // The bounces of iteration `iter` queued now, for the pt_render_pass(iter) that follows (pt_amd.h).
+static int render_ahead(pt_ctx* c, int32_t iter, hipStream_t st);
 int pt_render_ahead(pt_ctx* c, int32_t iter, void* stream) {
     if (!c) return pt::fail(PT_ERR_ARG, "null context");
     if (iter < 0) return pt::fail(PT_ERR_ARG, "iteration index must be >= 0");
     if (c->args.tile.spp != 1) return pt::fail(PT_ERR_ARG, "render-ahead needs a context of one iteration per pass");
-    hipStream_t st = (hipStream_t)stream;
+    const int rc = render_ahead(c, iter, (hipStream_t)stream);
+    if (rc != PT_OK) {
+        // A caller may treat a failed render-ahead as a lost overlap only (host/pathtrace.cpp): nothing
+        // is left to claim, later passes still order after whatever was queued, and the HIP last-error
+        // is cleared so the next pass's launch check does not report this failure.
+        c->ahead_valid = false;
+        if (c->ev_ahead && hipEventRecord(c->ev_ahead, (hipStream_t)stream) == hipSuccess) c->ahead_recorded = true;
+        (void)hipGetLastError();
+    }
+    return rc;
+}
+
+static int render_ahead(pt_ctx* c, int32_t iter, hipStream_t st) {
     if (!c->ev_ahead) {   // first use: the ahead buffers
         const size_t nemit = (size_t)64 * c->args.emit_stride;
         if (int rc = c->alloc(&c->ahead_col, (size_t)c->args.tile.P)) return rc;
@@ -4808,6 +4880,10 @@ int pt_render_ahead(pt_ctx* c, int32_t iter, void* stream) {
         HIP_TRY(hipStreamSynchronize(c->io_stream));
         HIP_TRY(hipEventCreateWithFlags(&c->ev_ahead, hipEventDisableTiming));
     }
+    // the context's last pass (its path buffers, control and segment words, tickets) and the last
+    // claim's settle (which reads ahead_col) may still run on another stream
+    if (int rc = order_after_ctx(c, st)) return rc;
+    c->pass_stream = st;
     if (c->ahead_recorded) {
         HIP_TRY(hipStreamWaitEvent(st, c->ev_ahead, 0));
         if (c->ahead_valid)
@@ -4868,7 +4944,13 @@ int pt_get_accum(pt_ctx* c, float* host_rgb) { return pt_get_image(c, host_rgb);
 
 int pt_host_register(void* host, uint64_t bytes) {
     if (!host || !bytes) return pt::fail(PT_ERR_ARG, "null argument");
-    HIP_TRY(hipHostRegister(host, (size_t)bytes, hipHostRegisterDefault));
+    const hipError_t e = hipHostRegister(host, (size_t)bytes, hipHostRegisterDefault);
+    if (e != hipSuccess) {
+        // a caller may go on without the page lock (the copies still work, staged): leave no sticky
+        // last-error behind for the next launch's hipGetLastError check to report
+        (void)hipGetLastError();
+        return pt::fail(PT_ERR_DEVICE, std::string("hipHostRegister: ") + hipGetErrorString(e));
+    }
     return PT_OK;
 }
 

@@ -301,6 +301,15 @@ class PathTracer:
         check_pt(lib().pt_ctx_counters(self._h, C.byref(b), C.byref(y)))
         return {"mask_builds": int(b.value), "flag_syncs": int(y.value)}
 
+    def stream_info(self) -> dict:
+        """Stream budget (pt_ctx_stream_info): the context's lanes and busy streams, the busy streams
+        of every live context of the process, the hardware queues per priority, and whether pt_create
+        capped the lanes to stay within them."""
+        v = [C.c_int32() for _ in range(5)]
+        check_pt(lib().pt_ctx_stream_info(self._h, *[C.byref(x) for x in v]))
+        k = ("lanes", "busy_streams", "process_busy", "hw_queues", "lanes_capped")
+        return {a: int(x.value) for a, x in zip(k, v)}
+
     def cmask_info(self) -> dict:
         """First-bounce camera masks (pt_ctx_cmask_info): built, share of empty 64-pixel blocks, and
         whether the fused first bounce skips those waves in its own instantiation."""

@@ -251,13 +251,28 @@ int pt_ctx_cmask_info(const pt_ctx* c, int32_t* on, double* empty_frac, int32_t*
  * the share of the layout's slots whose cull margin can pay.  The cull is on when
  * that share is >= 1/4 (PT_AMD_TCULL=0/1 forces it); it never changes a result. */
 int pt_ctx_walk_info(const pt_ctx* c, int32_t* quad_walk, int32_t* tcull_on, double* tcull_frac);
+/* Stream budget.  HIP maps a process's streams of one priority onto GPU_MAX_HW_QUEUES (default 4)
+ * hardware queues; streams beyond that share queues and their work runs in submission order.  A
+ * context keeps busy: the caller's stream, one stream per extra lane of a batched pass, and the
+ * finalize stream of a batched pass.  pt_create caps the lanes it picks by itself so that the busy
+ * streams of all live contexts stay within GPU_MAX_HW_QUEUES (PT_AMD_LANES overrides the choice and
+ * the cap).  The synchronous entry points copy on a high-priority stream of the context's own, a
+ * pool of queues apart from the compute streams.  So one context's passes never wait for another's,
+ * and its synchronous reads never queue behind another's passes, while the process's busy
+ * normal-priority streams — the library's and the caller's own (torch's stream pool, say) — are at
+ * most GPU_MAX_HW_QUEUES; past that, contexts share queues and may serialise (still correct).
+ * pt_ctx_stream_info: the context's lanes, its busy streams, the sum over the live contexts, the
+ * budget, and whether its lanes were capped. */
+int pt_ctx_stream_info(const pt_ctx* c, int32_t* lanes, int32_t* busy_streams, int32_t* process_busy,
+                       int32_t* hw_queues, int32_t* lanes_capped);
 /* One pass: iterations [iter_first, iter_first + spp) for this tile, accumulated into the tile
  * image.  Asynchronous on `stream`; no host synchronisation inside.  A batched pass (spp > 1)
  * runs its iterations in lanes on internal streams and adds their colours into the image on a
  * finalize stream; `stream` itself is not made to wait for every lane (the next pass starts during
  * this one's tail).  Read the image through pt_copy_image / pt_preview_rgba / pt_reset_image (they
- * wait for the last finalize on their stream) or the synchronising calls; issue the passes of one
- * context on one stream, or synchronise between streams. */
+ * wait for the last finalize on their stream) or the synchronising calls.  Passes of one context
+ * may go to different streams: a pass on another stream than the previous pass first waits (on the
+ * device) for all of the context's queued work; passes on one stream keep their overlap. */
 int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream);
 /* Render-ahead for a one-iteration context (spp 1; the drop-in pathtrace() loop): queues the bounces
  * of iteration `iter` on `stream` now, without touching the image, so they run while the caller
@@ -265,7 +280,10 @@ int pt_render_pass(pt_ctx* c, int32_t iter_first, void* stream);
  * with the same flags claims them and only adds their colours into the image (the same bits as
  * rendering then); any other pass — another iteration, changed flags — drops them first.  Counts
  * (pt_stats) include an iteration once it is claimed.  Not synchronising; pt_get_image and the
- * other synchronising calls do not wait for unclaimed ahead work. */
+ * other synchronising calls do not wait for unclaimed ahead work.  Ordering on any streams: the
+ * ahead work waits (on the device) for the context's last pass, claim or image call when that went
+ * to another stream, and every later pass or ahead waits for the ahead work.  On failure nothing is
+ * left to claim and the HIP last-error is cleared (the caller may go on without the overlap). */
 int pt_render_ahead(pt_ctx* c, int32_t iter, void* stream);
 /* sendImageToPBO (pathtrace.cu:64-86) for the tile: d_rgba = npix * 4 bytes on the device. */
 int pt_preview_rgba(pt_ctx* c, int32_t iter, uint8_t* d_rgba, void* stream);

@@ -946,23 +946,62 @@ def test_render_ahead_claimed_and_dropped_bitexact(cornell_path, room_path, scen
 
 
 def test_render_ahead_across_streams(cornell_path):
-    """The iteration traced ahead on one stream and claimed (or dropped) by a pass on another: the
-    claiming pass waits for the ahead work's event, so the image equals the oracle's either way."""
+    """Render-ahead and passes of one context on two streams, arranged so that any missing
+    cross-stream ordering overlaps or reorders shared work on the device (not by host timing):
+
+    * race A — an ahead pass on stream B while passes still run on stream A (they share the path
+      buffers, control and segment words): six 800x800 passes are queued on A, and B is released by
+      an event recorded after the FIRST of them, so an unordered ahead pass would start exactly when
+      pass 2 starts;
+    * race B — the next ahead pass on B while the claim's settle on A still reads ahead_col: A sleeps
+      (a 20+ ms device spin) before the claim, so an unordered ahead would rewrite ahead_col first;
+    * alternating plain passes — pass i on A behind a device spin, pass i + 1 on B.
+
+    The image must equal the oracle's sequential render bit for bit, and the per-bounce counts the
+    oracle's; pt_render_ahead waits for the context's last work on another stream (ev_done) and a
+    pass on a new stream waits for all of it."""
     import torch
     from cuda_pathtracer_amd import PathTracer
-    s, o = _pair(cornell_path, (40, 32))
+    s, o = _pair(cornell_path, (800, 800))
     pt = PathTracer(s, _gui())
     sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
-    ref = None
+    spin = int(5e7)   # torch's bounded device spin (clock cycles): tens of milliseconds
+    ref, live_ref = None, [0] * o.depth
+
+    def oracle(it):
+        nonlocal ref, live_ref
+        ref, live = O.render_pass(o, _oflags(_gui()), it, image=ref)
+        live_ref = [a + b for a, b in zip(live_ref, live)]
+
+    # race A
+    first_done = torch.cuda.Event()
     for it in range(1, 7):
-        run_on = sa if it % 2 else sb
-        pt.render_pass(it, run_on)
-        ref, _ = O.render_pass(o, _oflags(_gui()), it, image=ref)
-        nxt = it + 1 if it != 4 else it + 2   # (after 4, iteration 6 is traced ahead: the pass of 5 drops it)
-        pt.render_ahead(nxt, sb if it % 2 else sa)
+        pt.render_pass(it, sa)
+        if it == 1:
+            first_done.record(sa)
+    sb.wait_event(first_done)
+    pt.render_ahead(7, sb)
+    pt.render_pass(7, sa)   # claims 7
+    # race B
+    pt.render_ahead(8, sb)
+    with torch.cuda.stream(sa):
+        torch.cuda._sleep(spin)
+    pt.render_pass(8, sa)   # claims 8: its settle reads ahead_col after the spin
+    pt.render_ahead(9, sb)  # must not rewrite ahead_col before that settle
+    pt.render_pass(9, sa)   # claims 9
+    # alternating plain passes
+    for it in range(10, 14):
+        st = sa if it % 2 == 0 else sb
+        with torch.cuda.stream(st):
+            torch.cuda._sleep(spin // 4)
+        pt.render_pass(it, st)
     torch.cuda.synchronize()
-    _assert_bitexact(pt.image(), ref, "render-ahead across streams")
-    assert pt.stats()["device_error"] == 0
+    for it in range(1, 14):
+        oracle(it)
+    _assert_bitexact(pt.image(), ref, "render-ahead and passes across streams")
+    st = pt.stats()
+    assert st["device_error"] == 0
+    assert st["bounce_live"] == live_ref
     pt.free()
 
 
@@ -1143,23 +1182,82 @@ def test_sorted_paths_that_all_end_early(cornell_path, spp, look):
         assert r.sum() > 0 and live[1] < live[0]
 
 
-def test_context_synchronisation_is_scoped():
-    """pt_get_image / pt_stats wait for their own context only (an event after its last pass, copies
-    on a non-blocking stream of the context's own), not for the device: with long batched passes of
-    another context queued, a small context's image and statistics are read while those passes are
-    still running (checked with an event queued after them), and both images stay bit-exact.
-    Run in a fresh process (tests/ctx_sync_worker.py): HIP maps a process's streams onto 4 hardware
-    queues (GPU_MAX_HW_QUEUES) and streams beyond that share queues in submission order, so the test
-    keeps its own streams the only ones on the device."""
-    import json
-    import subprocess
-    import sys
-    from pathlib import Path
-    worker = Path(__file__).resolve().parent / "ctx_sync_worker.py"
-    res = subprocess.run([sys.executable, str(worker)], capture_output=True, text=True, timeout=240)
-    assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-3000:]
-    r = json.loads(res.stdout.strip().splitlines()[-1])
-    assert r["first_ok"] and r["second_ok"], r
-    assert r["small_live0"] == 32 * 24 and r["small_err"] == 0, r
-    assert r["big_live0"] == 9 * 64 * 800 * 800 and r["big_err"] == 0, r
-    assert r["running"], f"the small context's reads waited for the other context: {r}"
+def test_context_synchronisation_is_scoped(cornell_path):
+    """pt_get_image / pt_stats wait for their own context only (an event after its last pass) and
+    copy on a high-priority stream of the context's own, so with long batched passes of another
+    context queued, a small context's image and statistics are read while those passes still run
+    (an event queued after them is still pending), and both stay bit-exact.  Runs inside the pytest
+    process, whose earlier tests left torch streams behind: HIP gives each priority level of a
+    process its own GPU_MAX_HW_QUEUES hardware queues, and the copy stream's level holds only copy
+    streams, so no compute stream — the library's, torch's or the caller's — can sit in front of it
+    (include/pt_amd.h, stream budget).  The stream accounting of both contexts is checked too."""
+    import time
+    import torch
+    from cuda_pathtracer_amd import GuiDataContainer, PathTracer, Scene
+    s = Scene(cornell_path)
+    s.set_camera((32, 24), 45.0, (0, 5, 10.5), (0, 5, 0), (0, 1, 0))
+    s.finalize()
+    o = O.OracleScene.from_json(cornell_path)
+    o.set_camera((32, 24), 45.0, (0, 5, 10.5), (0, 5, 0), (0, 1, 0))
+    small = PathTracer(s, GuiDataContainer())
+    small.render_pass(1)
+    ref, _ = O.render_pass(o, O.flags(), 1)
+    _assert_bitexact(small.image(), ref, "small context before")
+    big = PathTracer(Scene(cornell_path), GuiDataContainer(), spp=64)
+    si_small, si_big = small.stream_info(), big.stream_info()
+    # the big context: caller + lanes + finalize; both contexts' busy streams within the budget
+    assert si_small["busy_streams"] == 1 and si_small["lanes"] == 1, si_small
+    assert si_big["busy_streams"] == 1 + (si_big["lanes"] - 1) + 1, si_big
+    assert si_big["process_busy"] >= si_small["busy_streams"] + si_big["busy_streams"], (si_small, si_big)
+    big.render_pass(1)                    # warm-up pass (first launches, code objects)
+    big.stats()
+    ev = torch.cuda.Event()
+    t0 = time.perf_counter()
+    for k in range(1, 9):                 # 8 x 64 iterations of 800x800: tens of ms of GPU work
+        big.render_pass(1 + 64 * k)
+    ev.record()
+    img = small.image()
+    st = small.stats()
+    t_small = time.perf_counter() - t0
+    running = not ev.query()
+    torch.cuda.synchronize()
+    t_big = time.perf_counter() - t0
+    bst = big.stats()
+    big.free()
+    small.free()
+    _assert_bitexact(img, ref, "small context read during the other context's passes")
+    assert st["bounce_live"][0] == 32 * 24 and st["device_error"] == 0, st
+    assert bst["bounce_live"][0] == 9 * 64 * 800 * 800 and bst["device_error"] == 0, bst
+    assert running, (f"the small context's reads waited for the other context "
+                     f"({t_small * 1e3:.2f} of {t_big * 1e3:.2f} ms; streams {si_small} {si_big})")
+
+
+def test_lanes_capped_by_stream_budget(cornell_path, monkeypatch):
+    """pt_create caps the lanes it picks by itself so that the busy streams of the live contexts stay
+    within GPU_MAX_HW_QUEUES: with a budget of 4, a 2-lane batched context holds 3 (caller, lane,
+    finalize), so a second one gets 1 lane (2 more streams, not 3); freeing both gives a third
+    context its 2 lanes back.  The capped context still renders bit-exact."""
+    import gc
+    from cuda_pathtracer_amd import PathTracer
+    gc.collect()   # (contexts of earlier tests not yet freed)
+    monkeypatch.delenv("PT_AMD_LANES", raising=False)
+    s, o = _pair(cornell_path, (40, 32))
+    probe = PathTracer(s, _gui())
+    base = probe.stream_info()["process_busy"] - 1   # busy streams of other live contexts, if any
+    probe.free()
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", str(4 + base))
+    a = PathTracer(s, _gui(), spp=4)
+    ia = a.stream_info()
+    assert ia["lanes"] == 2 and ia["busy_streams"] == 3 and not ia["lanes_capped"], ia
+    b = PathTracer(s, _gui(), spp=4)
+    ib = b.stream_info()
+    assert ib["lanes"] == 1 and ib["lanes_capped"] and ib["process_busy"] == base + ia["busy_streams"] + 2, ib
+    b.render_pass(1)
+    ref, _ = O.render_pass(o, _oflags(_gui()), 1, spp=4)
+    _assert_bitexact(b.image(), ref, "lane-capped context")
+    a.free()
+    b.free()
+    c = PathTracer(s, _gui(), spp=4)
+    ic = c.stream_info()
+    assert ic["lanes"] == 2 and not ic["lanes_capped"] and ic["process_busy"] == base + 3, ic
+    c.free()
