@@ -510,9 +510,14 @@ def main() -> None:
     live = [b - a for a, b in zip(s0["bounce_live"], s1["bounce_live"])]
     t_max = elapsed
     seg_all = seg
+    ranks = None
     if dist is not None:
         t_max = D.max_over_ranks(torch, dist, elapsed, dev)
         seg_all = D.sum_over_ranks(torch, dist, seg, dev)
+        # per-rank elapsed time and segments (min, max, spread): an imbalanced N-GPU line is
+        # diagnosable from the line itself
+        ranks = D.rank_spread(D.per_rank(torch, dist, (elapsed, seg), dev))
+        ranks["gather_ms_per_rank"] = [r[0] for r in D.per_rank(torch, dist, (gather_ms,), dev)]
 
     # roofline of the dominant kernel (bounces >= 1), over the profiled segment
     depth = st_r.traceDepth
@@ -607,6 +612,8 @@ def main() -> None:
             assert gather_ms is not None and gather_ms_min is not None, "N > 1: the tile gather was not timed"
             assert seg_all >= seg > 0 and rows_all is not None and len(rows_all) == world, \
                 "N > 1: per-rank segment sums or gathered tiles missing"
+            assert ranks is not None and len(ranks["segments"]) == world and sum(ranks["segments"]) == seg_all \
+                and abs(ranks["elapsed_max_s"] - t_max) < 1e-9, "N > 1: per-rank diagnostics inconsistent"
         value = seg_all / t_max / 1e6
         strong = args.scaling == "strong"
         desc = (f"cornell.json 800x800 DEPTH 8 default flags; a step = {args.samples} samples per pixel of the whole "
@@ -647,6 +654,7 @@ def main() -> None:
             "first_bounce_avg_ms": f_ms / max(f_n, 1),
             "gather_ms": gather_ms,
             "gather_ms_last_rank": gather_ms_min,
+            "ranks": ranks,
         }
         if not args.no_scan:
             result["scan"] = scan_bench(torch, dev, args.scan_n, args.scan_reps)

@@ -162,6 +162,11 @@ struct DGeom {
     // normals (interactions.cu:23-33: p1 = normalize(cross(n, dnn)), p2 = normalize(cross(n, p1))),
     // also a function of (geom, code) only: frm[code] = (p1, p2), evaluated once by pt_create.
     float frm[6][6];
+    // bkind 3: the widened world box with each axis's two planes side by side, (wlo[k], whi[k]) at
+    // wbox[2k], so one packed f32 operation (v_pk_add_f32 / v_pk_mul_f32, IEEE per component) takes
+    // both planes of an axis from one SGPR pair (pt_kernels.hip slab2)
+    float wbox[6];
+    float pad_[2];
 };
 
 struct DMaterial {   // == pt_material

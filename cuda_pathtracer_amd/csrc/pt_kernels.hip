@@ -631,6 +631,38 @@ __device__ __forceinline__ void stage_geoms(const SceneDev& S, LGeom* s_geoms) {
     }
 }
 
+// World-box cubes (bkind 3) in packed f32 operations: both planes of an axis, ((lo - o) * r,
+// (hi - o) * r), in one v_pk_add_f32 and one v_pk_mul_f32 (<2 x float> operations; IEEE per
+// component, the same bits as two subtractions and two multiplications), the box pair from the
+// geom's SGPRs (wbox).  The bound is bound_geom<3>'s (below) bit for bit, returned TAGGED (tag_bound).
+// With E0 = max(E, 0), "E > X || X < 0" is "E0 > X" (NaN slabs included: both are false for a NaN X,
+// and a NaN E gives E0 = 0).
+__device__ __forceinline__ uint32_t tag_bound(float v, uint32_t i);
+template <class G>
+__device__ __forceinline__ uint32_t bound_wbox_tagged(const G& g, f3 o, f3 r, float rl, uint32_t i) {
+    const v2f tx = ((v2f){g.wbox[0], g.wbox[1]} - (v2f){o.x, o.x}) * (v2f){r.x, r.x};
+    const v2f ty = ((v2f){g.wbox[2], g.wbox[3]} - (v2f){o.y, o.y}) * (v2f){r.y, r.y};
+    const v2f tz = ((v2f){g.wbox[4], g.wbox[5]} - (v2f){o.z, o.z}) * (v2f){r.z, r.z};
+    const float E0 = fmaxf(fmaxf(fminf(tx.x, tx.y), fminf(ty.x, ty.y)), fmaxf(fminf(tz.x, tz.y), 0.0f));
+    const float X = fminf(fminf(fmaxf(tx.x, tx.y), fmaxf(ty.x, ty.y)), fmaxf(tz.x, tz.y));
+    const float v = fmaxf(E0 * rl - g.back, 0.0f) * g.tslack;
+    // a miss ORs in the exponent of +inf: the result is then >= +inf's bits (no candidate) with no
+    // branch around the tag, so the geom loop's scalar loads are not split by one
+    return tag_bound(v, i) | (E0 > X ? 0x7f800000u : 0u);
+}
+
+// A bound v >= 0 (or +0 / -0) with geom index i in its low 5 bits, as the bits of a float that is
+// <= v: max(bits, 32) - 32 with the low 5 bits replaced by i (at most 32 ulp below v; +-0 become
+// the denormal i * 2^-149, which is below every later comparison's rounding: the scene's absolute
+// slack is subtracted before any use, and fl(tag - slack) = fl(0 - slack)).  Non-negative floats
+// order as their bits, so the pass keeps the three smallest with integer min / median operations,
+// and the index of a candidate is its low bits.  Bits >= +inf's (+inf, or a miss's tag with the
+// exponent ORed in: a NaN pattern, which every later comparison rejects) mean no candidate.
+__device__ __forceinline__ uint32_t tag_bound(float v, uint32_t i) {
+    const uint32_t b = (uint32_t)(max((int32_t)__float_as_uint(v), 32) - 32);
+    return (b & ~31u) | i;
+}
+
 // Lower bound on the exact test's world distance for geom g (before the scene's absolute slack),
 // +inf when the exact test surely misses.  Rounding here is irrelevant: only the widened bounds,
 // the relative slack and the comparisons' direction matter (NaNs fall through to "candidate").
@@ -806,23 +838,31 @@ __device__ __forceinline__ Hit intersect_bounded(const SceneDev& S, const FlagsD
         // loads of the next geom need not wait for this one's kind; the candidates' identity and
         // order do not matter to the result (pass 2 below), only the set of bounds
         const auto* B = as_const(S.bgeoms);
-        auto insert = [&](float lo, int i) {
-            lo -= S.abs_slack;
-            const bool c1 = lo < lo1, c2 = lo < lo2, c3 = lo < lo3;
-            lo3 = c2 ? lo2 : (c3 ? lo : lo3);
-            lo2 = c1 ? lo1 : (c2 ? lo : lo2);
-            g2 = c1 ? g1 : (c2 ? i : g2);
-            lo1 = c1 ? lo : lo1;
-            g1 = c1 ? i : g1;
+        // the three smallest bounds, as tagged bits (tag_bound): u1 <= u2 <= u3, the geoms of the first
+        // two in their low bits.  The scene's absolute slack is subtracted from the three after the pass:
+        // x - c rounds monotonically, so they are the three smallest slackened bounds; a tie that the
+        // subtraction (or the tag) creates between two geoms only swaps which one pass 2 tests first —
+        // both are tested (the first hit's t is >= the tied bound), and the selection is order-independent.
+        uint32_t u1 = 0x7f800000u, u2 = 0x7f800000u, u3 = 0x7f800000u;
+        auto insert_tagged = [&](uint32_t t) {   // (medians: u1 <= u2 <= u3)
+            u3 = min(u3, max(u2, t));
+            u2 = min(u2, max(u1, t));
+            u1 = min(u1, t);
         };
-        for (int j = S.bk[3]; j < S.bk[4]; ++j)
-            if ((gmask >> B[j].orig) & 1u) insert(bound_geom<3, SEL>(B[j], ro, rd, invd, rl, rinf), B[j].orig);
+        auto insert = [&](float lo, int i) { insert_tagged(lo == kInf ? 0x7f800000u : tag_bound(lo, (uint32_t)i)); };
+        for (int j = S.bk[3]; j < S.bk[4]; ++j)   // world-box cubes: packed slabs
+            if ((gmask >> B[j].orig) & 1u) insert_tagged(bound_wbox_tagged(B[j], ro, invd, rl, (uint32_t)B[j].orig));
         for (int j = S.bk[4]; j < S.bk[5]; ++j)
             if ((gmask >> B[j].orig) & 1u) insert(bound_geom<4, SEL>(B[j], ro, rd, invd, rl, rinf), B[j].orig);
         for (int j = S.bk[1]; j < S.bk[2]; ++j)
             if ((gmask >> B[j].orig) & 1u) insert(bound_geom<1, SEL>(B[j], ro, rd, invd, rl, rinf), B[j].orig);
         for (int j = S.bk[2]; j < S.bk[3]; ++j)
             if ((gmask >> B[j].orig) & 1u) insert(bound_geom<2, SEL>(B[j], ro, rd, invd, rl, rinf), B[j].orig);
+        g1 = u1 >= 0x7f800000u ? -1 : (int)(u1 & 31u);
+        g2 = u2 >= 0x7f800000u ? -1 : (int)(u2 & 31u);
+        lo1 = __uint_as_float(u1) - S.abs_slack;
+        lo2 = __uint_as_float(u2) - S.abs_slack;
+        lo3 = __uint_as_float(u3) - S.abs_slack;
 #if defined(PT_DUP) && PT_DUP == 4   // diagnostic: the bounds pass again on an opaque origin
         if (SEL) {
             f3 r2 = ro;
@@ -3532,6 +3572,10 @@ void update_bounds(pt_ctx* c, float aperture) {
                     d.whi[r] = (float)(hi[r] + pad + std::ldexp(std::fabs(hi[r]), -18));
                 }
                 d.back = (float)(1.0002e-4 * stretch * (1.0 + 1e-5));
+                for (int r = 0; r < 3; ++r) {
+                    d.wbox[2 * r] = d.wlo[r];
+                    d.wbox[2 * r + 1] = d.whi[r];
+                }
                 d.bkind = 3;
             }
         }

@@ -86,3 +86,26 @@ def sum_over_ranks(torch, dist, count: int, device) -> int:
     t = torch.tensor([int(count)], dtype=torch.int64, device=_coll_device(torch, dist, device))
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return int(t.item())
+
+
+def per_rank(torch, dist, values, device) -> list:
+    """Every rank's `values` (a short list of numbers), in rank order, on every rank (one
+    all_gather): the bench's per-rank elapsed time and segments, so an imbalanced N-GPU line can be
+    diagnosed from the line itself."""
+    t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=_coll_device(torch, dist, device))
+    out = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [[float(x) for x in o.tolist()] for o in out]
+
+
+def rank_spread(rows) -> dict:
+    """Summary of per_rank((elapsed_s, segments)) rows: per-rank lists, min / max, and the spread of
+    the elapsed time (max / min - 1) and of the segments (max / min - 1)."""
+    el = [r[0] for r in rows]
+    sg = [int(r[1]) for r in rows]
+    return {"elapsed_s": el, "segments": sg,
+            "elapsed_min_s": min(el), "elapsed_max_s": max(el),
+            "elapsed_spread": max(el) / min(el) - 1.0 if min(el) > 0 else None,
+            "segments_min": min(sg), "segments_max": max(sg),
+            "segments_spread": max(sg) / min(sg) - 1.0 if min(sg) > 0 else None,
+            "slowest_rank": int(max(range(len(el)), key=lambda i: el[i]))}

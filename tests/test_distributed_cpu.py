@@ -51,6 +51,12 @@ def _worker(rank, world, port, out_dir):
         img = D.assemble([t.cpu().numpy() for t in tiles], H, world) if tiles is not None else None
         t = D.max_over_ranks(torch, dist, 1.0 + rank, torch.device("cpu"))
         n = D.sum_over_ranks(torch, dist, 10 * (rank + 1), torch.device("cpu"))
+        # bench.py's N > 1 diagnostics: every rank's (elapsed, segments), rank order, on every rank
+        rows = D.per_rank(torch, dist, (1.0 + rank, 10 * (rank + 1)), torch.device("cpu"))
+        assert rows == [[1.0 + r, 10.0 * (r + 1)] for r in range(world)]
+        sp = D.rank_spread(rows)
+        assert sp["elapsed_max_s"] == t and sum(sp["segments"]) == n and sp["slowest_rank"] == world - 1
+        assert abs(sp["elapsed_spread"] - world + 1) < 1e-12 and sp["segments_min"] == 10
         if rank == 0:
             np.save(Path(out_dir) / "gathered.npy", img)
             np.save(Path(out_dir) / "reduce.npy", np.array([t, n], np.float64))
