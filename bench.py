@@ -15,23 +15,23 @@ value = all ranks' traced segments / max-over-ranks wall time / 1e6.
 
 Roofline: the dominant kernel of analytic scenes is the fused bounce kernel k_bounce<false,...>
 (bounces >= 1); of mesh scenes (config 5) the BVH walk k_traverse4<false> (bounces >= 1), with the
-bounce kernel that follows it reported beside it (roofline.bounce_kernel).  Average launch times
-come from HIP events recorded on the launch stream, per kernel kind, over a profiled segment of the
-same workload (rocprofv3 --kernel-trace --stats of the same command agrees: profiles/r0*_*); the
-algorithmic bytes per launch are SURVEY.md §8d's 184 B per traced segment (ray 24 + hit write 28 +
-hit read 28 + path read 48 + write 48 + compaction 8) x the segments that launch traces
-(DESIGN.md §4).  roofline.frac = those bytes / the average launch duration / 8 TB/s, per launch;
-roofline.step_frac = the same bytes of every bounce of a step / ms_per_step / 8 TB/s.  Batched
-passes run two lanes of iterations whose launches overlap; the bytes over the union of the launch
-intervals are reported separately (roofline.aggregate).  The fused kernel itself needs only 40 B in
-+ 40 B per survivor + 24 B per emissive hit (kernel_min_bytes; path planes of 16 + 16 + 8 B).
-Measured in the same run (N = 1): rocprofv3 --pmc passes over the same workload (scripts/pmc.py)
-give the kernel's fabric traffic per launch (roofline.traffic, FETCH_SIZE x 2 + WRITE_SIZE) and its
-VALU wave-instructions (roofline.valu_issue: against the chip's VALU issue rate, 256 CUs x 4 SIMDs x
-2.4 GHz / 2 cycles per wave64 instruction, MI355X_MICROARCH.md) — the kernels are issue/latency-
-bound, not bandwidth-bound (roofline.limiter).  For the BVH walk also its memory instructions, L2
-hit rate and, with the diagnostic counter build present (scripts/trav_build.sh), the walk's lane
-counters (scripts/trav_stats.py).
+bounce kernel that follows it reported beside it (roofline.bounce_kernel).  Launch times come from HIP
+events recorded on the launch stream, per kernel kind, over a profiled segment of the same workload;
+the kernel's time per launch is the union of its launch intervals / launches (effective_launch_ms:
+the two lanes' launches overlap, and launches x it fits the step; rocprofv3 --kernel-trace of the same
+command agrees: profiles/r0*_union_check.txt).  The roofline names the BINDING resource
+(_finalize_roofline): the in-run rocprofv3 --pmc passes (scripts/pmc.py) give the kernel's fabric
+traffic (FETCH_SIZE x 2 + WRITE_SIZE) and its VALU wave-instructions per launch; when the traffic is
+below half the HBM peak the bound is "issue" and achieved / peak / frac are the VALU issue rate's
+(256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles per wave64 instruction, MI355X_MICROARCH.md).  The byte
+figures stay beside it under roofline.hbm: SURVEY.md §8d's 184 B per traced segment (a MODEL — ray 24
++ hit write 28 + hit read 28 + path read 48 + write 48 + compaction 8; the fused kernel keeps the hit
+in registers), the kernel's own minimum bytes (40 B in + 40 B per survivor + 24 B per emissive hit;
+path planes of 16 + 16 + 8 B) and the counters' traffic, each over effective_launch_ms.
+roofline.step_model_ratio = the §8d bytes of every bounce of a step / ms_per_step / 8 TB/s (a model
+ratio: above 1 it is flagged in model_ratios_above_1).  For the BVH walk also its memory
+instructions, L2 hit rate and, with the diagnostic counter build present (scripts/trav_build.sh), the
+walk's lane counters (scripts/trav_stats.py).
 The scan kernel is measured separately at n = 2^28 (8 B/element, 2 GiB, beyond the 256 MiB MALL).
 """
 from __future__ import annotations
@@ -319,6 +319,82 @@ def _pmc_leg(args, scene_path, spp_pass, sorted_, avg_ms, kernel_prefix, seg_per
     return out
 
 
+def _finalize_roofline(r: dict) -> None:
+    """The line's roofline names the kernel's BINDING resource.
+
+    Byte figures, each over the kernel's time per launch (effective_launch_ms, the union of its launch
+    intervals / launches: launches x it fits the step):
+      hbm.model_184B     — SURVEY.md §8d's 184 B per traced segment (ray 24 + hit 28 + 28 + path 48 + 48 +
+                           compaction 8).  A MODEL: the fused kernel keeps the hit record in registers and
+                           never moves most of these bytes;
+      hbm.kernel_min     — the fused kernel's own minimum bytes (path planes in, survivors out, emissive
+                           colour read-modify-write: kernel_min_bytes_per_launch);
+      hbm.counter_traffic— measured fabric traffic (rocprofv3 --pmc FETCH_SIZE x 2 + WRITE_SIZE, in-run).
+    VALU issue (when the --pmc passes ran): SQ_INSTS_VALU per launch / effective_launch_ms / VALU_PEAK.
+    bound = "hbm" when the measured traffic reaches half the HBM peak, else "issue" — then the top-level
+    achieved / peak / unit / frac are the VALU issue rate's, and the byte figures stay under "hbm".
+    Without --pmc: the §8d model's fraction, labelled as such.  Every reported fraction is <= 1 unless
+    listed in fractions_above_1 (with the reason)."""
+    eff = r.get("effective_launch_ms") or r.get("avg_launch_ms") or 0.0
+    secs = eff * 1e-3
+    hbm = {"peak": HBM_PEAK_GBS, "unit": "GB/s"}
+    model = r.get("algorithmic_bytes_per_launch")
+    if model is not None and secs > 0:
+        hbm["model_184B"] = {"bytes_per_launch": model, "achieved": model / secs / 1e9,
+                             "frac": model / secs / 1e9 / HBM_PEAK_GBS,
+                             "definition": "SURVEY.md §8d model: 184 B x segments per launch / effective_launch_ms"}
+    kmin = r.get("kernel_min_bytes_per_launch")
+    if kmin is not None and secs > 0:
+        hbm["kernel_min"] = {"bytes_per_launch": kmin, "achieved": kmin / secs / 1e9,
+                             "frac": kmin / secs / 1e9 / HBM_PEAK_GBS,
+                             "per_segment": kmin / max(r.get("segments_per_launch") or 1.0, 1.0),
+                             "definition": "the fused kernel's own minimum bytes (40 B path in, 40 B per survivor "
+                                           "out, 24 B per emissive hit) / effective_launch_ms"}
+    if r.get("traffic") is not None and secs > 0:
+        hbm["counter_traffic"] = {"bytes_per_launch": r["traffic"], "achieved": r["traffic"] / secs / 1e9,
+                                  "frac": r["traffic"] / secs / 1e9 / HBM_PEAK_GBS,
+                                  "per_segment": r.get("traffic_per_segment"),
+                                  "definition": "rocprofv3 --pmc FETCH_SIZE x 2 + WRITE_SIZE per launch (in-run "
+                                                "passes of the same workload) / effective_launch_ms"}
+    r["hbm"] = hbm
+    v = r.get("valu_issue")
+    counters = hbm.get("counter_traffic")
+    if v and v.get("instructions_per_launch") and secs > 0:
+        v["frac"] = v["instructions_per_launch"] / secs / VALU_PEAK
+        v["achieved"] = v["instructions_per_launch"] / secs
+    if v and counters and counters["frac"] < 0.5:
+        r["bound"] = "issue"
+        r["achieved"], r["peak"], r["unit"], r["frac"] = v["achieved"], VALU_PEAK, "wave64 VALU instr/s", v["frac"]
+        r["definition"] = ("binding resource: VALU issue — SQ_INSTS_VALU per launch (rocprofv3 --pmc, in-run) / "
+                           "effective_launch_ms (union of the kernel's launch intervals / launches) / "
+                           "(256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU instruction); measured fabric "
+                           f"traffic is {counters['frac']:.2f} of the HBM peak (hbm.counter_traffic)")
+    elif counters and counters["frac"] >= 0.5:
+        r["bound"] = "hbm"
+        r["achieved"], r["peak"], r["unit"], r["frac"] = counters["achieved"], HBM_PEAK_GBS, "GB/s", counters["frac"]
+        r["definition"] = "binding resource: HBM — measured fabric traffic per launch / effective_launch_ms / 8 TB/s"
+    elif "model_184B" in hbm:
+        r["bound"] = "hbm"
+        r["achieved"], r["peak"], r["unit"], r["frac"] = (hbm["model_184B"]["achieved"], HBM_PEAK_GBS, "GB/s",
+                                                          hbm["model_184B"]["frac"])
+        r["definition"] = ("no counters in this run (--no-pmc): SURVEY.md §8d MODEL bytes (184 B per segment) / "
+                           "effective_launch_ms / 8 TB/s — a model, not measured traffic")
+    above = []
+    def walk(d, path):
+        for k, x in d.items():
+            if isinstance(x, dict):
+                walk(x, path + [k])
+            elif k in ("frac", "aggregate_frac") and isinstance(x, (int, float)) and x > 1.0:
+                above.append(".".join(path + [k]))
+    walk(r, [])
+    notes = {}
+    if (r.get("step_model_ratio") or 0) > 1.0:
+        notes["step_model_ratio"] = ("> 1: the §8d model counts bytes the fused kernel never moves (hit records "
+                                     "stay in registers), so the model saturates; it is not an HBM fraction")
+    r["fractions_above_1"] = above
+    r["model_ratios_above_1"] = notes
+
+
 def _walk_counters(scene_path, spp_pass, timeout=300) -> dict | None:
     """The BVH walk's lane counters from the diagnostic build (scripts/trav_build.sh ->
     cuda_pathtracer_amd/build/libpt_amd_trav.so; scripts/trav_stats.py), one pass of the same
@@ -580,9 +656,10 @@ def main() -> None:
                                              "other lane's, so launches x this exceeds the step)"},
                 "segments_per_launch": seg_bounce / max(k_n, 1),
                 "algorithmic_bytes_per_launch": per_launch_bytes,
-                "step_frac": SEGMENT_BYTES * step_seg / (elapsed / max(args.steps, 1)) / 1e9 / HBM_PEAK_GBS
+                "step_model_ratio": SEGMENT_BYTES * step_seg / (elapsed / max(args.steps, 1)) / 1e9 / HBM_PEAK_GBS
                 if world == 1 else None,
-                "step_frac_definition": "184 B x traced segments of one step (all bounces) / ms_per_step / 8 TB/s",
+                "step_model_ratio_definition": "§8d model bytes (184 B x traced segments of one step, all bounces) / "
+                                               "ms_per_step / 8 TB/s — a model ratio, not a measured HBM fraction",
                 # two lanes' launches overlap: the same bytes over the union of the launch intervals
                 "aggregate": {"busy_ms": k_busy,
                               "achieved": SEGMENT_BYTES * seg_bounce / (k_busy * 1e-3) / 1e9 if k_busy > 0 else 0.0,
@@ -691,6 +768,8 @@ def main() -> None:
             roofline["isolated"]["ms_per_step_if_serial"] = lps * roofline["isolated"]["avg_launch_ms"]
     if rank == 0 and world == 1 and walk and not args.no_walk_counters:
         roofline["walk_counters"] = _walk_counters(scene_path, spp)
+    if rank == 0:
+        _finalize_roofline(roofline)
     if rank == 0:
         print(json.dumps(result), flush=True)
 

@@ -144,17 +144,10 @@ struct Hit {
     float u, v;
     int32_t frame = -1;   // cube hits: geom * 6 + slab code (the precomputed tangent frame, DGeom::frm)
 };
-#ifndef PT_SKIP_MISS_WAVES
-#define PT_SKIP_MISS_WAVES 1   // (A/B knob: the sorted camera-ray producer's waves whose camera mask is empty skip
-                               // raygen + closest hit: config 3 35.6k -> 36.9k, same box)
-#endif
 // The fused first bounce does the same in its own instantiation (k_bounce<true, .., kAnalyticSkip>: 5
 // more VGPRs), chosen per context when at least kSkipEmptyMin of the camera-mask blocks are empty
 // (build_cmask; config 4's 16:9 view +4.0%, while Cornell at 800x800 lost 1.1% to the registers).
 constexpr double kSkipEmptyMin = 0.2;
-#ifndef PT_SKIP_EMPTY_TILES
-#define PT_SKIP_EMPTY_TILES 1   // (A/B knob: the plain fused first bounce skips tiles whose 4 mask blocks are all empty)
-#endif
 // What the closest hit returns for a ray that meets nothing (intersect_bounded, computeIntersections'
 // t = -1 with materialId 0: pathtrace.cu:466).
 __device__ __forceinline__ Hit miss_hit() {
@@ -576,19 +569,6 @@ __device__ __forceinline__ Hit intersect_scene(const SceneDev& S, const FlagsDev
 // index on ties, pathtrace.cu:284-288) is the reference's bit for bit.  Typically one exact test
 // per ray instead of one per geom.  PT_AMD_VERIFY_BOUNDS=1 re-runs the plain loop and counts any
 // difference (pt_stats_t.bound_mismatch).
-// Diagnostic build only (scripts/stamps.sh: -DPT_STAMPS): per-wave s_memtime phase sums of the
-// non-first bounce kernel, each phase closed by s_waitcnt 0 (so the split perturbs the schedule).
-#ifdef PT_STAMPS
-__device__ unsigned long long g_stamps[16];   // [0..5] phases, [8..] closest-hit counters
-#ifdef PT_STAMPS_FIRST
-constexpr bool kStampFirst = true;    // phase stamps of the first bounce (raygen in "load")
-#else
-constexpr bool kStampFirst = false;   // phase stamps of bounces >= 1
-#endif
-#define STAMP(v) do { __builtin_amdgcn_s_waitcnt(0); v = __builtin_amdgcn_s_memtime(); } while (0)
-#else
-#define STAMP(v) do { } while (0)
-#endif
 
 constexpr int kLdsGeoms = 32;
 // What the exact tests and the hit normal read: 47 words, padded to a 52-word (208-byte) row so
@@ -818,16 +798,13 @@ __device__ __forceinline__ Hit intersect_bounded(const SceneDev& S, const FlagsD
             if (G[i].type == PT_GEOM_MESH && mh->id >= G[i].tri_start && mh->id < G[i].tri_end) { mesh_geom = i; break; }
         if (mesh_geom >= 0 && mh->t > 0.0f) { t_min = mh->t; hit_geom = mesh_geom; }
     }
-#ifndef PT_ONE_GEOM_MASK
-#define PT_ONE_GEOM_MASK 1   // (A/B knob: a wave whose camera-ray mask holds one geom tests it without bounds)
-#endif
     float lo1 = kInf, lo2 = kInf, lo3 = kInf;
     int g1 = -1, g2 = -1;
     uint32_t rest = 0u;   // geoms tested after the candidates regardless of bounds
     // A wave whose rays can hit only one geom (the first bounce's camera-ray mask, wave-uniform): that
     // geom's exact test is the closest hit — the bounds pass would make it the only candidate.
     const uint32_t gone = gmask & ng_all_mask(S.ngeoms);
-    const bool one = PT_ONE_GEOM_MASK && !PRE && !plain && gone != 0u && (gone & (gone - 1u)) == 0u;
+    const bool one = !PRE && !plain && gone != 0u && (gone & (gone - 1u)) == 0u;
     if (one) {
         g1 = __builtin_ctz(gone);
     } else if (!plain) {
@@ -935,22 +912,6 @@ __device__ __forceinline__ Hit intersect_bounded(const SceneDev& S, const FlagsD
             m &= m - 1u;
         }
     }
-#ifdef PT_STAMPS
-        {
-            const uint64_t m2 = __ballot(g2 >= 0 && lo2 <= t_min), m3 = __ballot(lo3 <= t_min);
-            const uint64_t mg = __ballot(g1 >= 0), ms = __ballot(g1 >= 0 && s_geoms[g1].type == PT_GEOM_SPHERE);
-            if ((threadIdx.x & 63) == 0) {
-                atomicAdd(&g_stamps[8], 1ull);
-                atomicAdd(&g_stamps[9], (unsigned long long)__popcll(m2));
-                atomicAdd(&g_stamps[10], m2 ? 1ull : 0ull);
-                atomicAdd(&g_stamps[11], (unsigned long long)__popcll(m3));
-                atomicAdd(&g_stamps[12], m3 ? 1ull : 0ull);
-                atomicAdd(&g_stamps[13], (ms && ms != mg) ? 1ull : 0ull);
-                atomicAdd(&g_stamps[14], (unsigned long long)__popcll(mg));
-                atomicAdd(&g_stamps[15], (unsigned long long)__popc(gmask & ng_all_mask(S.ngeoms)));   // bounded geoms
-            }
-        }
-#endif
 
     Hit h;
     if (hit_geom < 0) {
@@ -1166,14 +1127,9 @@ __device__ __forceinline__ void raygen(const CamDev& cam, const FlagsDev& fl, co
 }
 
 // Path planes stream through HBM once per bounce (GBs per lane, far beyond the Infinity Cache):
-// non-temporal loads and stores (PT_NO_NT_PATHS: plain ones).
-#ifdef PT_NO_NT_PATHS
-#define PT_LD(p) (*(p))
-#define PT_ST(v, p) (*(p) = (v))
-#else
+// non-temporal loads and stores.
 #define PT_LD(p) __builtin_nontemporal_load(p)
 #define PT_ST(v, p) __builtin_nontemporal_store((v), (p))
-#endif
 __device__ __forceinline__ void load_path(const PathSoA& B, int i, int bounce, PathReg& p) {
     const v4f a = PT_LD(B.a + i), b = PT_LD(B.b + i);
     const v2f c = PT_LD(B.c + i);
@@ -1460,26 +1416,9 @@ constexpr int kTravChunk = 256;  // rays per ticket grab
 constexpr int kRefillMin = 16;   // idle lanes that trigger a refill
 constexpr int kTravLdsRows = 32; // LDS stack entries per thread (HybStack; the rest in scratch)
 constexpr int kTrav4LdsRows = 16;   // k_traverse4: LDS stack entries per thread (5 workgroups per CU)
-#ifndef PT_FOLD_BATCH
-#define PT_FOLD_BATCH 4
-#endif
-constexpr int kFoldBatch = PT_FOLD_BATCH;   // k_traverse4: task results read per LDS round trip
-#ifndef PT_T4_LOADS
-#define PT_T4_LOADS 0    // k_traverse4 loads: 0 masked, quad first; 1 every lane; 2 masked, triangle after the box tests
-#endif
-#ifndef PT_T4_OVERLAP
-#define PT_T4_OVERLAP 1  // k_traverse4: a leaf sent out whole and the node after it in one trip
-#endif
-#ifndef PT_T4_PUSH
-#define PT_T4_PUSH 1     // k_traverse4: branch-free pushes in trips whose stack is LDS-only
-#endif
-#ifndef PT_T4_ASSIGN
-#define PT_T4_ASSIGN 0   // k_traverse4 leaf tasks: 0 owner tag + ballot + ds_bpermute; 1 task slots written by owners
-#endif
-#ifndef PT_T4_TASKS
-#define PT_T4_TASKS 2    // k_traverse4 leaf tasks: K consecutive triangles of one leaf per lane per trip
-#endif                   // (a leaf's remaining count rounded up to a multiple of K: 64 K triangle tests per trip),
-                         // for walks without the exact t-cull; with it, K = 1 (pt_ctx::walk_k)
+constexpr int kFoldBatch = 4;      // k_traverse4: task results read per LDS round trip
+// k_traverse4 leaf tasks: K = kT4K consecutive triangles of one leaf per lane per trip for walks
+// without the exact t-cull; with it, K = 1 (pt_ctx::walk_k).
 // Measured (config 5, 64 iterations per pass, same box, two alternations; profiles/r05_walk_ab.txt):
 // K = 1 / 2 / 3 / 4: 822 / 929 / 793 / 723 Mray/s.  K = 2 halves the trips the triangle tasks need
 // (112 per ray at 64 per trip: they, not the 56 interior steps, bounded a ray's trips) at 122 VGPRs,
@@ -1487,20 +1426,7 @@ constexpr int kFoldBatch = PT_FOLD_BATCH;   // k_traverse4: task results read pe
 // (the tessellated workload, room.json) the cull leaves few triangles per reached leaf, the trips are
 // bound by the interior steps, and the second slot only adds divergent work: K = 2 5,542 vs K = 1
 // 5,755 Mray/s on the tessellated workload (same box) — so those walks run K = 1.
-constexpr int kT4K = PT_T4_TASKS;
-#ifndef PT_T4_COOP
-#define PT_T4_COOP 0     // k_traverse4 quad fetch: 0 each interior lane loads its own 112 B (7 loads);
-                         // 1 the wave loads the quads cooperatively, 8 lanes per 128-B row, register-
-                         // staged into LDS; 2 the same by LDS-DMA (global_load_lds_dwordx4).
-                         // Measured on config 5 (round 4, profiles/r04_walk_coop_ab.txt): 0 845.8,
-                         // 2 with 16 / 32 / 64 rows 745.7 / 589.9 / 416.2, 1 (32 rows) 477.3 Mray/s —
-                         // the walk waits on its dependent loads (46% of wave cycles), and the LDS
-                         // hand-over, its waits and the lower occupancy cost more than the address
-                         // cycles saved; 0 ships
-#endif
-#ifndef PT_T4_COOP_ROWS
-#define PT_T4_COOP_ROWS 32   // quads fetched cooperatively per trip (interior lanes of rank >= this load their own)
-#endif
+constexpr int kT4K = 2;
 
 // Exclusive prefix of the previous launch's segment survivor counts into s_pre[0..nseg]; returns
 // the total.  All threads of the block call it (barriers).
@@ -1757,35 +1683,17 @@ __device__ __forceinline__ void wave_sync() {
 // order are BVHIntersectionTest's; only the scheduling across lanes differs.  Rays whose o or 1/d
 // is not finite (axis-parallel or NaN directions) get the record kRecWalkHere: the bounce kernel
 // walks them itself with the node-at-a-time walk (glm's ternary slab test, the reference's stack).
-#ifndef PT_T4_WAVES
-#define PT_T4_WAVES 1   // (A/B knob: minimum waves per SIMD of k_traverse4)
-#endif
-#ifndef PT_T4_WAVES_FIRST
-#define PT_T4_WAVES_FIRST 4   // (A/B knob: minimum waves per SIMD of the camera-ray walk: 138 -> 128 VGPRs, +1%)
-#endif
+constexpr int kT4Waves = 1; // (minimum waves per SIMD of k_traverse4)
+constexpr int kT4WavesFirst = 4; // (minimum waves per SIMD of the camera-ray walk: 138 -> 128 VGPRs, +1%)
 template <bool FIRST, int K>
-__global__ __launch_bounds__(kBlock, FIRST ? PT_T4_WAVES_FIRST : PT_T4_WAVES) void k_traverse4(const KArgs A) {
+__global__ __launch_bounds__(kBlock, FIRST ? kT4WavesFirst : kT4Waves) void k_traverse4(const KArgs A) {
     extern __shared__ int s_tstack[];   // stack_rows entries per thread, column layout
     __shared__ int32_t s_pre[FIRST ? 1 : kMaxSeg + 1];
     __shared__ uint32_t s_wsum[4];
     // leaf tasks, per task lane j: [2j] = (owner's o, triangle index), [2j + 1] = (owner's d, -),
     // then overwritten by the task's result (t or NaN = no hit, bx, by, -)
-#if PT_T4_ASSIGN == 1
-    __shared__ v4f s_task[2 * kBlock];
-#else
     __shared__ v4f s_task[K * kBlock];  // task results only (K per lane)
-#endif
-#if PT_T4_ASSIGN == 0
     __shared__ int32_t s_own[kBlock];   // leaf tasks: tag << 6 | owner lane, at the owner's first task
-#endif
-#if PT_T4_COOP
-    // cooperative quad fetch: per wave, the quad indices of the trip's interior lanes by rank, and
-    // PT_T4_COOP_ROWS staged 128-B rows (row r = the quad of the rank-r interior lane; its 16-B
-    // column k holds chunk (k - (r >> 1)) & 7, so the owners' ds_read_b128 of one chunk hit 16
-    // distinct 16-B bank slots per lane group)
-    __shared__ int32_t s_qlist[kBlock];
-    __shared__ v4f s_stage[(kBlock / 64) * PT_T4_COOP_ROWS * 8];
-#endif
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const SceneDev& S = A.S;
     int N, nseg = 0, chunk = 0;
@@ -1797,13 +1705,6 @@ __global__ __launch_bounds__(kBlock, FIRST ? PT_T4_WAVES_FIRST : PT_T4_WAVES) vo
         chunk = (int)A.ctl[par].chunk;
         N = seg_prefix(reinterpret_cast<const uint32_t*>(A.seg) + (size_t)par * kMaxSeg, nseg, s_pre, s_wsum);
     }
-#if PT_T4_COOP
-    int32_t* const qlist = s_qlist + wave * 64;
-    v4f* const stage = s_stage + wave * (PT_T4_COOP_ROWS * 8);
-#endif
-#ifndef PT_T4_SEGCUR
-#define PT_T4_SEGCUR 1   // (A/B knob: refills find their segment from the chunk's, not by a binary search each)
-#endif
     auto seg_of = [&](int k) -> int {   // the last segment starting at or before k (binary search)
         int lo = 0, hi = nseg - 1;
         while (lo < hi) {
@@ -1812,7 +1713,7 @@ __global__ __launch_bounds__(kBlock, FIRST ? PT_T4_WAVES_FIRST : PT_T4_WAVES) vo
         }
         return lo;
     };
-    int wseg = 0;   // (!FIRST, PT_T4_SEGCUR) the segment of the wave's current chunk start
+    int wseg = 0;   // (!FIRST) the segment of the wave's current chunk start
     auto ray = [&](int k, f3& o, f3& d) -> int {   // as k_traverse
         if (FIRST) {
             PathReg p;
@@ -1821,32 +1722,21 @@ __global__ __launch_bounds__(kBlock, FIRST ? PT_T4_WAVES_FIRST : PT_T4_WAVES) vo
             d = p.d;
             return k;
         }
-#if PT_T4_SEGCUR
         // a chunk spans a few hundred rays and a segment is a bounce workgroup's survivors: a step
         // or two from the chunk start's segment instead of ~11 dependent LDS reads per refill
         int lo = wseg;
         while (lo + 1 < nseg && s_pre[lo + 1] <= k) ++lo;
-#else
-        const int lo = seg_of(k);
-#endif
         const int q = lo * chunk + (k - s_pre[lo]);
         const v4f a = PT_LD(A.in.a + q), b = PT_LD(A.in.b + q);
         o = F3(a[0], a[1], a[2]);
         d = F3(a[3], b[0], b[1]);
         return q;
     };
-#if PT_T4_ASSIGN == 1
-    v4f* task = s_task + wave * 128;
-#define PT_RES(j) task[2 * (j) + 1]
-#else
     v4f* task = s_task + wave * (64 * K);
 #define PT_RES(j) task[(j)]
-#endif
-#if PT_T4_ASSIGN == 0
     int32_t* own = s_own + wave * 64;
     own[lane] = 0;   // tags start at 1
     uint32_t tag = 0;
-#endif
     int* const col = s_tstack + tid;
     const int rows = A.stack_rows;
     int spill[64];
@@ -1893,9 +1783,7 @@ __global__ __launch_bounds__(kBlock, FIRST ? PT_T4_WAVES_FIRST : PT_T4_WAVES) vo
                 else {
                     cnext = base;
                     cend = min(base + csz, N);
-#if PT_T4_SEGCUR
                     if (!FIRST) wseg = __builtin_amdgcn_readfirstlane(seg_of(base));
-#endif
                 }
             }
             if (!exhausted) {
@@ -1962,7 +1850,6 @@ __global__ __launch_bounds__(kBlock, FIRST ? PT_T4_WAVES_FIRST : PT_T4_WAVES) vo
         const int cov = (pcnt > 0 && pre < 64) ? min(cnt, K * (64 - pre)) : 0;   // triangles covered this trip
         const bool is_task = lane < T;
         bool inner = have && !leaf;
-#if PT_T4_OVERLAP
         // A leaf lane whose remaining triangles all go out this trip already takes its next node
         // (everything after the leaf in the walk's order): an interior node is tested in this same
         // trip, beside its leaf's triangle tests, whose results are folded first (the order of the
@@ -1975,54 +1862,13 @@ __global__ __launch_bounds__(kBlock, FIRST ? PT_T4_WAVES_FIRST : PT_T4_WAVES) vo
                 inner = true;
             }
         }
-#endif
         // ---- the quad of every interior lane ----
         v4f x0, x1, x2, x3, x4, x5, x6;
         uint32_t meta;
-#if PT_T4_COOP
-        // The address path costs about one cycle per cache line per load instruction, so a lane
-        // fetching its own 112 B costs 7 line-accesses; eight lanes fetching one 128-B row together
-        // cost one (scripts/probes/gather_lds.hip: 11.7 -> 5.2-5.4 ps per row from L2).  The rows
-        // go through LDS to their owners; interior lanes of rank >= PT_T4_COOP_ROWS load their own.
-        const uint64_t imask = __ballot(inner);
-        const int n_in = __popcll(imask);
-        const int irank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(imask >> 32),
-                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)imask, 0u));
-        const int nst = min(n_in, PT_T4_COOP_ROWS);   // (wave-uniform)
-        const bool staged = inner && irank < PT_T4_COOP_ROWS;
-        if (nst > 0) {
-            if (staged) qlist[irank] = cur & kQuadIdxMask;
-            wave_sync();
-            for (int j = 0; j * 8 < nst; ++j) {   // (wave-uniform) 8 rows per instruction
-                const int srow = j * 8 + (lane >> 3);
-                const int qi = qlist[min(srow, nst - 1)];
-                const int ck = ((lane & 7) - (srow >> 1)) & 7;   // the chunk whose column is lane & 7
-                const v4f* src = reinterpret_cast<const v4f*>(S.quads + qi) + ck;
-#if PT_T4_COOP == 2
-                if (srow < nst)
-                    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src),
-                                                     reinterpret_cast<__attribute__((address_space(3))) void*>(
-                                                         reinterpret_cast<uintptr_t>(stage + j * 64)),
-                                                     16, 0, 0);
-#else
-                if (srow < nst) stage[j * 64 + lane] = *src;
-#endif
-            }
-        }
-        if (inner && !staged) {
-            const v4f* qsrc = reinterpret_cast<const v4f*>(S.quads + (cur & kQuadIdxMask));
-            x0 = qsrc[0]; x1 = qsrc[1]; x2 = qsrc[2]; x3 = qsrc[3]; x4 = qsrc[4]; x5 = qsrc[5]; x6 = qsrc[6];
-        }
-#else
-#if PT_T4_LOADS == 1   // every lane loads (idle and leaf lanes: their last quad, cached): static wait counts
-        {
-#else
         if (inner) {
-#endif
             const v4f* qsrc = reinterpret_cast<const v4f*>(S.quads + (cur & kQuadIdxMask));
             x0 = qsrc[0]; x1 = qsrc[1]; x2 = qsrc[2]; x3 = qsrc[3]; x4 = qsrc[4]; x5 = qsrc[5]; x6 = qsrc[6];
         }
-#endif
         meta = (uint32_t)cur >> kQuadMetaShift;   // (the code that led here carries the quad's meta)
         typedef uint32_t v4u __attribute__((ext_vector_type(4)));
         v4u cw = {0u, 0u, 0u, 0u};   // the quad's exact t-cull words (one per slot)
@@ -2031,19 +1877,6 @@ __global__ __launch_bounds__(kBlock, FIRST ? PT_T4_WAVES_FIRST : PT_T4_WAVES) vo
         int tidx = 0;
         int ntask = 1;   // (K > 1) triangles tidx .. tidx + ntask - 1 of this task lane
         if (T > 0) {   // (wave-uniform)
-#if PT_T4_ASSIGN == 1   // owners write (ray, triangle index) into each of their task slots
-            for (int k = 0; k < cov; ++k) {
-                task[2 * (pre + k)] = v4f{o.x, o.y, o.z, __int_as_float(ti + k)};
-                task[2 * (pre + k) + 1] = v4f{d.x, d.y, d.z, 0.f};
-            }
-            wave_sync();
-            if (is_task) {
-                const v4f a = task[2 * lane], b = task[2 * lane + 1];
-                to = F3(a[0], a[1], a[2]);
-                tidx = __float_as_int(a[3]);
-                td = F3(b[0], b[1], b[2]);
-            }
-#else   // owners mark their first task slot (tag | lane); task lanes find it by ballot, fetch by ds_bpermute
             if (tag == (1u << 25)) {   // (never in practice: ~10^5 trips per launch) restart the tags
                 own[lane] = 0;
                 tag = 0;
@@ -2061,7 +1894,6 @@ __global__ __launch_bounds__(kBlock, FIRST ? PT_T4_WAVES_FIRST : PT_T4_WAVES) vo
             if (K > 1) ntask = min(K, __shfl(te, ow) - tidx);   // (the leaf's triangles left in this group)
             to = F3(__shfl(o.x, ow), __shfl(o.y, ow), __shfl(o.z, ow));
             td = F3(__shfl(d.x, ow), __shfl(d.y, ow), __shfl(d.z, ow));
-#endif
 #ifdef PT_TRAV_STATS
             {   // triangles dealt this trip (K per task lane at most)
                 const uint32_t tt = __builtin_amdgcn_readlane(lb::wave_inclusive_scan((uint32_t)cov), 63);
@@ -2071,18 +1903,10 @@ __global__ __launch_bounds__(kBlock, FIRST ? PT_T4_WAVES_FIRST : PT_T4_WAVES) vo
         }
         v4f t0, t1, t2;
         v4f u[K > 1 ? K - 1 : 1][3];   // the group's further triangles
-#ifndef PT_T4_TRI_PACK
-#define PT_T4_TRI_PACK 1
-#endif
-#ifndef PT_T4_TRI_X4
-#define PT_T4_TRI_X4 1   // (A/B knob: K = 2 groups loaded as 4 x 16 B + 8 B)
-#endif
         auto load_tri = [&]() {
-#if PT_T4_TRI_PACK
             // 36 bytes per triangle: a leaf's consecutive triangles cover fewer cache lines
             typedef float v3f __attribute__((ext_vector_type(3)));
             const float* p = S.tpack + 9 * (size_t)tidx;
-#if PT_T4_TRI_X4
             if (K == 2) {
                 // the group's 72 contiguous bytes in five loads (4 x 16 B + 8 B, dword-aligned) instead
                 // of six 12-byte ones: 5.4 instead of 6.4 cache-line accesses per lane on average (the
@@ -2098,7 +1922,6 @@ __global__ __launch_bounds__(kBlock, FIRST ? PT_T4_WAVES_FIRST : PT_T4_WAVES) vo
                 u[0][2] = v4f{q3[3], q4[0], q4[1], 0.f};
                 return;
             }
-#endif
             const v3f a = *reinterpret_cast<const v3f*>(p), b = *reinterpret_cast<const v3f*>(p + 3),
                       c = *reinterpret_cast<const v3f*>(p + 6);
             t0 = v4f{a[0], a[1], a[2], 0.f}; t1 = v4f{b[0], b[1], b[2], 0.f}; t2 = v4f{c[0], c[1], c[2], 0.f};
@@ -2112,16 +1935,8 @@ __global__ __launch_bounds__(kBlock, FIRST ? PT_T4_WAVES_FIRST : PT_T4_WAVES) vo
                     u[j - 1][1] = v4f{b2[0], b2[1], b2[2], 0.f};
                     u[j - 1][2] = v4f{c2[0], c2[1], c2[2], 0.f};
                 }
-#else
-            const v4f* tsrc = reinterpret_cast<const v4f*>(S.tris + tidx);   // (non-task lanes: triangle 0)
-            t0 = tsrc[0]; t1 = tsrc[1]; t2 = tsrc[2];
-#endif
         };
-#if PT_T4_LOADS == 1
-        load_tri();
-#elif PT_T4_LOADS == 0
         if (is_task) load_tri();
-#endif
 #ifdef PT_TRAV_STATS
         {
             const uint64_t ib = __ballot(inner);
@@ -2129,21 +1944,6 @@ __global__ __launch_bounds__(kBlock, FIRST ? PT_T4_WAVES_FIRST : PT_T4_WAVES) vo
         }
 #endif
         // ---- interior step ----
-#if PT_T4_COOP
-        if (nst > 0) {   // (wave-uniform) the staged rows have landed: each owner reads its row
-#if PT_T4_COOP == 2
-            __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0): the LDS-DMA writes
-#endif
-            wave_sync();
-            if (staged) {
-                const v4f* row = stage + irank * 8;
-                const int rot = irank >> 1;
-                x0 = row[(0 + rot) & 7]; x1 = row[(1 + rot) & 7]; x2 = row[(2 + rot) & 7];
-                x3 = row[(3 + rot) & 7]; x4 = row[(4 + rot) & 7]; x5 = row[(5 + rot) & 7];
-                x6 = row[(6 + rot) & 7];
-            }
-        }
-#endif
         int next = kWalkNone;
         if (inner) {
             uint32_t hm = quad_hits(x0, x1, x2, x3, x4, x5, o, inv) & meta & 15u;
@@ -2182,7 +1982,6 @@ __global__ __launch_bounds__(kBlock, FIRST ? PT_T4_WAVES_FIRST : PT_T4_WAVES) vo
                 hm = ((hm & 3u) << 2) | (hm >> 2);
             }
             // push the later hits (farthest first), continue with the first
-#if PT_T4_PUSH
             if (fast) {   // (wave-uniform) LDS rows only: the pushes without branches
                 // hit slot k after the first hit goes to top + (hit slots above k): the farthest
                 // deepest, as the sequential pushes below place them
@@ -2195,7 +1994,6 @@ __global__ __launch_bounds__(kBlock, FIRST ? PT_T4_WAVES_FIRST : PT_T4_WAVES) vo
                 next = m == 0 ? pn : (f == 0 ? c0 : (f == 1 ? c1 : (f == 2 ? c2 : c3)));
                 top += m > 0 ? (int)m - 1 : (top > 0 ? -1 : 0);
             } else
-#endif
             {
                 int nx = 0;
                 bool got = false;
@@ -2208,9 +2006,6 @@ __global__ __launch_bounds__(kBlock, FIRST ? PT_T4_WAVES_FIRST : PT_T4_WAVES) vo
         }
         // ---- triangle tests ----
         if (is_task) {
-#if PT_T4_LOADS == 2   // (the triangle's loads after the box tests)
-            load_tri();
-#endif
             float bx = 0.f, by = 0.f, bz = 0.f;
             const bool h = ray_tri(DTri{t0, t1, t2}, to, td, bx, by, bz);
             PT_RES(K * lane) = v4f{h ? bz : __builtin_nanf(""), bx, by, 0.f};
@@ -2235,11 +2030,7 @@ __global__ __launch_bounds__(kBlock, FIRST ? PT_T4_WAVES_FIRST : PT_T4_WAVES) vo
                         if (k0 + k < cov) fold(x[k], ti + k0 + k);
                 }
                 ti += cov;
-#if PT_T4_OVERLAP
                 if (ti == te && !inner) next = after_leaf;   // (inner: the quad step above set `next`)
-#else
-                if (ti == te) next = pop();
-#endif
             }
         }
         if (next == kWalkDone) {
@@ -2263,18 +2054,14 @@ __global__ __launch_bounds__(kBlock, FIRST ? PT_T4_WAVES_FIRST : PT_T4_WAVES) vo
 }
 
 // [raygen] -> intersect -> shade -> segmented compaction (above).
-#ifndef PT_LATER_WAVES
-#define PT_LATER_WAVES 8   // (A/B knob: minimum waves per SIMD of the later-bounce kernels)
-#endif
+constexpr int kLaterWaves = 8; // (minimum waves per SIMD of the later-bounce kernels)
 // At ~60 VGPRs the later bounces' occupancy is set by their SGPRs: 106 give 7 waves per SIMD (of 800).
 // 8 waves (SGPRs capped) lost 0.3% in round 4; after round 5's code-size cuts (LDS-only tables, one
 // inlined exact test: 9,473 -> 5,408 ISA lines) they gain: Cornell +0.5%, config 4 +1.5%
 // (profiles/r05_later_waves8_ab.txt).
-#ifndef PT_FIRST_WAVES
-#define PT_FIRST_WAVES 1   // (A/B knob: minimum waves per SIMD of the analytic first-bounce kernels)
-#endif
+constexpr int kFirstWaves = 1; // (minimum waves per SIMD of the analytic first-bounce kernels)
 template <bool FIRST, bool SPP1, int MESH>
-__global__ __launch_bounds__(kBlock, (MESH != 0 && MESH != kAnalyticSkip) ? 1 : (FIRST ? PT_FIRST_WAVES : PT_LATER_WAVES))
+__global__ __launch_bounds__(kBlock, (MESH != 0 && MESH != kAnalyticSkip) ? 1 : (FIRST ? kFirstWaves : kLaterWaves))
 void k_bounce(const KArgs A) {
     // scene tables sized to the scene (dynamic LDS, bounce_lds_bytes): geom rows, then materials
     extern __shared__ __align__(16) uint8_t s_dyn[];
@@ -2344,12 +2131,9 @@ void k_bounce(const KArgs A) {
     }
     uint32_t kept = 0, emit_cnt = 0;
     int k = 0;
-#ifdef PT_STAMPS
-    unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0}, t0, t1, t2, t3, t4, t5;
-#endif
     for (int base = first; base < last; base += kBlock, ++k) {
         const int i = base + tid;
-        if (FIRST && (MESH == 0 || MESH == kAnalyticGM) && PT_SKIP_EMPTY_TILES && A.cmask) {
+        if (FIRST && (MESH == 0 || MESH == kAnalyticGM) && A.cmask) {
             // a tile whose four camera-mask blocks are all empty: every ray misses — shade's miss exit
             // (colour 0, no random number) without raygen, closest hit or the tile's ballots and
             // barrier (workgroup-uniform; k stays, so the count buffers keep alternating per barrier)
@@ -2373,10 +2157,6 @@ void k_bounce(const KArgs A) {
         }
         bool alive = false, emitted = false;
         PathReg p;
-        STAMP(t0);
-#ifdef PT_STAMPS
-        t1 = t2 = t0;   // lanes past the end of a partial tile skip the inner stamps
-#endif
         // a wave whose camera rays can hit no geom (camera mask 0): no raygen, no closest hit
         // (misses draw no random number)
         bool skip = false;
@@ -2408,7 +2188,6 @@ void k_bounce(const KArgs A) {
                 q = s * chunk_in + (i - s_pre[s]);
                 load_path(A.in, q, A.bounce, p);
             }
-            STAMP(t1);
             Hit h;
             if constexpr (MESH == kMeshPre) {
                 const v4f m = PT_LD(A.mhit + q);
@@ -2452,7 +2231,6 @@ void k_bounce(const KArgs A) {
                 }
 #endif
             }
-            STAMP(t2);
             const int key = A.fl.rng_pixel ? slot_pixel(A.cam, A.tile, p.slot) : i - it_base;
             // every path entering bounce b has b bounces behind it: a wave-uniform value, so the
             // shading RNG's (iteration, remaining depth) hash is computed once per wave on the SALU
@@ -2491,7 +2269,6 @@ void k_bounce(const KArgs A) {
                 retire<SPP1>(A, p);
             }
         }
-        STAMP(t3);
         emit_cnt += (uint32_t)__popcll(__ballot(emitted));
         // in-tile ranks: wave ballot + mbcnt, 4 wave counts through LDS (double-buffered, so
         // one barrier per tile: buffer k&1 was last read two tiles ago, before the last barrier)
@@ -2501,20 +2278,10 @@ void k_bounce(const KArgs A) {
         __syncthreads();
         const uint32_t w0 = s_wc[k & 1][0], w1 = s_wc[k & 1][1], w2 = s_wc[k & 1][2], w3 = s_wc[k & 1][3];
         const uint32_t before = (wave > 0 ? w0 : 0u) + (wave > 1 ? w1 : 0u) + (wave > 2 ? w2 : 0u);
-        STAMP(t4);
         if (alive) store_path(A.out, (int)blockIdx.x * chunk + (int)(kept + before + rank), p);
         kept += (w0 + w1) + (w2 + w3);
         if (!FIRST) seg = seg_walk(s_pre, nseg_in, seg, min(base + kBlock, last - 1));
-        STAMP(t5);
-#ifdef PT_STAMPS
-        st_acc[0] += t1 - t0; st_acc[1] += t2 - t1; st_acc[2] += t3 - t2; st_acc[3] += t4 - t3; st_acc[4] += t5 - t4;
-        st_acc[5] += 1;
-#endif
     }
-#ifdef PT_STAMPS
-    if (FIRST == kStampFirst && lane == 0)
-        for (int q = 0; q < 6; ++q) atomicAdd(&g_stamps[q], st_acc[q]);
-#endif
     if (tid == 0) A.seg[(size_t)(par ^ 1) * kMaxSeg + blockIdx.x] = (int32_t)(kept | ((uint32_t)my_it << kSegItShift));
     flush_emissive(A, emit_cnt, &s_cnt);
 }
@@ -2673,20 +2440,12 @@ struct SortArgs {
 };
 // The next producer's work list: per work position, the record it gathers and the sorted position
 // of the record's run (+ the record's rank = its sorted position).
-// PT_PF_PACKED (default): one (slot, position) pair per work position in `perm` (8 bytes: one store
+// One (slot, position) pair per work position in `perm` (8 bytes: one store
 // and one load per path instead of two each); 0: the separate arrays perm / fpos.
-#ifndef PT_PF_PACKED
-#define PT_PF_PACKED 1
-#endif
 typedef int v2i_pf __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void pf_store(int32_t* perm, int32_t* fpos, uint32_t w, int32_t slot, int32_t pos) {
-#if PT_PF_PACKED
     (void)fpos;
     reinterpret_cast<v2i_pf*>(perm)[w] = v2i_pf{slot, pos};
-#else
-    perm[w] = slot;
-    fpos[w] = pos;
-#endif
 }
 
 constexpr int kSortMaxMats = 256;  // per-tile material counts in LDS (one thread per material)
@@ -2730,13 +2489,9 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_w, u
     return before + incl - v;
 }
 
-#ifndef PT_PRODUCE_WAVES
-#define PT_PRODUCE_WAVES 7   // (A/B knob: minimum waves per SIMD of the analytic producer; 7 caps the
+constexpr int kProduceWaves = 7; // (minimum waves per SIMD of the analytic producer; 7 caps the
                              // first bounce's producer at 72 VGPRs: config 3 +0.8% on the same box)
-#endif
-#ifndef PT_PRODUCE_WAVES_FIRST
-#define PT_PRODUCE_WAVES_FIRST PT_PRODUCE_WAVES
-#endif
+constexpr int kProduceWavesFirst = kProduceWaves;
 // VERIFY: the PT_AMD_VERIFY_BOUNDS=1 build of the producer (the plain-loop re-run of every closest
 // hit compiled in); the default one carries no diagnostic code (round 4: the later producer's 8-byte
 // register spill went away with it).
@@ -2744,7 +2499,7 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_w, u
 // shading reads materials only there (one inlined shade instead of a uniform branch between an LDS and a
 // global-memory copy) and the closest hit has no plain loop over a larger geom table.
 template <bool FIRST, bool SPP1, bool MESH, bool VERIFY, bool LDSM = false>
-__global__ __launch_bounds__(kBlock, MESH ? 1 : (FIRST ? PT_PRODUCE_WAVES_FIRST : PT_PRODUCE_WAVES))
+__global__ __launch_bounds__(kBlock, MESH ? 1 : (FIRST ? kProduceWavesFirst : kProduceWaves))
 void k_sort_produce(const KArgs A, const SortArgs SA) {
     __shared__ DMaterial s_mats[kLdsMats];
     __shared__ LGeom s_geoms[MESH ? 1 : kLdsGeoms];
@@ -2816,7 +2571,7 @@ void k_sort_produce(const KArgs A, const SortArgs SA) {
         PathReg p;
         Hit h;
         bool ends = false;
-        if (FIRST && PT_SKIP_EMPTY_TILES && !VERIFY && A.cmask) {
+        if (FIRST && !VERIFY && A.cmask) {
             // the whole tile's camera-mask blocks empty (workgroup-uniform): every ray misses — colour
             // 0 retired, one run of material 0 holding the tile's paths and no record; the tile's
             // ballots and barriers are skipped (k stays: the count buffers alternate per barrier)
@@ -2845,7 +2600,7 @@ void k_sort_produce(const KArgs A, const SortArgs SA) {
             }
         }
         bool skip = false;
-        if (FIRST && PT_SKIP_MISS_WAVES && !VERIFY && A.cmask) {
+        if (FIRST && !VERIFY && A.cmask) {
             const int lp0 = __builtin_amdgcn_readfirstlane(idx - it_base);
             skip = lp0 < it_end - it_base && A.cmask[lp0 >> 6] == 0u;
         }
@@ -2863,12 +2618,8 @@ void k_sort_produce(const KArgs A, const SortArgs SA) {
                 raygen_at(A.cam, A.fl, A.tile, idx, it, idx - it_base, p);
                 alive = true;
             } else {
-#if PT_PF_PACKED
                 const v2i_pf pf = reinterpret_cast<const v2i_pf*>(SA.perm)[idx];
                 const int j = pf[0], fp = pf[1];
-#else
-                const int j = SA.perm[idx], fp = 0;
-#endif
                 const v4f* r = srec(A.in, j);
                 // (plain loads: a gather of 32-byte records)
                 const v4f r0 = r[0], r1 = r[1];
@@ -2908,7 +2659,7 @@ void k_sort_produce(const KArgs A, const SortArgs SA) {
                 }
                 // key: sorted index within the path's own iteration (paths that ended in the
                 // previous launch hold positions too: fpos)
-                const int key = A.fl.rng_pixel ? slot_pixel(A.cam, A.tile, p.slot) : ((PT_PF_PACKED ? fp : SA.fpos[idx]) + (int)rank) - __builtin_amdgcn_readfirstlane(s_fb[it]);
+                const int key = A.fl.rng_pixel ? slot_pixel(A.cam, A.tile, p.slot) : (fp + (int)rank) - __builtin_amdgcn_readfirstlane(s_fb[it]);
                 const float* frames = lds_geoms ? s_frm : nullptr;
                 alive = lds_mats ? shade_from(A.S, A.fl, A.tile.depth, iter, key, p, h, hitp, s_mats, frames)
                                  : shade_from(A.S, A.fl, A.tile.depth, iter, key, p, h, hitp, A.S.mats, frames);
@@ -3150,20 +2901,18 @@ __global__ __launch_bounds__(kBlock) void k_hist_apply(const int32_t* __restrict
 }
 
 // spp > 1: add the per-slot colours in sample order (finalGather as `spp` sequential iterations).
-#ifndef PT_FIN_BATCH
-#define PT_FIN_BATCH 16
-#endif
+constexpr int kFinBatch = 16;
 __global__ void k_finalize_spp(float* __restrict__ image, const v4f* __restrict__ col, int npix, int spp) {
     for (int lp = blockIdx.x * blockDim.x + threadIdx.x; lp < npix; lp += gridDim.x * blockDim.x) {
         float r = image[3 * (size_t)lp], g = image[3 * (size_t)lp + 1], b = image[3 * (size_t)lp + 2];
         int s = 0;
         // the loads of a batch of samples issued together (independent), the adds in sample order
-        for (; s + PT_FIN_BATCH <= spp; s += PT_FIN_BATCH) {
-            v4f c[PT_FIN_BATCH];
+        for (; s + kFinBatch <= spp; s += kFinBatch) {
+            v4f c[kFinBatch];
 #pragma unroll
-            for (int k = 0; k < PT_FIN_BATCH; ++k) c[k] = PT_LD(col + (size_t)(s + k) * npix + lp);
+            for (int k = 0; k < kFinBatch; ++k) c[k] = PT_LD(col + (size_t)(s + k) * npix + lp);
 #pragma unroll
-            for (int k = 0; k < PT_FIN_BATCH; ++k) { r += c[k][0]; g += c[k][1]; b += c[k][2]; }
+            for (int k = 0; k < kFinBatch; ++k) { r += c[k][0]; g += c[k][1]; b += c[k][2]; }
         }
         for (; s < spp; ++s) {
             const v4f c = PT_LD(col + (size_t)s * npix + lp);
@@ -4581,8 +4330,8 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
         ss.hist_cap = (int64_t)((size_t)c->nmats * (cap / kBlock + 1) + 2);
         const size_t tiles = ((size_t)ss.hist_cap + kHistTile - 1) / kHistTile;
         if (int rc = c->alloc(&ss.hslot, (size_t)ss.hist_cap)) return bail(rc);
-        if (int rc = c->alloc(&ss.perm, PT_PF_PACKED ? 2 * paths : paths)) return bail(rc);   // (pf_store)
-        if (int rc = c->alloc(&ss.fpos, PT_PF_PACKED ? 1 : paths)) return bail(rc);
+        if (int rc = c->alloc(&ss.perm, 2 * paths)) return bail(rc);   // (pf_store)
+        if (int rc = c->alloc(&ss.fpos, 1)) return bail(rc);
         if (int rc = c->alloc(&ss.hist2, (size_t)ss.hist_cap)) return bail(rc);
         if (int rc = c->alloc(&ss.offs2, (size_t)ss.hist_cap)) return bail(rc);
         if (int rc = c->alloc(&ss.hist, (size_t)ss.hist_cap)) return bail(rc);
@@ -4706,10 +4455,7 @@ static int render_pass(pt_ctx* c, int32_t iter_first, hipStream_t st, bool ahead
             a.out = bufs[lcur ^ 1];
             a.hit.uv = ss.uv[lcur];
             const SortArgs sa{ss.hslot, ss.hist, ss.offs, ss.hist2, ss.offs2, ss.perm, ss.fpos, ss.itb, ss.uv[lcur ^ 1]};
-#ifndef PT_PRODUCER_ALWAYS_VERIFY
-#define PT_PRODUCER_ALWAYS_VERIFY 0   // (A/B knob: the diagnostic producer build for every run, round 3's form)
-#endif
-            hipLaunchKernelGGL(produce_kernel(first, spp1, mesh, a.fl.verify != 0 || PT_PRODUCER_ALWAYS_VERIFY,
+            hipLaunchKernelGGL(produce_kernel(first, spp1, mesh, a.fl.verify != 0,
                                               c->nmats <= kLdsMats && a.S.ngeoms <= kLdsGeoms),
                                dim3(c->grid_bounce[0]), dim3(kBlock),
                                (size_t)16 * c->nmats * sizeof(uint32_t), s, a, sa);
@@ -4727,10 +4473,8 @@ static int render_pass(pt_ctx* c, int32_t iter_first, hipStream_t st, bool ahead
         a.parity = (int)(lc & 1);
         const uint32_t* nlive = &a.ctl[a.parity].hist_live;
         const int tiles = (int)((ss.hist_cap + kHistTile - 1) / kHistTile);
-#ifndef PT_HIST_GRID
-#define PT_HIST_GRID 4   // (A/B knob: histogram-scan workgroups per CU)
-#endif
-        const int hgrid = std::min(tiles, PT_HIST_GRID * c->cus);   // (grid-stride over the live blocks)
+        constexpr int kHistGrid = 4; // (histogram-scan workgroups per CU)
+        const int hgrid = std::min(tiles, kHistGrid * c->cus);   // (grid-stride over the live blocks)
         hipLaunchKernelGGL(k_hist_sums, dim3(hgrid), dim3(kBlock), 0, s, (const int32_t*)ss.hist, (const int32_t*)ss.hist2,
                            ss.hist_cap, nlive, ss.sums);
         hipLaunchKernelGGL(k_hist_scan_sums, dim3(1), dim3(kBlock), 0, s, ss.sums, ss.hist_cap, nlive);
@@ -5070,17 +4814,6 @@ int pt_stats(pt_ctx* c, pt_stats_t* out) {
                  : PT_OK;
 }
 
-#ifdef PT_STAMPS
-int pt_debug_stamps(unsigned long long* out8, int32_t reset) {
-    HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 16));
-    if (reset) {
-        unsigned long long z[16] = {};
-        HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof z));
-    }
-    return PT_OK;
-}
-#endif
 
 #ifdef PT_TRAV_STATS
 // Diagnostic build only (scripts/trav_stats.py): k_traverse[4]'s counters summed over their slots:
