@@ -267,6 +267,15 @@ def _pmc_leg(args, scene_path, spp_pass, sorted_, avg_ms, kernel_prefix, seg_per
             out["traffic_frac"] = out["traffic"] / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
             if out["traffic_frac"] < 0.5:   # measured traffic far below the HBM peak (as for k_bounce)
                 out["bound"] = "issue"
+            if all("SQ_INSTS_VALU" in m for m in ks.values()):
+                valu = sum(m["SQ_INSTS_VALU"] * m["launches"] for m in ks.values()) / segs * seg_per_launch
+                out["valu_issue"] = {
+                    "unit": "wave64 VALU instr/s", "peak": VALU_PEAK, "instructions_per_launch": valu,
+                    "instructions_per_segment": valu / max(seg_per_launch, 1.0),
+                    "achieved": valu / (avg_ms * 1e-3), "frac": valu / (avg_ms * 1e-3) / VALU_PEAK,
+                    "definition": "SQ_INSTS_VALU of the sorted-pipeline kernels of bounces >= 1 (as traffic_kernels) "
+                                  "per traced segment x segments per pipeline bounce / the pipeline bounce's time "
+                                  "(roofline.effective_launch_ms) / (256 CUs x 4 SIMDs x 2.4 GHz / 2)"}
         return out
     m = pmc.pick(res, kernel_prefix)
     if m is None or "bytes_per_launch" not in m:
