@@ -112,7 +112,9 @@ struct KArgs {
     PathSoA in, out;
     HitSoA hit;
     float* image;          // npix * 3 (AoS float3, tile-local)
-    v4f* colbuf;           // P (spp > 1): final path colour per slot, one 16-byte store
+    v4f* colbuf;           // P (spp > 1): final path colour per slot, one 16-byte store (retire)
+    uint32_t col_tag;      // this pass's tag in a colour slot's w: slots not written this pass hold a
+                           // zero colour (retire writes only nonzero colours; k_finalize_spp)
     Ctl* ctl;              // [2]
     uint64_t* status;      // [2][max_tiles] look-back words of k_compact_paths
     int32_t max_tiles;
@@ -1155,8 +1157,11 @@ __device__ __forceinline__ void retire(const KArgs& A, const PathReg& p) {
             px[1] += p.c.y;
             px[2] += p.c.z;
         }
-    } else {
-        A.colbuf[p.slot] = v4f{p.c.x, p.c.y, p.c.z, 0.0f};   // (scattered: plain, so L2 can merge neighbours)
+    } else if (p.c.x != 0.0f || p.c.y != 0.0f || p.c.z != 0.0f) {
+        // only nonzero colours are stored (~4% of Cornell's paths: the others miss the light), tagged
+        // with the pass; a slot whose tag is not the pass's holds a zero colour (k_finalize_spp)
+        // (scattered: plain, so L2 can merge neighbours)
+        A.colbuf[p.slot] = v4f{p.c.x, p.c.y, p.c.z, __uint_as_float(A.col_tag)};
     }
 }
 
@@ -2902,7 +2907,14 @@ __global__ __launch_bounds__(kBlock) void k_hist_apply(const int32_t* __restrict
 
 // spp > 1: add the per-slot colours in sample order (finalGather as `spp` sequential iterations).
 constexpr int kFinBatch = 16;
-__global__ void k_finalize_spp(float* __restrict__ image, const v4f* __restrict__ col, int npix, int spp) {
+// A slot's colour this pass: its stored colour when it carries the pass's tag, else zero (retire stored
+// nothing: the path's colour was zero).  Colours are never -0 (products and sums of non-negative
+// factors, or +0), so adding this +0 is what adding the zero colour did.
+__device__ __forceinline__ v4f slot_colour(const v4f& c, uint32_t tag) {
+    const bool ok = __float_as_uint(c[3]) == tag;
+    return v4f{ok ? c[0] : 0.0f, ok ? c[1] : 0.0f, ok ? c[2] : 0.0f, 0.0f};
+}
+__global__ void k_finalize_spp(float* __restrict__ image, const v4f* __restrict__ col, int npix, int spp, uint32_t tag) {
     for (int lp = blockIdx.x * blockDim.x + threadIdx.x; lp < npix; lp += gridDim.x * blockDim.x) {
         float r = image[3 * (size_t)lp], g = image[3 * (size_t)lp + 1], b = image[3 * (size_t)lp + 2];
         int s = 0;
@@ -2910,12 +2922,12 @@ __global__ void k_finalize_spp(float* __restrict__ image, const v4f* __restrict_
         for (; s + kFinBatch <= spp; s += kFinBatch) {
             v4f c[kFinBatch];
 #pragma unroll
-            for (int k = 0; k < kFinBatch; ++k) c[k] = PT_LD(col + (size_t)(s + k) * npix + lp);
+            for (int k = 0; k < kFinBatch; ++k) c[k] = slot_colour(PT_LD(col + (size_t)(s + k) * npix + lp), tag);
 #pragma unroll
             for (int k = 0; k < kFinBatch; ++k) { r += c[k][0]; g += c[k][1]; b += c[k][2]; }
         }
         for (; s < spp; ++s) {
-            const v4f c = PT_LD(col + (size_t)s * npix + lp);
+            const v4f c = slot_colour(PT_LD(col + (size_t)s * npix + lp), tag);
             r += c[0]; g += c[1]; b += c[2];
         }
         image[3 * (size_t)lp] = r; image[3 * (size_t)lp + 1] = g; image[3 * (size_t)lp + 2] = b;
@@ -2927,11 +2939,11 @@ __global__ void k_finalize_spp(float* __restrict__ image, const v4f* __restrict_
 // kept).  Emissive counts: `rows` bounces of `stride` per-workgroup slots.
 __global__ void k_ahead_settle(float* __restrict__ image, const v4f* __restrict__ col, int npix, DevStats* __restrict__ st,
                                DevStats* __restrict__ ast, unsigned long long* __restrict__ emit,
-                               unsigned long long* __restrict__ aemit, int nemit, int add) {
+                               unsigned long long* __restrict__ aemit, int nemit, int add, uint32_t tag) {
     const int gid = blockIdx.x * blockDim.x + threadIdx.x, gsz = gridDim.x * blockDim.x;
     if (add)
         for (int lp = gid; lp < npix; lp += gsz) {
-            const v4f c = PT_LD(col + lp);
+            const v4f c = slot_colour(PT_LD(col + lp), tag);
             image[3 * (size_t)lp] += c[0]; image[3 * (size_t)lp + 1] += c[1]; image[3 * (size_t)lp + 2] += c[2];
         }
     for (int j = gid; j < nemit; j += gsz) {
@@ -3128,6 +3140,8 @@ struct pt_ctx {
     bool ahead_recorded = false, ahead_valid = false;
     int32_t ahead_iter = 0;
     pt_flags ahead_flags{};
+    // colour-slot tags (KArgs::col_tag): one per batched or render-ahead pass, never 0 (the zeroed slots)
+    uint32_t col_tag = 0, ahead_tag = 0;
 
     ~pt_ctx() {
         g_busy_streams.fetch_sub(busy_streams);
@@ -4234,6 +4248,9 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
     if (sh.spp > 1) {
         if (int rc = c->alloc(&c->colbuf, 2 * (size_t)P)) return bail(rc);
         A.colbuf = c->colbuf;
+        // zero slots carry tag 0, which no pass uses (next_col_tag)
+        if ((e = hipMemset(c->colbuf, 0, 2 * (size_t)P * sizeof(v4f))) != hipSuccess)
+            return bail(pt::fail(PT_ERR_HIP, std::string("hipMemset: ") + hipGetErrorString(e)));
         if ((e = hipStreamCreateWithFlags(&c->fin_stream, hipStreamNonBlocking)) != hipSuccess)
             return bail(pt::fail(PT_ERR_HIP, std::string("hipStreamCreate: ") + hipGetErrorString(e)));
         for (int h = 0; h < 2; ++h)
@@ -4423,6 +4440,17 @@ int pt_ctx_counters(const pt_ctx* c, uint64_t* mask_builds, uint64_t* flag_syncs
 
 static int wait_finalize(pt_ctx* c, hipStream_t st);
 
+// The next colour-slot tag: a slot written by an earlier pass (or zeroed at allocation) never carries
+// it.  (After 2^32 - 1 passes the tags repeat: the slot buffers are cleared then.)
+static uint32_t next_col_tag(pt_ctx* c) {
+    if (++c->col_tag == 0u) {
+        c->col_tag = 1u;
+        if (c->colbuf) (void)hipMemset(c->colbuf, 0, 2 * (size_t)c->args.tile.P * sizeof(v4f));
+        if (c->ahead_col) (void)hipMemset(c->ahead_col, 0, (size_t)c->args.tile.P * sizeof(v4f));
+    }
+    return c->col_tag;
+}
+
 // One pass on st; ahead: a render-ahead pass (one-iteration context) whose colours and counts go to
 // the ahead buffers and that neither finalizes nor marks the context (pt_render_ahead).
 static int render_pass(pt_ctx* c, int32_t iter_first, hipStream_t st, bool ahead) {
@@ -4434,10 +4462,12 @@ static int render_pass(pt_ctx* c, int32_t iter_first, hipStream_t st, bool ahead
     const int mmode = mesh_mode(c);   // k_bounce's mesh mode (fused pipeline)
     int cur = 0;   // paths start in buf[0]
     const int h = c->col_half;
+    if (ahead || !spp1) A.col_tag = next_col_tag(c);
     if (ahead) {
         A.colbuf = c->ahead_col;
         A.stats = c->ahead_stats;
         A.emit_slots = c->ahead_emit;
+        c->ahead_tag = A.col_tag;
     } else if (!spp1) {
         A.colbuf = c->colbuf + (size_t)h * (size_t)A.tile.P;
         if (c->fin_out[h]) HIP_TRY(hipStreamWaitEvent(st, c->ev_fin[h], 0));   // pass p-2's finalize
@@ -4591,7 +4621,7 @@ static int render_pass(pt_ctx* c, int32_t iter_first, hipStream_t st, bool ahead
         HIP_TRY(hipEventRecord(c->ev_pass[h], st));
         HIP_TRY(hipStreamWaitEvent(c->fin_stream, c->ev_pass[h], 0));
         hipLaunchKernelGGL(k_finalize_spp, dim3(std::min((npix + 255) / 256, 4096)), dim3(256), 0, c->fin_stream,
-                           A.image, (const v4f*)A.colbuf, npix, A.tile.spp);
+                           A.image, (const v4f*)A.colbuf, npix, A.tile.spp, A.col_tag);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(c->ev_fin[h], c->fin_stream));
         c->fin_out[h] = true;
@@ -4607,7 +4637,7 @@ static int settle_ahead(pt_ctx* c, hipStream_t st, bool add) {
     const int nemit = std::min(c->depth, 64) * c->args.emit_stride;
     hipLaunchKernelGGL(k_ahead_settle, dim3(add ? std::min((npix + 255) / 256, 4096) : 64), dim3(256), 0, st,
                        c->args.image, (const v4f*)c->ahead_col, npix, c->stats, c->ahead_stats, c->args.emit_slots,
-                       c->ahead_emit, nemit, add ? 1 : 0);
+                       c->ahead_emit, nemit, add ? 1 : 0, c->ahead_tag);
     HIP_TRY(hipGetLastError());
     c->ahead_valid = false;
     return PT_OK;
@@ -4663,6 +4693,7 @@ static int render_ahead(pt_ctx* c, int32_t iter, hipStream_t st) {
         if (int rc = c->alloc(&c->ahead_col, (size_t)c->args.tile.P)) return rc;
         if (int rc = c->alloc(&c->ahead_stats, 1)) return rc;
         if (int rc = c->alloc(&c->ahead_emit, nemit)) return rc;
+        HIP_TRY(hipMemsetAsync(c->ahead_col, 0, (size_t)c->args.tile.P * sizeof(v4f), c->io_stream));
         HIP_TRY(hipMemsetAsync(c->ahead_stats, 0, sizeof(DevStats), c->io_stream));
         HIP_TRY(hipMemsetAsync(c->ahead_emit, 0, nemit * sizeof(unsigned long long), c->io_stream));
         HIP_TRY(hipStreamSynchronize(c->io_stream));
