@@ -113,8 +113,12 @@ struct KArgs {
     HitSoA hit;
     float* image;          // npix * 3 (AoS float3, tile-local)
     v4f* colbuf;           // P (spp > 1): final path colour per slot, one 16-byte store (retire)
-    uint32_t col_tag;      // this pass's tag in a colour slot's w: slots not written this pass hold a
-                           // zero colour (retire writes only nonzero colours; k_finalize_spp)
+    uint8_t* colflag;      // (spp > 1) one byte per slot, pixel-major: [pixel][iteration of the pass]; 1 when
+                           // retire stored a (nonzero) colour in the slot this pass — the others are zero colours,
+                           // which retire does not store; k_finalize_spp reads and clears them
+    int32_t col_spp;       // iterations of the pass (the flag row length), over all lanes
+    int32_t col_off;       // this lane's first iteration within the pass
+    float inv_npix;        // 1 / tile.npix (retire: a slot's iteration and pixel)
     Ctl* ctl;              // [2]
     uint64_t* status;      // [2][max_tiles] look-back words of k_compact_paths
     int32_t max_tiles;
@@ -1149,7 +1153,7 @@ __device__ __forceinline__ void store_path(const PathSoA& B, int i, const PathRe
 
 // A path that terminated this bounce: its colour is final (finalGather, pathtrace.cu:347-356).
 template <bool SPP1>
-__device__ __forceinline__ void retire(const KArgs& A, const PathReg& p) {
+__device__ __forceinline__ void retire(const KArgs& A, const PathReg& p, int it = -1) {
     if (SPP1) {
         if (p.c.x != 0.0f || p.c.y != 0.0f || p.c.z != 0.0f) {
             float* px = A.image + 3 * (size_t)p.slot;
@@ -1158,10 +1162,20 @@ __device__ __forceinline__ void retire(const KArgs& A, const PathReg& p) {
             px[2] += p.c.z;
         }
     } else if (p.c.x != 0.0f || p.c.y != 0.0f || p.c.z != 0.0f) {
-        // only nonzero colours are stored (~4% of Cornell's paths: the others miss the light), tagged
-        // with the pass; a slot whose tag is not the pass's holds a zero colour (k_finalize_spp)
+        // only nonzero colours are stored (~4% of Cornell's paths: the others miss the light), and
+        // flagged in the pass's pixel-major flag row; an unflagged slot is a zero colour (k_finalize_spp)
         // (scattered: plain, so L2 can merge neighbours)
-        A.colbuf[p.slot] = v4f{p.c.x, p.c.y, p.c.z, __uint_as_float(A.col_tag)};
+        A.colbuf[p.slot] = v4f{p.c.x, p.c.y, p.c.z, 0.0f};
+        // slot = it * npix + pixel within the lane: `it` is the caller's (its workgroup's or tile's
+        // iteration, uniform) or, when not known (< 0), derived from the slot
+        const int npix = A.tile.npix;
+        if (it < 0) {
+            it = (int)((float)p.slot * A.inv_npix);
+            if (p.slot - it * npix < 0) --it;
+            else if (p.slot - it * npix >= npix) ++it;
+        }
+        const int lp = p.slot - it * npix;
+        A.colflag[(size_t)lp * (size_t)A.col_spp + (size_t)(A.col_off + it)] = 1;
     }
 }
 
@@ -1269,7 +1283,7 @@ __global__ __launch_bounds__(kBlock) void k_trace(const KArgs A) {
                 store_survivor(A.in, i, p, FIRST);
             } else {
                 emitted = p.c.x != 0.0f || p.c.y != 0.0f || p.c.z != 0.0f;
-                retire<SPP1>(A, p);
+                retire<SPP1>(A, p, it);
             }
             A.flags[i] = alive ? 1 : 0;
         }
@@ -2154,7 +2168,7 @@ void k_bounce(const KArgs A) {
                     PathReg z;
                     z.c = F3(0.0f, 0.0f, 0.0f);
                     z.slot = i;
-                    retire<SPP1>(A, z);
+                    retire<SPP1>(A, z, my_it);
                 }
                 --k;
                 continue;
@@ -2173,7 +2187,7 @@ void k_bounce(const KArgs A) {
             if (i < last) {   // shade's miss exit: colour 0, retired (no record, no random number)
                 p.c = F3(0.0f, 0.0f, 0.0f);
                 p.slot = i;
-                retire<SPP1>(A, p);
+                retire<SPP1>(A, p, my_it);
             }
         } else if (i < last) {
             int q = i;   // physical index of the path (and of its k_traverse record)
@@ -2271,7 +2285,7 @@ void k_bounce(const KArgs A) {
                              : shade(A.S, A.fl, A.tile.depth, iter, key, p, h, A.S.mats, frames);
             if (!alive) {
                 emitted = p.c.x != 0.0f || p.c.y != 0.0f || p.c.z != 0.0f;
-                retire<SPP1>(A, p);
+                retire<SPP1>(A, p, my_it);
             }
         }
         emit_cnt += (uint32_t)__popcll(__ballot(emitted));
@@ -2592,7 +2606,7 @@ void k_sort_produce(const KArgs A, const SortArgs SA) {
                     PathReg z;
                     z.c = F3(0.0f, 0.0f, 0.0f);
                     z.slot = idx;
-                    retire<SPP1>(A, z);
+                    retire<SPP1>(A, z, it);
                 }
                 if (tid < nmats) {
                     const size_t e = sort_hidx(t0, t1, nmats, t, tid);
@@ -2670,7 +2684,7 @@ void k_sort_produce(const KArgs A, const SortArgs SA) {
                                  : shade_from(A.S, A.fl, A.tile.depth, iter, key, p, h, hitp, A.S.mats, frames);
                 if (!alive) {
                     emitted = p.c.x != 0.0f || p.c.y != 0.0f || p.c.z != 0.0f;
-                    retire<SPP1>(A, p);
+                    retire<SPP1>(A, p, it);
                 }
             }
             uint32_t gm = ~0u;
@@ -2745,7 +2759,7 @@ void k_sort_produce(const KArgs A, const SortArgs SA) {
                 PathReg e = p;
                 (void)(lds_mats ? shade_ends(h, s_mats, e) : shade_ends(h, A.S.mats, e));
                 em_next = e.c.x != 0.0f || e.c.y != 0.0f || e.c.z != 0.0f;
-                retire<SPP1>(A, e);
+                retire<SPP1>(A, e, it);
             } else {
                 const int q = t * kBlock + (int)(s_kbase[key] + kb2);
                 v4f* r = srec(A.out, q);
@@ -2907,28 +2921,38 @@ __global__ __launch_bounds__(kBlock) void k_hist_apply(const int32_t* __restrict
 
 // spp > 1: add the per-slot colours in sample order (finalGather as `spp` sequential iterations).
 constexpr int kFinBatch = 16;
-// A slot's colour this pass: its stored colour when it carries the pass's tag, else zero (retire stored
-// nothing: the path's colour was zero).  Colours are never -0 (products and sums of non-negative
-// factors, or +0), so adding this +0 is what adding the zero colour did.
-__device__ __forceinline__ v4f slot_colour(const v4f& c, uint32_t tag) {
-    const bool ok = __float_as_uint(c[3]) == tag;
-    return v4f{ok ? c[0] : 0.0f, ok ? c[1] : 0.0f, ok ? c[2] : 0.0f, 0.0f};
-}
-__global__ void k_finalize_spp(float* __restrict__ image, const v4f* __restrict__ col, int npix, int spp, uint32_t tag) {
+// finalGather of a batched pass: each pixel's colours added in sample order.  Only flagged slots hold
+// a colour (retire); the others are zero colours, whose additions are identities once the sum is not
+// -0 — colours are never -0 (products and sums of non-negative factors, or +0), so one +0 added first
+// (turning an accumulator of -0, which only pt_set_accum can give, into +0) and the flagged colours in
+// order give the bits that adding every slot's colour gave.  The flags are cleared for the next pass.
+__global__ void k_finalize_spp(float* __restrict__ image, const v4f* __restrict__ col, uint8_t* __restrict__ flag,
+                               int npix, int spp) {
     for (int lp = blockIdx.x * blockDim.x + threadIdx.x; lp < npix; lp += gridDim.x * blockDim.x) {
-        float r = image[3 * (size_t)lp], g = image[3 * (size_t)lp + 1], b = image[3 * (size_t)lp + 2];
+        float r = image[3 * (size_t)lp] + 0.0f, g = image[3 * (size_t)lp + 1] + 0.0f, b = image[3 * (size_t)lp + 2] + 0.0f;
+        uint8_t* row = flag + (size_t)lp * (size_t)spp;
         int s = 0;
-        // the loads of a batch of samples issued together (independent), the adds in sample order
-        for (; s + kFinBatch <= spp; s += kFinBatch) {
-            v4f c[kFinBatch];
+        if ((spp & 15) == 0 && (((size_t)row) & 15) == 0) {   // 16 flags per load (row starts 16-byte aligned)
+            for (; s < spp; s += 16) {
+                uint4 f = *reinterpret_cast<const uint4*>(row + s);
+                if ((f.x | f.y | f.z | f.w) == 0u) continue;
+                *reinterpret_cast<uint4*>(row + s) = make_uint4(0u, 0u, 0u, 0u);
+                const uint32_t w[4] = {f.x, f.y, f.z, f.w};
 #pragma unroll
-            for (int k = 0; k < kFinBatch; ++k) c[k] = slot_colour(PT_LD(col + (size_t)(s + k) * npix + lp), tag);
-#pragma unroll
-            for (int k = 0; k < kFinBatch; ++k) { r += c[k][0]; g += c[k][1]; b += c[k][2]; }
-        }
-        for (; s < spp; ++s) {
-            const v4f c = slot_colour(PT_LD(col + (size_t)s * npix + lp), tag);
-            r += c[0]; g += c[1]; b += c[2];
+                for (int q = 0; q < 4; ++q)
+                    for (uint32_t m = w[q]; m != 0u; m &= m - 1u) {   // flagged bytes (each holds 1) in sample order
+                        const int k = 4 * q + (__builtin_ctz(m) >> 3);
+                        const v4f c = PT_LD(col + (size_t)(s + k) * npix + lp);
+                        r += c[0]; g += c[1]; b += c[2];
+                    }
+            }
+        } else {
+            for (; s < spp; ++s)
+                if (row[s]) {
+                    row[s] = 0;
+                    const v4f c = PT_LD(col + (size_t)s * npix + lp);
+                    r += c[0]; g += c[1]; b += c[2];
+                }
         }
         image[3 * (size_t)lp] = r; image[3 * (size_t)lp + 1] = g; image[3 * (size_t)lp + 2] = b;
     }
@@ -2937,15 +2961,19 @@ __global__ void k_finalize_spp(float* __restrict__ image, const v4f* __restrict_
 // Render-ahead claim (add != 0: the iteration's colours into the image — k_finalize_spp with one
 // sample — and its counts into the context's) or drop (add == 0: the counts zeroed, device errors
 // kept).  Emissive counts: `rows` bounces of `stride` per-workgroup slots.
-__global__ void k_ahead_settle(float* __restrict__ image, const v4f* __restrict__ col, int npix, DevStats* __restrict__ st,
-                               DevStats* __restrict__ ast, unsigned long long* __restrict__ emit,
-                               unsigned long long* __restrict__ aemit, int nemit, int add, uint32_t tag) {
+__global__ void k_ahead_settle(float* __restrict__ image, const v4f* __restrict__ col, uint8_t* __restrict__ flag, int npix,
+                               DevStats* __restrict__ st, DevStats* __restrict__ ast, unsigned long long* __restrict__ emit,
+                               unsigned long long* __restrict__ aemit, int nemit, int add) {
     const int gid = blockIdx.x * blockDim.x + threadIdx.x, gsz = gridDim.x * blockDim.x;
-    if (add)
-        for (int lp = gid; lp < npix; lp += gsz) {
-            const v4f c = slot_colour(PT_LD(col + lp), tag);
+    for (int lp = gid; lp < npix; lp += gsz) {   // (a dropped iteration's flags are cleared too)
+        const bool f = flag[lp] != 0;
+        if (f) flag[lp] = 0;
+        if (add) {
+            // the flagged colour, else the zero colour retire did not store (k_finalize_spp)
+            const v4f c = f ? PT_LD(col + lp) : v4f{0.0f, 0.0f, 0.0f, 0.0f};
             image[3 * (size_t)lp] += c[0]; image[3 * (size_t)lp + 1] += c[1]; image[3 * (size_t)lp + 2] += c[2];
         }
+    }
     for (int j = gid; j < nemit; j += gsz) {
         const unsigned long long v = aemit[j];
         if (v) {
@@ -3140,8 +3168,8 @@ struct pt_ctx {
     bool ahead_recorded = false, ahead_valid = false;
     int32_t ahead_iter = 0;
     pt_flags ahead_flags{};
-    // colour-slot tags (KArgs::col_tag): one per batched or render-ahead pass, never 0 (the zeroed slots)
-    uint32_t col_tag = 0, ahead_tag = 0;
+    uint8_t* colflag = nullptr;   // 2 x P flag bytes (KArgs::colflag), pass halves like colbuf; zero between passes
+    uint8_t* ahead_flag = nullptr;   // npix flag bytes of the render-ahead colours
 
     ~pt_ctx() {
         g_busy_streams.fetch_sub(busy_streams);
@@ -4177,6 +4205,7 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
     A.cam.res[1] = H;
     A.tile = TileDev{W, sh.rank, sh.world, (int)npix, sh.spp, (int)P, S.depth, 1, 0};
     if ((double)npix * (double)W < 0x1p40) A.tile.wdiv = ((1ull << 40) + (uint64_t)W - 1) / (uint64_t)W;
+    A.inv_npix = 1.0f / (float)std::max<int64_t>((int64_t)npix, 1);   // (retire's estimate, corrected by one step)
 
     A.emit_stride = 256 * 8;   // >= any grid_trace (cus * 8) / grid_bounce
     // k_trace has no inter-workgroup dependency: 8 workgroups per CU, grid-stride beyond that.
@@ -4248,8 +4277,8 @@ int pt_create(const pt_scene* scene, const pt_flags* flags, const pt_shard* shar
     if (sh.spp > 1) {
         if (int rc = c->alloc(&c->colbuf, 2 * (size_t)P)) return bail(rc);
         A.colbuf = c->colbuf;
-        // zero slots carry tag 0, which no pass uses (next_col_tag)
-        if ((e = hipMemset(c->colbuf, 0, 2 * (size_t)P * sizeof(v4f))) != hipSuccess)
+        if (int rc = c->alloc(&c->colflag, 2 * (size_t)P)) return bail(rc);   // (every pass's finalize clears its half)
+        if ((e = hipMemset(c->colflag, 0, 2 * (size_t)P)) != hipSuccess)
             return bail(pt::fail(PT_ERR_HIP, std::string("hipMemset: ") + hipGetErrorString(e)));
         if ((e = hipStreamCreateWithFlags(&c->fin_stream, hipStreamNonBlocking)) != hipSuccess)
             return bail(pt::fail(PT_ERR_HIP, std::string("hipStreamCreate: ") + hipGetErrorString(e)));
@@ -4440,17 +4469,6 @@ int pt_ctx_counters(const pt_ctx* c, uint64_t* mask_builds, uint64_t* flag_syncs
 
 static int wait_finalize(pt_ctx* c, hipStream_t st);
 
-// The next colour-slot tag: a slot written by an earlier pass (or zeroed at allocation) never carries
-// it.  (After 2^32 - 1 passes the tags repeat: the slot buffers are cleared then.)
-static uint32_t next_col_tag(pt_ctx* c) {
-    if (++c->col_tag == 0u) {
-        c->col_tag = 1u;
-        if (c->colbuf) (void)hipMemset(c->colbuf, 0, 2 * (size_t)c->args.tile.P * sizeof(v4f));
-        if (c->ahead_col) (void)hipMemset(c->ahead_col, 0, (size_t)c->args.tile.P * sizeof(v4f));
-    }
-    return c->col_tag;
-}
-
 // One pass on st; ahead: a render-ahead pass (one-iteration context) whose colours and counts go to
 // the ahead buffers and that neither finalizes nor marks the context (pt_render_ahead).
 static int render_pass(pt_ctx* c, int32_t iter_first, hipStream_t st, bool ahead) {
@@ -4462,14 +4480,16 @@ static int render_pass(pt_ctx* c, int32_t iter_first, hipStream_t st, bool ahead
     const int mmode = mesh_mode(c);   // k_bounce's mesh mode (fused pipeline)
     int cur = 0;   // paths start in buf[0]
     const int h = c->col_half;
-    if (ahead || !spp1) A.col_tag = next_col_tag(c);
+    A.col_spp = A.tile.spp;
+    A.col_off = 0;
     if (ahead) {
         A.colbuf = c->ahead_col;
+        A.colflag = c->ahead_flag;
         A.stats = c->ahead_stats;
         A.emit_slots = c->ahead_emit;
-        c->ahead_tag = A.col_tag;
     } else if (!spp1) {
         A.colbuf = c->colbuf + (size_t)h * (size_t)A.tile.P;
+        A.colflag = c->colflag + (size_t)h * (size_t)A.tile.P;
         if (c->fin_out[h]) HIP_TRY(hipStreamWaitEvent(st, c->ev_fin[h], 0));   // pass p-2's finalize
     }
     const bool laned = (sorted || c->fused) && c->lanes >= 2 && !spp1 && !ahead;
@@ -4532,6 +4552,7 @@ static int render_pass(pt_ctx* c, int32_t iter_first, hipStream_t st, bool ahead
             L[l].tile.P = n_l * npix;
             L[l].tile.iter_first = iter_first + off;
             L[l].colbuf = A.colbuf + (size_t)off * (size_t)npix;
+            L[l].col_off = off;   // (the flag rows are the whole pass's, pixel-major)
             if (l > 0) {
                 L[l].ctl = c->lctl[l];
                 L[l].seg = c->lseg[l];
@@ -4621,7 +4642,7 @@ static int render_pass(pt_ctx* c, int32_t iter_first, hipStream_t st, bool ahead
         HIP_TRY(hipEventRecord(c->ev_pass[h], st));
         HIP_TRY(hipStreamWaitEvent(c->fin_stream, c->ev_pass[h], 0));
         hipLaunchKernelGGL(k_finalize_spp, dim3(std::min((npix + 255) / 256, 4096)), dim3(256), 0, c->fin_stream,
-                           A.image, (const v4f*)A.colbuf, npix, A.tile.spp, A.col_tag);
+                           A.image, (const v4f*)A.colbuf, A.colflag, npix, A.tile.spp);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(c->ev_fin[h], c->fin_stream));
         c->fin_out[h] = true;
@@ -4636,8 +4657,8 @@ static int settle_ahead(pt_ctx* c, hipStream_t st, bool add) {
     const int npix = c->args.tile.npix;
     const int nemit = std::min(c->depth, 64) * c->args.emit_stride;
     hipLaunchKernelGGL(k_ahead_settle, dim3(add ? std::min((npix + 255) / 256, 4096) : 64), dim3(256), 0, st,
-                       c->args.image, (const v4f*)c->ahead_col, npix, c->stats, c->ahead_stats, c->args.emit_slots,
-                       c->ahead_emit, nemit, add ? 1 : 0, c->ahead_tag);
+                       c->args.image, (const v4f*)c->ahead_col, c->ahead_flag, npix, c->stats, c->ahead_stats,
+                       c->args.emit_slots, c->ahead_emit, nemit, add ? 1 : 0);
     HIP_TRY(hipGetLastError());
     c->ahead_valid = false;
     return PT_OK;
@@ -4691,9 +4712,10 @@ static int render_ahead(pt_ctx* c, int32_t iter, hipStream_t st) {
     if (!c->ev_ahead) {   // first use: the ahead buffers
         const size_t nemit = (size_t)64 * c->args.emit_stride;
         if (int rc = c->alloc(&c->ahead_col, (size_t)c->args.tile.P)) return rc;
+        if (int rc = c->alloc(&c->ahead_flag, (size_t)c->args.tile.P)) return rc;
         if (int rc = c->alloc(&c->ahead_stats, 1)) return rc;
         if (int rc = c->alloc(&c->ahead_emit, nemit)) return rc;
-        HIP_TRY(hipMemsetAsync(c->ahead_col, 0, (size_t)c->args.tile.P * sizeof(v4f), c->io_stream));
+        HIP_TRY(hipMemsetAsync(c->ahead_flag, 0, (size_t)c->args.tile.P, c->io_stream));
         HIP_TRY(hipMemsetAsync(c->ahead_stats, 0, sizeof(DevStats), c->io_stream));
         HIP_TRY(hipMemsetAsync(c->ahead_emit, 0, nemit * sizeof(unsigned long long), c->io_stream));
         HIP_TRY(hipStreamSynchronize(c->io_stream));
