@@ -2078,7 +2078,8 @@ constexpr int kLaterWaves = 8; // (minimum waves per SIMD of the later-bounce ke
 // 8 waves (SGPRs capped) lost 0.3% in round 4; after round 5's code-size cuts (LDS-only tables, one
 // inlined exact test: 9,473 -> 5,408 ISA lines) they gain: Cornell +0.5%, config 4 +1.5%
 // (profiles/r05_later_waves8_ab.txt).
-constexpr int kFirstWaves = 1; // (minimum waves per SIMD of the analytic first-bounce kernels)
+constexpr int kFirstWaves = 8;   // (minimum waves per SIMD of the analytic first-bounce kernels: 8 caps them at 64
+                                 // VGPRs, one spilled; Cornell +1.8%, first bounce -11% per launch, profiles/r06_first_waves_ab.txt)
 template <bool FIRST, bool SPP1, int MESH>
 __global__ __launch_bounds__(kBlock, (MESH != 0 && MESH != kAnalyticSkip) ? 1 : (FIRST ? kFirstWaves : kLaterWaves))
 void k_bounce(const KArgs A) {
