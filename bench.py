@@ -30,7 +30,7 @@ in registers), the kernel's own minimum bytes (40 B in + 40 B per survivor + 24 
 path planes of 16 + 16 + 8 B) and the counters' traffic, each over effective_launch_ms.
 roofline.step_model_ratio = the §8d bytes of every bounce of a step / ms_per_step / 8 TB/s (a model
 ratio: above 1 it is flagged in model_ratios_above_1).  For the BVH walk also its memory
-instructions, L2 hit rate and, with the diagnostic counter build present (scripts/trav_build.sh), the
+instructions, L2 hit rate and, with the diagnostic counter build (build.py build_trav_stats), the
 walk's lane counters (scripts/trav_stats.py).
 The scan kernel is measured separately at n = 2^28 (8 B/element, 2 GiB, beyond the 256 MiB MALL).
 """
@@ -405,7 +405,7 @@ def _finalize_roofline(r: dict) -> None:
 
 
 def _walk_counters(scene_path, spp_pass, timeout=300) -> dict | None:
-    """The BVH walk's lane counters from the diagnostic build (scripts/trav_build.sh ->
+    """The BVH walk's lane counters from the diagnostic build (cuda_pathtracer_amd/build.py build_trav_stats ->
     cuda_pathtracer_amd/build/libpt_amd_trav.so; scripts/trav_stats.py), one pass of the same
     scene in a subprocess, or None when the diagnostic library is absent."""
     import subprocess

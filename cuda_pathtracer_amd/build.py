@@ -160,9 +160,31 @@ def build_test_hooks(verbose: bool = False, force: bool = False) -> Path:
     return TESTHOOKS_LIB
 
 
+TRAV_LIB = PKG / "build" / "libpt_amd_trav.so"
+
+
+def build_trav_stats(verbose: bool = False, force: bool = False) -> Path:
+    """Diagnostic library (not the product): pt_kernels.hip with the BVH walk's lane counters
+    (-DPT_TRAV_STATS), read by scripts/trav_stats.py for the bench's roofline.walk_counters.  Built
+    here so it always matches the product library's ABI."""
+    objdir = PKG / "build"
+    src = CSRC / "pt_kernels.hip"
+    obj = objdir / "pt_kernels_trav.o"
+    headers = list(CSRC.glob("*.h")) + list((ROOT / "include").glob("*.h"))
+    if force or _stale(obj, [src] + headers):
+        _run([HIPCC, "-x", "hip", f"--offload-arch={ARCH}", *COMMON, *EXTRA["pt_kernels.hip"], "-DPT_TRAV_STATS",
+              "-I", str(ROOT / "include"), "-c", str(src), "-o", str(obj)], verbose)
+    others = [objdir / (s + ".o") for s in DEVICE_SRCS + HOST_SRCS if s != "pt_kernels.hip"]
+    if force or _stale(TRAV_LIB, [obj] + others):
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(TRAV_LIB), str(obj),
+              *map(str, others), "-lz"], verbose)
+    return TRAV_LIB
+
+
 def build_all(verbose: bool = False, force: bool = False) -> None:
     build_native(verbose, force)
     build_test_hooks(verbose, force)
+    build_trav_stats(verbose, force)
     build_oracle(verbose, force)
     build_cpp_tests(verbose, force)
     build_pin(verbose, force)

@@ -1,5 +1,5 @@
 """BVH traversal counters of k_traverse / k_traverse4 (diagnostic library built with -DPT_TRAV_STATS,
-scripts/trav_build.sh): rays, interior fetches and triangle tests per ray, and how many lanes of
+cuda_pathtracer_amd/build.py build_trav_stats): rays, interior fetches and triangle tests per ray, and how many lanes of
 the wave do useful work.  Usage: trav_stats.py scene.json [spp] (PT_AMD_TRAV=pairs: round 2's walk).
 
 Definitions (one 'trip' = one iteration of the walk loop by one wave with at least one ray):
