@@ -4815,10 +4815,18 @@ int pt_stream_destroy(void* stream) {
     return PT_OK;
 }
 
+// The accumulator is loaded with every -0 replaced by +0.  The reference adds every iteration's colour
+// (zero or not) into every pixel, so after any pass its image holds no -0 (-0 + 0 = +0); the passes here
+// skip the additions of zero colours (retire, k_finalize_spp), which are identities on every value but -0.
+// A +0 loaded in place of -0 makes the two agree bit for bit from the first pass on.
 int pt_set_accum(pt_ctx* c, const float* host_rgb) {
     if (!c || !host_rgb) return pt::fail(PT_ERR_ARG, "null argument");
     if (int rc = wait_ctx(c)) return rc;
-    HIP_TRY(io_copy(c, c->args.image, host_rgb, (size_t)c->args.tile.npix * 3 * sizeof(float), hipMemcpyHostToDevice));
+    const size_t n = (size_t)c->args.tile.npix * 3;
+    std::vector<float> img(host_rgb, host_rgb + n);
+    for (float& v : img)
+        if (v == 0.0f) v = 0.0f;   // (-0 == 0: both zeros become +0)
+    HIP_TRY(io_copy(c, c->args.image, img.data(), n * sizeof(float), hipMemcpyHostToDevice));
     return PT_OK;
 }
 

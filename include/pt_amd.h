@@ -298,7 +298,8 @@ int pt_copy_image(pt_ctx* c, float* d_rgb, void* stream);   /* device-to-device 
 int pt_reset_image(pt_ctx* c, void* stream);
 /* Resume (extension; the reference has none): load a previously saved float accumulator of this
  * context's tile (npix x float3, as pt_get_accum returns it).  Continuing with the next iteration
- * indices reproduces an uninterrupted render bit for bit. */
+ * indices reproduces an uninterrupted render bit for bit.  Any -0 is loaded as +0 (the reference's
+ * image holds no -0 after a pass: every iteration adds a colour, zero or not, into every pixel). */
 int pt_set_accum(pt_ctx* c, const float* host_rgb);
 int pt_stats(pt_ctx* c, pt_stats_t* out);                   /* synchronises the context stream */
 /* The synchronous calls above (pt_get_image, pt_get_accum, pt_set_accum, pt_stats, and pt_set_flags

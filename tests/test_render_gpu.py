@@ -1261,3 +1261,29 @@ def test_lanes_capped_by_stream_budget(cornell_path, monkeypatch):
     ic = c.stream_info()
     assert ic["lanes"] == 2 and not ic["lanes_capped"] and ic["process_busy"] == base + 3, ic
     c.free()
+
+
+@pytest.mark.parametrize("spp", [1, 4])
+def test_signed_zero_accumulator_then_pass_bitexact(cornell_path, spp):
+    """Passes skip the additions of zero colours (retire stores only nonzero colours, k_finalize_spp adds
+    only flagged slots; the one-iteration path adds only nonzero colours into the image).  Those
+    additions are identities on every value but -0, so an accumulator loaded with -0, NaN and ordinary
+    values (pt_set_accum, the resume extension) then traced must equal the oracle, which adds every
+    iteration's colour into every pixel — bit for bit, the signs of zeros included."""
+    from cuda_pathtracer_amd import PathTracer
+    s, o = _pair(cornell_path, (40, 32))
+    rng = np.random.default_rng(7)
+    img = rng.random((32, 40, 3), dtype=np.float32)
+    img[::3] = np.float32(-0.0)
+    img[1::7, :, 1] = np.float32(0.0)
+    img[2, 5, :] = np.float32(np.nan)
+    pt = PathTracer(s, _gui(), spp=spp)
+    pt.set_image(img)
+    pt.render_pass(1)
+    got = pt.image()
+    pt.free()
+    ref, _ = O.render_pass(o, _oflags(_gui()), 1, spp=spp, image=img.copy())
+    g, r = got.view(np.uint32), ref.view(np.uint32)
+    same = (g == r) | (np.isnan(got) & np.isnan(ref))
+    assert same.all(), f"spp={spp}: {int((~same).sum())} values differ in bits (signed zeros included)"
+    assert np.signbit(got[np.asarray(got == 0)]).sum() == 0   # no -0 left after a pass
