@@ -1240,6 +1240,20 @@ __device__ __forceinline__ void store_survivor(const PathSoA& B, int i, const Pa
     B.c[i] = v2f{p.c.z, __int_as_float(p.slot)};
 }
 
+// A kernel parameter re-read from the kernarg segment (at byte `offset`: parameters are laid out in
+// order at their natural alignment) through a pointer the compiler cannot follow.  Used at the top of
+// a kernel's per-tile loop: the fields are then loaded (scalar loads) in each iteration where they are
+// used, instead of being hoisted to the kernel's start and kept live in SGPRs across the loop — at
+// 8 waves per SIMD (~80 SGPRs) those spilled to VGPR lanes, and every reload was a v_readlane on the
+// VALU (k_bounce<false, false, 0>: 75 SGPRs spilled -> 14, profiles/r06_kernel_resources.txt).
+template <class T>
+__device__ __forceinline__ const T& fresh_param(uint32_t offset) {
+    const char PT_CONST_AS* p = (const char PT_CONST_AS*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return *(const T*)(const T PT_CONST_AS*)(p + offset);
+}
+__device__ __forceinline__ const KArgs& fresh_args() { return fresh_param<KArgs>(0); }
+
 // Trace one bounce: [raygen] -> intersect -> shade, one path per lane, no barriers and no
 // inter-workgroup dependency (any grid size is correct).  Survivors are written back IN PLACE
 // and flagged; the stable compaction runs in k_compact_paths.  The RNG key of a path is its
@@ -1257,6 +1271,7 @@ __global__ __launch_bounds__(kBlock) void k_trace(const KArgs A) {
     count_bounce(A, N);
     uint32_t emit_cnt = 0;
     for (int base = blockIdx.x * kBlock; base < N; base += gridDim.x * kBlock) {
+        const KArgs& A = fresh_args();   // (shadows the parameter: its fields are re-read per tile)
         const int i = base + (int)threadIdx.x;
         bool emitted = false;
         if (i < N) {
@@ -2152,6 +2167,7 @@ void k_bounce(const KArgs A) {
     uint32_t kept = 0, emit_cnt = 0;
     int k = 0;
     for (int base = first; base < last; base += kBlock, ++k) {
+        const KArgs& A = fresh_args();   // (shadows the parameter: its fields are re-read per tile)
         const int i = base + tid;
         if (FIRST && (MESH == 0 || MESH == kAnalyticGM) && A.cmask) {
             // a tile whose four camera-mask blocks are all empty: every ray misses — shade's miss exit
@@ -2581,6 +2597,8 @@ void k_sort_produce(const KArgs A, const SortArgs SA) {
     uint32_t emit_cnt = 0, emit_next = 0;
     int k = 0, it = 0;
     for (int t = (int)blockIdx.x; t < T; t += (int)gridDim.x, ++k) {
+        const KArgs& A = fresh_args();   // (shadow the parameters: their fields are re-read per tile)
+        const SortArgs& SA = fresh_param<SortArgs>((sizeof(KArgs) + alignof(SortArgs) - 1) / alignof(SortArgs) * alignof(SortArgs));
         it = tile_iteration_next(s_tb, spp, t, it);
         const int t0 = __builtin_amdgcn_readfirstlane(s_tb[it]), t1 = __builtin_amdgcn_readfirstlane(s_tb[it + 1]);
         const int it_base = __builtin_amdgcn_readfirstlane(s_sb[it]);
