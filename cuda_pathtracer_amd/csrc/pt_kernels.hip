@@ -1241,7 +1241,9 @@ __device__ __forceinline__ void store_survivor(const PathSoA& B, int i, const Pa
 }
 
 // A kernel parameter re-read from the kernarg segment (at byte `offset`: parameters are laid out in
-// order at their natural alignment) through a pointer the compiler cannot follow.  Used at the top of
+// order at their natural alignment; tests/test_kernarg_layout_cpu.py checks the offsets the compiler
+// assigned) through a pointer the compiler cannot follow.  (Not through the parameter's own address:
+// taking it makes clang copy the parameter to private memory.)  Used at the top of
 // a kernel's per-tile loop: the fields are then loaded (scalar loads) in each iteration where they are
 // used, instead of being hoisted to the kernel's start and kept live in SGPRs across the loop — at
 // 8 waves per SIMD (~80 SGPRs) those spilled to VGPR lanes, and every reload was a v_readlane on the
