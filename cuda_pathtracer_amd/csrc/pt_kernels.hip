@@ -644,6 +644,13 @@ __device__ __forceinline__ uint32_t bound_wbox_tagged(const G& g, f3 o, f3 r, fl
 // order as their bits, so the pass keeps the three smallest with integer min / median operations,
 // and the index of a candidate is its low bits.  Bits >= +inf's (+inf, or a miss's tag with the
 // exponent ORed in: a NaN pattern, which every later comparison rejects) mean no candidate.
+// The median of three unsigned ints in one v_med3_u32 (the compiler keeps min(c, max(a, b)) as two
+// operations even when a <= c is known).
+__device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
 __device__ __forceinline__ uint32_t tag_bound(float v, uint32_t i) {
     const uint32_t b = (uint32_t)(max((int32_t)__float_as_uint(v), 32) - 32);
     return (b & ~31u) | i;
@@ -828,8 +835,8 @@ __device__ __forceinline__ Hit intersect_bounded(const SceneDev& S, const FlagsD
         // both are tested (the first hit's t is >= the tied bound), and the selection is order-independent.
         uint32_t u1 = 0x7f800000u, u2 = 0x7f800000u, u3 = 0x7f800000u;
         auto insert_tagged = [&](uint32_t t) {   // (medians: u1 <= u2 <= u3)
-            u3 = min(u3, max(u2, t));
-            u2 = min(u2, max(u1, t));
+            u3 = umed3(u2, t, u3);
+            u2 = umed3(u1, t, u2);
             u1 = min(u1, t);
         };
         auto insert = [&](float lo, int i) { insert_tagged(lo == kInf ? 0x7f800000u : tag_bound(lo, (uint32_t)i)); };
