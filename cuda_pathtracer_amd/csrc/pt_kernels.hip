@@ -620,7 +620,8 @@ __device__ __forceinline__ void stage_geoms(const SceneDev& S, LGeom* s_geoms) {
 // World-box cubes (bkind 3) in packed f32 operations: both planes of an axis, ((lo - o) * r,
 // (hi - o) * r), in one v_pk_add_f32 and one v_pk_mul_f32 (<2 x float> operations; IEEE per
 // component, the same bits as two subtractions and two multiplications), the box pair from the
-// geom's SGPRs (wbox).  The bound is bound_geom<3>'s (below) bit for bit, returned TAGGED (tag_bound).
+// geom's SGPRs (wbox).  The bound is bound_geom<3>'s (below) up to the rounding of its last step,
+// returned TAGGED (tag_bound).
 // With E0 = max(E, 0), "E > X || X < 0" is "E0 > X" (NaN slabs included: both are false for a NaN X,
 // and a NaN E gives E0 = 0).
 __device__ __forceinline__ uint32_t tag_bound(float v, uint32_t i);
@@ -631,14 +632,18 @@ __device__ __forceinline__ uint32_t bound_wbox_tagged(const G& g, f3 o, f3 r, fl
     const v2f tz = ((v2f){g.wbox[4], g.wbox[5]} - (v2f){o.z, o.z}) * (v2f){r.z, r.z};
     const float E0 = fmaxf(fmaxf(fminf(tx.x, tx.y), fminf(ty.x, ty.y)), fmaxf(fminf(tz.x, tz.y), 0.0f));
     const float X = fminf(fminf(fmaxf(tx.x, tx.y), fmaxf(ty.x, ty.y)), fmaxf(tz.x, tz.y));
-    const float v = fmaxf(E0 * rl - g.back, 0.0f) * g.tslack;
+    // one fma instead of a product and a difference: a single rounding, so no less a lower bound
+    // (tslack's 2^-14 and abs_slack cover both forms).  No clamp at 0: a negative v is a negative
+    // int, which tag_bound's integer max turns into the tag of +0, as the clamp did.  (v is never
+    // NaN: E0 is a maxNum chain that includes 0, rl is in (0.5, 2), back and tslack are finite.)
+    const float v = fmaf(E0, rl, -g.back) * g.tslack;
     // a miss ORs in the exponent of +inf: the result is then >= +inf's bits (no candidate) with no
     // branch around the tag, so the geom loop's scalar loads are not split by one
     return tag_bound(v, i) | (E0 > X ? 0x7f800000u : 0u);
 }
 
-// A bound v >= 0 (or +0 / -0) with geom index i in its low 5 bits, as the bits of a float that is
-// <= v: max(bits, 32) - 32 with the low 5 bits replaced by i (at most 32 ulp below v; +-0 become
+// A bound v >= 0 (or +0 / -0; a negative v counts as +0) with geom index i in its low 5 bits, as
+// the bits of a float that is <= v: max(bits, 32) - 32 (as signed ints) with the low 5 bits replaced by i (at most 32 ulp below v; +-0 become
 // the denormal i * 2^-149, which is below every later comparison's rounding: the scene's absolute
 // slack is subtracted before any use, and fl(tag - slack) = fl(0 - slack)).  Non-negative floats
 // order as their bits, so the pass keeps the three smallest with integer min / median operations,
