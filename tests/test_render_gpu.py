@@ -120,6 +120,60 @@ def test_materials_reflective_refractive():
     assert st["bounce_live"] == live
 
 
+def _coincident_scene():
+    """Geoms whose bounds and exact distances tie: three identical axis-aligned cubes (world-box
+    bounds) and two identical uniform spheres at the same place with different materials, a cube
+    sharing a face with another, and the walls.  The reference keeps the first geom of equal t
+    (`t < t_min`, pathtrace.cu:284-288), so a wrong tie-break changes the colours."""
+    from cuda_pathtracer_amd import CUBE, SPHERE, Scene
+    s, o = Scene(), O.OracleScene()
+    for sc in (s, o):
+        light = sc.add_material(rgb=(1, 1, 1), emittance=5.0)
+        white = sc.add_material(rgb=(0.98, 0.98, 0.98))
+        red = sc.add_material(rgb=(0.9, 0.2, 0.2))
+        green = sc.add_material(rgb=(0.2, 0.9, 0.2))
+        mirror = sc.add_material(rgb=(0.9, 0.9, 0.9), specrgb=(0.95, 0.95, 0.95), reflective=1.0)
+        sc.add_geom(CUBE, light, (0, 10, 0), (0, 0, 0), (3, 0.3, 3))
+        sc.add_geom(CUBE, white, (0, 0, 0), (0, 0, 0), (10, 0.01, 10))
+        sc.add_geom(CUBE, white, (0, 5, -5), (0, 90, 0), (0.01, 10, 10))
+        for m in (red, green, mirror):   # three coincident cubes
+            sc.add_geom(CUBE, m, (-2.5, 2, -1), (0, 0, 0), (2, 2, 2))
+        sc.add_geom(CUBE, green, (-0.5, 2, -1), (0, 0, 0), (2, 2, 2))   # shares the x = -1.5 face
+        for m in (mirror, red):   # two coincident spheres
+            sc.add_geom(SPHERE, m, (2.5, 3, 0), (0, 0, 0), (2.5, 2.5, 2.5))
+        sc.set_camera((64, 48), 45.0, (0, 5, 10.5), (0, 3, 0), (0, 1, 0))
+    s.set_render(4, 8, "tie")
+    s.finalize()
+    o.depth = 8
+    return s, o
+
+
+@pytest.mark.parametrize("kw", [dict(), dict(sortbyMaterial=True)])
+def test_coincident_geoms_tie_break_bitexact(kw):
+    """Exact ties between geoms (equal bounds, equal t): the bounded closest hit's tagged
+    candidates (equal bounds differ only in their index bits) and its order-independent selection
+    give the reference's first-geom choice — GPU == oracle bit for bit, fused and sorted."""
+    s, o = _coincident_scene()
+    g, r, st, live = _run(s, o, _gui(**kw), iters=3)
+    _assert_bitexact(g, r, f"coincident geoms {kw}")
+    assert st["bounce_live"] == live
+
+
+def test_coincident_geoms_bounded_equals_plain_loop(monkeypatch):
+    """The same scene under PT_AMD_VERIFY_BOUNDS=1: every ray's bounded hit equals the plain loop's."""
+    from cuda_pathtracer_amd import PathTracer
+    monkeypatch.setenv("PT_AMD_VERIFY_BOUNDS", "1")
+    monkeypatch.setenv("PT_PIPELINE", "split")
+    s, _ = _coincident_scene()
+    pt = PathTracer(s, _gui(), spp=8)
+    for k in range(2):
+        pt.render_pass(1 + 8 * k)
+    st = pt.stats()
+    pt.free()
+    assert st["bound_mismatch"] == 0
+    assert st["segments"] > 10_000
+
+
 @pytest.mark.parametrize("kw", [dict(), dict(sortbyMaterial=True)])
 def test_glass_cubes_total_internal_reflection(kw):
     """Rotated glass cubes (config 4's glass objects are cubes): rays inside a cube meet its faces
