@@ -731,6 +731,28 @@ __device__ __forceinline__ float bound_geom(const G& g, f3 ro, f3 rd, f3 invd, f
     return miss ? kInf : v;
 }
 
+// Uniformly scaled spheres (bkind 4) for the select-based pass, returned TAGGED like the world-box
+// cubes: bound_geom<4>'s bound with the per-geom transcendentals replaced by per-ray ones and host
+// constants — ia = rcp(|d|^2) * (1 / is2) (whi[1]) and the pull-back 1.0002e-4 / sqrt(|d|^2 is2) as
+// back (1.0002e-4 / sqrt(is2), rounded up) * rsq(|d|^2): a few ulp from the per-geom forms, inside
+// eps (2^-16 relative), the pull-back's 2e-4 margin and tslack — and no clamps at 0 (a negative
+// bound is tag_bound's +0; when the sphere is not missed, every term is finite or the bound is -inf).
+template <class G>
+__device__ __forceinline__ uint32_t bound_sphere_tagged(const G& g, f3 ro, f3 rd, float dd, float rl, float rinf,
+                                                       float rdd, float rsdd, uint32_t i) {
+    const f3 w = F3(ro.x - g.wlo[0], ro.y - g.wlo[1], ro.z - g.wlo[2]);
+    const float a = dd * g.whi[0];
+    const float b = dot(w, rd) * g.whi[0];
+    const float q2 = dot(w, w) * g.whi[0];
+    const bool departing = b > 0.0f && q2 - 0.25f > (q2 + 1.0f) * (g.kcs * rinf + g.kc3);
+    const float disc = b * b - a * (q2 - g.r2w);
+    const float sq = __builtin_amdgcn_sqrtf(disc), ia = rdd * g.whi[1];
+    const float eps = (fabsf(b) + sq) * ia * 0x1p-16f;
+    const bool miss = departing || disc < 0.0f || (sq - b) * ia < -eps;
+    const float v = (((-b - sq) * ia - eps) - g.back * rsdd) * rl * g.tslack;
+    return miss ? 0x7f800000u : tag_bound(v, i);
+}
+
 // Exact test of one geom from its LDS row: boxIntersectionTest (intersections.cu:3-58) and
 // sphereIntersectionTest (:60-115) with their common prologue (object-space ray) and epilogue
 // (pointOnRay, back-transform, world length) shared, so a wave whose lanes test different geom
@@ -847,8 +869,17 @@ __device__ __forceinline__ Hit intersect_bounded(const SceneDev& S, const FlagsD
         auto insert = [&](float lo, int i) { insert_tagged(lo == kInf ? 0x7f800000u : tag_bound(lo, (uint32_t)i)); };
         for (int j = S.bk[3]; j < S.bk[4]; ++j)   // world-box cubes: packed slabs
             if ((gmask >> B[j].orig) & 1u) insert_tagged(bound_wbox_tagged(B[j], ro, invd, rl, (uint32_t)B[j].orig));
-        for (int j = S.bk[4]; j < S.bk[5]; ++j)
-            if ((gmask >> B[j].orig) & 1u) insert(bound_geom<4, SEL>(B[j], ro, rd, invd, rl, rinf), B[j].orig);
+        if (SEL) {
+            if (S.bk[4] < S.bk[5]) {   // uniformly scaled spheres: per-ray reciprocals (bound_sphere_tagged)
+                const float dd = dot(rd, rd), rdd = __builtin_amdgcn_rcpf(dd), rsdd = __builtin_amdgcn_rsqf(dd);
+                for (int j = S.bk[4]; j < S.bk[5]; ++j)
+                    if ((gmask >> B[j].orig) & 1u)
+                        insert_tagged(bound_sphere_tagged(B[j], ro, rd, dd, rl, rinf, rdd, rsdd, (uint32_t)B[j].orig));
+            }
+        } else {
+            for (int j = S.bk[4]; j < S.bk[5]; ++j)
+                if ((gmask >> B[j].orig) & 1u) insert(bound_geom<4, SEL>(B[j], ro, rd, invd, rl, rinf), B[j].orig);
+        }
         for (int j = S.bk[1]; j < S.bk[2]; ++j)
             if ((gmask >> B[j].orig) & 1u) insert(bound_geom<1, SEL>(B[j], ro, rd, invd, rl, rinf), B[j].orig);
         for (int j = S.bk[2]; j < S.bk[3]; ++j)
@@ -3349,6 +3380,10 @@ void update_bounds(pt_ctx* c, float aperture) {
                 // 4 ulp of S_a assumed above): margins doubled
                 for (int k = 0; k < 3; ++k) d.wlo[k] = d.xf.c[3][k];
                 d.whi[0] = (float)s2;
+                // bound_sphere_tagged's per-geom constants: 1 / is2 and the pull-back factor
+                // 1.0002e-4 / sqrt(is2), rounded up (is2 as the device reads it, a float)
+                d.whi[1] = (float)(1.0 / (double)d.whi[0]);
+                d.back = std::nextafter((float)(1.0002e-4 / std::sqrt((double)d.whi[0])), HUGE_VALF);
                 d.r2w = (float)(0.25 + std::ldexp((smax + 1.0) * (smax + 1.0), -15));
                 d.kcs *= 2.0f;
                 d.kc3 *= 2.0f;
