@@ -166,7 +166,8 @@ struct DGeom {
     // wbox[2k], so one packed f32 operation (v_pk_add_f32 / v_pk_mul_f32, IEEE per component) takes
     // both planes of an axis from one SGPR pair (pt_kernels.hip slab2)
     float wbox[6];
-    float pad_[2];
+    float wback;   // bkind 3: back * SceneDev::wb_tslack rounded up (bound_wbox_tagged)
+    float pad_;
 };
 
 struct DMaterial {   // == pt_material

@@ -79,6 +79,7 @@ struct SceneDev {
     int32_t ngeoms, nmats, ntris, nnodes;
     int32_t bvh_depth;     // deepest interior node (root = 0): bounds the traversal stack
     float abs_slack;       // absolute slack of the world-distance lower bounds (bound_geom)
+    float wb_tslack;       // the smallest tslack of the world-box cubes (bound_wbox_tagged; DGeom::wback)
     const struct DPair* __restrict__ pairs;   // child-pair layout of the BVH (bvh_walk_pairs)
     int32_t root_code;     // code of the root (see DPair), meaningful when pairs != nullptr
     v4f root_lo, root_hi;  // root box
@@ -625,8 +626,10 @@ __device__ __forceinline__ void stage_geoms(const SceneDev& S, LGeom* s_geoms) {
 // With E0 = max(E, 0), "E > X || X < 0" is "E0 > X" (NaN slabs included: both are false for a NaN X,
 // and a NaN E gives E0 = 0).
 __device__ __forceinline__ uint32_t tag_bound(float v, uint32_t i);
+// rlt = rl * wb_tslack (per ray): v = E0 * rl * ts - back * ts with the smallest tslack of the world-box
+// cubes for every one of them (a smaller slack is still a slack) and wback = back * that, rounded up.
 template <class G>
-__device__ __forceinline__ uint32_t bound_wbox_tagged(const G& g, f3 o, f3 r, float rl, uint32_t i) {
+__device__ __forceinline__ uint32_t bound_wbox_tagged(const G& g, f3 o, f3 r, float rlt, uint32_t i) {
     const v2f tx = ((v2f){g.wbox[0], g.wbox[1]} - (v2f){o.x, o.x}) * (v2f){r.x, r.x};
     const v2f ty = ((v2f){g.wbox[2], g.wbox[3]} - (v2f){o.y, o.y}) * (v2f){r.y, r.y};
     const v2f tz = ((v2f){g.wbox[4], g.wbox[5]} - (v2f){o.z, o.z}) * (v2f){r.z, r.z};
@@ -636,7 +639,7 @@ __device__ __forceinline__ uint32_t bound_wbox_tagged(const G& g, f3 o, f3 r, fl
     // (tslack's 2^-14 and abs_slack cover both forms).  No clamp at 0: a negative v is a negative
     // int, which tag_bound's integer max turns into the tag of +0, as the clamp did.  (v is never
     // NaN: E0 is a maxNum chain that includes 0, rl is in (0.5, 2), back and tslack are finite.)
-    const float v = fmaf(E0, rl, -g.back) * g.tslack;
+    const float v = fmaf(E0, rlt, -g.wback);
     // a miss ORs in the exponent of +inf: the result is then >= +inf's bits (no candidate) with no
     // branch around the tag, so the geom loop's scalar loads are not split by one
     return tag_bound(v, i) | (E0 > X ? 0x7f800000u : 0u);
@@ -867,8 +870,9 @@ __device__ __forceinline__ Hit intersect_bounded(const SceneDev& S, const FlagsD
             u1 = min(u1, t);
         };
         auto insert = [&](float lo, int i) { insert_tagged(lo == kInf ? 0x7f800000u : tag_bound(lo, (uint32_t)i)); };
+        const float rlt = rl * S.wb_tslack;
         for (int j = S.bk[3]; j < S.bk[4]; ++j)   // world-box cubes: packed slabs
-            if ((gmask >> B[j].orig) & 1u) insert_tagged(bound_wbox_tagged(B[j], ro, invd, rl, (uint32_t)B[j].orig));
+            if ((gmask >> B[j].orig) & 1u) insert_tagged(bound_wbox_tagged(B[j], ro, invd, rlt, (uint32_t)B[j].orig));
         if (SEL) {
             if (S.bk[4] < S.bk[5]) {   // uniformly scaled spheres: per-ray reciprocals (bound_sphere_tagged)
                 const float dd = dot(rd, rd), rdd = __builtin_amdgcn_rcpf(dd), rsdd = __builtin_amdgcn_rsqf(dd);
@@ -3449,6 +3453,13 @@ void update_bounds(pt_ctx* c, float aperture) {
         d.tslack = (float)(1.0 - 4.0 * std::sqrt(dev) - std::ldexp(1.0, -14));
     }
     c->args.S.abs_slack = (float)std::ldexp(R + 1.0, -17);
+    // bound_wbox_tagged: one tslack for every world-box cube (their smallest), folded into the pull-back
+    float ts = 1.0f;
+    for (const DGeom& d : c->hgeoms)
+        if (d.bkind == 3) ts = std::min(ts, d.tslack);
+    c->args.S.wb_tslack = ts;
+    for (DGeom& d : c->hgeoms)
+        d.wback = d.bkind == 3 ? std::nextafter((float)((double)d.back * (double)ts), HUGE_VALF) : 0.0f;
 }
 
 // ---- first-bounce geom masks ----------------------------------------------------------------
