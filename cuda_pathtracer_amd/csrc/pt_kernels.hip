@@ -756,6 +756,27 @@ __device__ __forceinline__ uint32_t bound_sphere_tagged(const G& g, f3 ro, f3 rd
     return miss ? 0x7f800000u : tag_bound(v, i);
 }
 
+// Oriented cubes (bkind 1) for the select-based pass, returned TAGGED: bound_geom<1>'s slabs, with the
+// pull-back bounded per geom instead of per ray — back (update_bounds: 1.0002e-4 * ||inverse of the
+// linear part||_F, rounded up) * rsq(|d|^2) >= 1.0002e-4 / |qv| — so no |qv|^2 and no rsq per cube, and
+// no clamps at 0 (a negative bound is tag_bound's +0).
+template <class G>
+__device__ __forceinline__ uint32_t bound_obox_tagged(const G& g, f3 ro, f3 rd, float rl, float rsdd, uint32_t i) {
+    const f3 qo = xform_point(g.inv, ro);
+    const f3 qv = xform_vector(g.inv, rd);   // un-normalized: world parameter = object parameter
+    float E = -kInf, X = kInf;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float r = __builtin_amdgcn_rcpf(at(qv, k));
+        const float t1 = (g.slo[k] - at(qo, k)) * r, t2 = (g.shi[k] - at(qo, k)) * r;
+        E = fmaxf(E, fminf(t1, t2));
+        X = fminf(X, fmaxf(t1, t2));
+    }
+    const bool miss = E > X || X < 0.0f;
+    const float v = (E - g.back * rsdd) * rl * g.tslack;
+    return miss ? 0x7f800000u : tag_bound(v, i);
+}
+
 // Exact test of one geom from its LDS row: boxIntersectionTest (intersections.cu:3-58) and
 // sphereIntersectionTest (:60-115) with their common prologue (object-space ray) and epilogue
 // (pointOnRay, back-transform, world length) shared, so a wave whose lanes test different geom
@@ -874,18 +895,22 @@ __device__ __forceinline__ Hit intersect_bounded(const SceneDev& S, const FlagsD
         for (int j = S.bk[3]; j < S.bk[4]; ++j)   // world-box cubes: packed slabs
             if ((gmask >> B[j].orig) & 1u) insert_tagged(bound_wbox_tagged(B[j], ro, invd, rlt, (uint32_t)B[j].orig));
         if (SEL) {
-            if (S.bk[4] < S.bk[5]) {   // uniformly scaled spheres: per-ray reciprocals (bound_sphere_tagged)
+            const bool spheres = S.bk[4] < S.bk[5], oboxes = S.bk[1] < S.bk[2];
+            if (spheres || oboxes) {   // per-ray reciprocals (bound_sphere_tagged, bound_obox_tagged)
                 const float dd = dot(rd, rd), rdd = __builtin_amdgcn_rcpf(dd), rsdd = __builtin_amdgcn_rsqf(dd);
                 for (int j = S.bk[4]; j < S.bk[5]; ++j)
                     if ((gmask >> B[j].orig) & 1u)
                         insert_tagged(bound_sphere_tagged(B[j], ro, rd, dd, rl, rinf, rdd, rsdd, (uint32_t)B[j].orig));
+                for (int j = S.bk[1]; j < S.bk[2]; ++j)
+                    if ((gmask >> B[j].orig) & 1u)
+                        insert_tagged(bound_obox_tagged(B[j], ro, rd, rl, rsdd, (uint32_t)B[j].orig));
             }
         } else {
             for (int j = S.bk[4]; j < S.bk[5]; ++j)
                 if ((gmask >> B[j].orig) & 1u) insert(bound_geom<4, SEL>(B[j], ro, rd, invd, rl, rinf), B[j].orig);
+            for (int j = S.bk[1]; j < S.bk[2]; ++j)
+                if ((gmask >> B[j].orig) & 1u) insert(bound_geom<1, SEL>(B[j], ro, rd, invd, rl, rinf), B[j].orig);
         }
-        for (int j = S.bk[1]; j < S.bk[2]; ++j)
-            if ((gmask >> B[j].orig) & 1u) insert(bound_geom<1, SEL>(B[j], ro, rd, invd, rl, rinf), B[j].orig);
         for (int j = S.bk[2]; j < S.bk[3]; ++j)
             if ((gmask >> B[j].orig) & 1u) insert(bound_geom<2, SEL>(B[j], ro, rd, invd, rl, rinf), B[j].orig);
         g1 = u1 >= 0x7f800000u ? -1 : (int)(u1 & 31u);
@@ -3440,6 +3465,17 @@ void update_bounds(pt_ctx* c, float aperture) {
                     d.wbox[2 * r + 1] = d.whi[r];
                 }
                 d.bkind = 3;
+            } else {
+                // oriented cube (bkind 1): bound_obox_tagged's pull-back factor, 1.0002e-4 / sigma_min(L)
+                // bounded by the Frobenius norm of X = L^-1 (a singular L: +inf, the bound is then 0)
+                double fro = HUGE_VAL;
+                if (std::fabs(det) > 0.0) {   // (X is computed above exactly then)
+                    fro = 0.0;
+                    for (int r = 0; r < 3; ++r)
+                        for (int k = 0; k < 3; ++k) fro += X[r][k] * X[r][k];
+                }
+                d.back = std::isfinite(fro) ? std::nextafter((float)(1.0002e-4 * std::sqrt(fro) * (1.0 + 1e-5)), HUGE_VALF)
+                                            : HUGE_VALF;
             }
         }
         double dev = 0.0;   // Frobenius norm of xf_lin * inv_lin - I
