@@ -638,20 +638,13 @@ __device__ __forceinline__ uint32_t bound_wbox_tagged(const G& g, f3 o, f3 r, fl
     // one fma instead of a product and a difference: a single rounding, so no less a lower bound
     // (tslack's 2^-14 and abs_slack cover both forms).  No clamp at 0: a negative v is a negative
     // int, which tag_bound's integer max turns into the tag of +0, as the clamp did.  (v is never
-    // NaN: E0 is a maxNum chain that includes 0, rl is in (0.5, 2), back and tslack are finite.)
+    // NaN: E0 is a maxNum chain that includes 0, rlt is finite and positive, wback is finite.)
     const float v = fmaf(E0, rlt, -g.wback);
     // a miss ORs in the exponent of +inf: the result is then >= +inf's bits (no candidate) with no
     // branch around the tag, so the geom loop's scalar loads are not split by one
     return tag_bound(v, i) | (E0 > X ? 0x7f800000u : 0u);
 }
 
-// A bound v >= 0 (or +0 / -0; a negative v counts as +0) with geom index i in its low 5 bits, as
-// the bits of a float that is <= v: max(bits, 32) - 32 (as signed ints) with the low 5 bits replaced by i (at most 32 ulp below v; +-0 become
-// the denormal i * 2^-149, which is below every later comparison's rounding: the scene's absolute
-// slack is subtracted before any use, and fl(tag - slack) = fl(0 - slack)).  Non-negative floats
-// order as their bits, so the pass keeps the three smallest with integer min / median operations,
-// and the index of a candidate is its low bits.  Bits >= +inf's (+inf, or a miss's tag with the
-// exponent ORed in: a NaN pattern, which every later comparison rejects) mean no candidate.
 // The median of three unsigned ints in one v_med3_u32 (the compiler keeps min(c, max(a, b)) as two
 // operations even when a <= c is known).
 __device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
@@ -659,6 +652,14 @@ __device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
     asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
     return r;
 }
+// A bound v >= 0 (or +0 / -0; a negative v counts as +0) with geom index i in its low 5 bits, as
+// the bits of a float that is <= v: max(bits, 32) - 32 (as signed ints) with the low 5 bits
+// replaced by i (at most 32 ulp below v; +-0 become the denormal i * 2^-149, which is below every
+// later comparison's rounding: the scene's absolute slack is subtracted before any use, and
+// fl(tag - slack) = fl(0 - slack)).  Non-negative floats order as their bits, so the pass keeps the
+// three smallest with integer min / median operations, and the index of a candidate is its low
+// bits.  Bits >= +inf's (+inf, or a miss's tag with the exponent ORed in: a NaN pattern, which
+// every later comparison rejects) mean no candidate.
 __device__ __forceinline__ uint32_t tag_bound(float v, uint32_t i) {
     const uint32_t b = (uint32_t)(max((int32_t)__float_as_uint(v), 32) - 32);
     return (b & ~31u) | i;
